@@ -1,0 +1,238 @@
+"""Benchmark of the north-star path: chunked zero-phase low-pass + decimate
+(LFProc.process_time_range, lf_das.py:219-290) on MI355X.
+
+Workload (BASELINE.json configs[2], "cfg3"): 10,000 channels x 1 h @ 500 Hz
+float32 (72 GB, channel-major, DASCore dims ("distance","time")), 4th-order
+Butterworth at 0.45 Hz, decimate to 1 Hz, LFProc chunking P = 600, B = 7.
+One step = one pass of the hot path over the whole hour (7 overlapping chunks,
+3,585 outputs per channel), inputs resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C]
+
+N > 1 is launched by torch.distributed.run (one rank per GPU); channels shard
+across ranks with no data-path collective (weak scaling: every rank owns a
+10,000-channel spool).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "low-freq-real-time_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+
+def _args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--channels", type=int, default=10_000)
+    p.add_argument("--seconds", type=float, default=3600.0)
+    p.add_argument("--fs", type=float, default=500.0)
+    p.add_argument("--dt-out", type=float, default=1.0)
+    p.add_argument("--patch-size", type=int, default=600)
+    p.add_argument("--edge-buff", type=int, default=7)
+    p.add_argument("--cpu-channels", type=int, default=192,
+                   help="channels of the bounded CPU-baseline sample (full hour each)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-rolling", action="store_true")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="rocprofv3 PMC traffic summary (tools/pmc_summary.py) for roofline.traffic")
+    return p.parse_args()
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def synth_fill(x, fs, seed):
+    """x[c, t] = 0.5 + sin(2*pi*0.05*t/fs + phi_c) + N(0,1), generated on the
+    device in channel slices (synthetic; there is no dataset)."""
+    import torch
+    g = torch.Generator(device=x.device)
+    g.manual_seed(seed)
+    n_ch, n = x.shape
+    t = torch.arange(n, device=x.device, dtype=torch.float32) * (2 * np.pi * 0.05 / fs)
+    step = max(1, int(2e9 // (n * 4)))
+    for c0 in range(0, n_ch, step):
+        c1 = min(n_ch, c0 + step)
+        phi = torch.rand((c1 - c0, 1), device=x.device, generator=g) * (2 * np.pi)
+        blk = x[c0:c1]
+        torch.randn(blk.shape, device=x.device, generator=g, out=blk)
+        blk += torch.sin(t[None, :] + phi) + 0.5
+
+
+def build_plan(n_ch, n, fs, dt_out, P, B):
+    from lfdas import schedule as S
+    from lfdas.design import lowpass_sos
+    from lfdas.plan import LowpassPlan
+    dt_ns = int(round(1e9 / fs))
+    t0 = 1_505_692_800_000_000_000
+    tg = S.time_grid(t0, t0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    lo, w = S.grid_positions(t0, dt_ns, tg)
+    chunks = [(*S.select_range(t0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    sos = lowpass_sos(fs, 1 / dt_out / 2 * 0.9, 4)
+    return LowpassPlan(sos, n_ch, n, lo, w, chunks), sched, sos, t0, dt_ns, tg
+
+
+def cpu_baseline(args, sos, sched, t0, dt_ns, tg):
+    """Oracle C restatement of scipy's sosfiltfilt (+ interp) over the same
+    LFProc chunks, 1 process / 1 thread, on a bounded channel sample."""
+    sys.path.insert(0, ROOT)
+    import oracle
+    n = int(args.seconds * args.fs)
+    rng = np.random.default_rng(0)
+    n_c = args.cpu_channels
+    t = np.arange(n, dtype=np.float64) * (2 * np.pi * 0.05 / args.fs)
+    x = (rng.standard_normal((n_c, n)) + 0.5 + np.sin(t)[None, :]).astype(np.float32)
+    from lfdas import schedule as S
+    t_start = time.perf_counter()
+    for a, b, oa, ob in sched:
+        s0, s1 = S.select_range(t0, dt_ns, n, tg[a], tg[b])
+        y = oracle.sosfiltfilt_rows_c(sos, x[:, s0:s1 + 1])
+        tt = (np.arange(s0, s1 + 1, dtype=np.int64) * dt_ns).astype(np.float64)
+        oracle.interp1d_linear(tt, y, (tg[oa:ob] - t0).astype(np.float64))
+    el = time.perf_counter() - t_start
+    return {"value": n_c * n / el, "unit": "channel-samples/s", "cores": 1, "kind": "port",
+            "sample": f"{n_c} ch x {n} samples ({args.seconds:.0f} s @ {args.fs:.0f} Hz), same LFProc "
+                      f"chunks, oracle C sosfiltfilt + interp1d, 1 thread, {el:.1f} s"}
+
+
+def main():
+    args = _args()
+    import torch
+    ws, rank, local = _dist()
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if ws > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from lfdas.plan import set_timing
+    n_ch = args.channels
+    n = int(args.seconds * args.fs)
+    plan, sched, sos, t0, dt_ns, tg = build_plan(n_ch, n, args.fs, args.dt_out, args.patch_size,
+                                                 args.edge_buff)
+    x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
+    synth_fill(x, args.fs, 1234 + rank)
+    y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
+    wsb = plan.alloc_workspace(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            torch.distributed.barrier()
+
+    set_timing(True)
+    for _ in range(args.warmup):
+        plan.execute(x, y, wsb, stream)
+    barrier()
+    k1_ms = []
+    scan_ms = []
+    t_a = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute(x, y, wsb, stream)
+        a, b = plan.last_timing_ms()  # syncs on this step's events
+        k1_ms.append(a)
+        scan_ms.append(b)
+    barrier()
+    el = time.perf_counter() - t_a
+    set_timing(False)
+    if ws > 1:
+        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = float(tt.item())
+
+    R = int(round(args.fs * args.dt_out))
+    samples = n_ch * n * ws
+    value = samples * args.steps / el
+    k1 = float(np.mean(k1_ms))
+    alg_bytes = n_ch * n * (4.0 + 4.0 / R)
+    achieved = alg_bytes / (k1 * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(args.pmc) as f:
+            pm = json.load(f)
+        if pm.get("channels") == n_ch and pm.get("samples") == n:
+            traffic = pm.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    secondary = {}
+    if not args.no_rolling and rank == 0:
+        from lfdas.plan import rolling_mean_device
+        del x
+        torch.cuda.empty_cache()
+        xr = torch.empty((5000, 600_000), dtype=torch.float32, device=dev)
+        synth_fill(xr, 1000.0, 99)
+        for _ in range(2):
+            rolling_mean_device(xr, 1000, 1000)
+        torch.cuda.synchronize(dev)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        reps = 10
+        for _ in range(reps):
+            rolling_mean_device(xr, 1000, 1000)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        gbs = 5000 * 600_000 * (4 + 4 / 1000) / (ms * 1e-3) / 1e9
+        secondary["rolling_mean_cfg2"] = {
+            "value": 5000 * 600_000 / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms,
+            "config": "5,000 ch x 10 min @ 1 kHz fp32, W = S = 1000",
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS}}
+        del xr
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(args, sos, sched, t0, dt_ns, tg)
+
+    if rank == 0:
+        out = {
+            "metric": "channel-samples/s low-pass+decimate",
+            "value": value,
+            "unit": "channel-samples/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (0.5 + sin + N(0,1), generated on device)",
+            "config": {"workload": "cfg3: 10,000 ch x 1 h @ 500 Hz fp32 (72 GB) per GPU, 4th-order "
+                                   "Butterworth 0.45 Hz zero-phase, decimate to 1 Hz, LFProc P=600 B=7",
+                       "channels_per_gpu": n_ch, "samples": n, "fs": args.fs, "dt_out": args.dt_out,
+                       "chunks": len(sched), "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),
+                       "parallelism": f"channel-shard x{ws}", "io_dtype": "f32"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_block_functionals", "kernel_ms": k1,
+                         "scan_kernel_ms": float(np.mean(scan_ms))},
+            "cpu_baseline": cpu,
+            "secondary": secondary,
+        }
+        print(json.dumps(out))
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,594 @@
+// C-ABI of liblfdas.so (include/lfdas.h): plan construction (host math in
+// x87 extended precision), workspace layout and kernel sequencing.
+//
+// The per-chunk semantics replicate scipy.signal.sosfiltfilt with odd padding
+// (scipy/signal/_signaltools.py:4718-4828) followed by linear interp1d at the
+// chunk's output grid (scipy/interpolate/_interpolate.py:457-484), as DASCore's
+// Patch.pass_filter(...).interpolate(...) does at lf_das.py:223-225, for every
+// chunk of LFProc.process_time_range (lf_das.py:252-290).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lfdas.h"
+#include "lfd_internal.h"
+
+using lfd::MAX_N;
+using lfd::MAX_SEC;
+
+namespace {
+
+thread_local std::string g_err;
+std::atomic<int> g_timing{0};
+
+int fail(int code, const std::string &m) {
+  g_err = m;
+  return code;
+}
+
+#define LFD_HIP(call)                                                      \
+  do {                                                                     \
+    hipError_t e_ = (call);                                                \
+    if (e_ != hipSuccess)                                                  \
+      return fail(LFD_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+typedef long double R;
+
+struct Cascade {
+  int ns = 0;
+  double b0[MAX_SEC], b1[MAX_SEC], b2[MAX_SEC], a1[MAX_SEC], a2[MAX_SEC];
+};
+
+// scipy/signal/_filter_design.py:728 `_validate_sos`: shape (n, 6), a0 == 1.
+int load_sos(const double *sos, int n_sec, Cascade &c) {
+  if (!sos) return fail(LFD_EINVAL, "sos is NULL");
+  if (n_sec < 1 || n_sec > MAX_SEC)
+    return fail(LFD_EINVAL, "n_sec must be in [1, " + std::to_string(MAX_SEC) + "]");
+  c.ns = n_sec;
+  for (int s = 0; s < n_sec; ++s) {
+    const double *r = sos + 6 * s;
+    for (int i = 0; i < 6; ++i)
+      if (!std::isfinite(r[i])) return fail(LFD_EINVAL, "sos has non-finite coefficients");
+    if (r[3] != 1.0) return fail(LFD_EINVAL, "sos[:, 3] should be all ones");
+    c.b0[s] = r[0];
+    c.b1[s] = r[1];
+    c.b2[s] = r[2];
+    c.a1[s] = r[4];
+    c.a2[s] = r[5];
+  }
+  return LFD_OK;
+}
+
+// scipy/signal/_signaltools.py:4811-4813
+int default_padlen(const Cascade &c) {
+  int nb2 = 0, na2 = 0;
+  for (int s = 0; s < c.ns; ++s) {
+    nb2 += c.b2[s] == 0.0;
+    na2 += c.a2[s] == 0.0;
+  }
+  return 3 * (2 * c.ns + 1 - std::min(nb2, na2));
+}
+
+// scipy/signal/_signaltools.py:4103-4175 (sosfilt_zi) with lfilter_zi's 2x2
+// solve of (I - companion(a).T) zi = b[1:] - a[1:] b0.
+void sosfilt_zi(const Cascade &c, double *zi) {
+  R scale = 1.0L;
+  for (int s = 0; s < c.ns; ++s) {
+    const R b0 = c.b0[s], b1 = c.b1[s], b2 = c.b2[s], a1 = c.a1[s], a2 = c.a2[s];
+    const R r0 = b1 - a1 * b0, r1 = b2 - a2 * b0;
+    const R det = (1.0L + a1) + a2;
+    const R z0 = (r0 + r1) / det;
+    const R z1 = ((1.0L + a1) * r1 - a2 * r0) / det;
+    zi[2 * s] = (double)(scale * z0);
+    zi[2 * s + 1] = (double)(scale * z1);
+    scale *= (b0 + b1 + b2) / ((1.0L + a1) + a2);
+  }
+}
+
+// One TDF-II cascade step in extended precision (same state layout as the
+// device and as SciPy's zi: [z_s0, z_s1] per section).
+R step(const Cascade &c, R *z, R x) {
+  for (int s = 0; s < c.ns; ++s) {
+    const R v = c.b0[s] * x + z[2 * s];
+    z[2 * s] = c.b1[s] * x - c.a1[s] * v + z[2 * s + 1];
+    z[2 * s + 1] = c.b2[s] * x - c.a2[s] * v;
+    x = v;
+  }
+  return x;
+}
+
+struct Mat {
+  int n;
+  R a[MAX_N][MAX_N];
+  explicit Mat(int n_ = 0) : n(n_) {
+    for (int i = 0; i < MAX_N; ++i)
+      for (int j = 0; j < MAX_N; ++j) a[i][j] = 0;
+  }
+  static Mat eye(int n) {
+    Mat m(n);
+    for (int i = 0; i < n; ++i) m.a[i][i] = 1;
+    return m;
+  }
+  Mat operator*(const Mat &o) const {
+    Mat r(n);
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < n; ++k)
+        for (int j = 0; j < n; ++j) r.a[i][j] += a[i][k] * o.a[k][j];
+    return r;
+  }
+};
+
+Mat mpow(const Mat &A, int64_t e) {
+  Mat r = Mat::eye(A.n), b = A;
+  while (e > 0) {
+    if (e & 1) r = r * b;
+    b = b * b;
+    e >>= 1;
+  }
+  return r;
+}
+
+bool minv(const Mat &A, Mat &out) {
+  const int n = A.n;
+  R w[MAX_N][2 * MAX_N];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 2 * n; ++j) w[i][j] = j < n ? A.a[i][j] : (j - n == i);
+  for (int col = 0; col < n; ++col) {
+    int p = col;
+    for (int i = col + 1; i < n; ++i)
+      if (std::fabs(w[i][col]) > std::fabs(w[p][col])) p = i;
+    if (w[p][col] == 0) return false;
+    for (int j = 0; j < 2 * n; ++j) std::swap(w[p][j], w[col][j]);
+    const R d = w[col][col];
+    for (int j = 0; j < 2 * n; ++j) w[col][j] /= d;
+    for (int i = 0; i < n; ++i)
+      if (i != col) {
+        const R f = w[i][col];
+        for (int j = 0; j < 2 * n; ++j) w[i][j] -= f * w[col][j];
+      }
+  }
+  out = Mat(n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) out.a[i][j] = w[i][j + n];
+  return true;
+}
+
+struct StateSpace {
+  Mat A, Ainv;
+  R B[MAX_N], C[MAX_N], D;
+};
+
+int state_space(const Cascade &c, StateSpace &ss) {
+  const int n = 2 * c.ns;
+  ss.A = Mat(n);
+  R z[MAX_N];
+  for (int j = 0; j < n; ++j) {
+    for (int i = 0; i < n; ++i) z[i] = (i == j);
+    ss.C[j] = step(c, z, 0);
+    for (int i = 0; i < n; ++i) ss.A.a[i][j] = z[i];
+  }
+  for (int i = 0; i < n; ++i) z[i] = 0;
+  ss.D = step(c, z, 1);
+  for (int i = 0; i < n; ++i) ss.B[i] = z[i];
+  if (!minv(ss.A, ss.Ainv))
+    return fail(LFD_EUNSUPPORTED, "singular TDF-II transition (a section has a2 == 0)");
+  return LFD_OK;
+}
+
+// Fill the block-functional and scan constants for block length L.
+int block_constants(const Cascade &c, int L, lfd::BlockConst &kc, lfd::ScanConst &sc) {
+  const int n = 2 * c.ns;
+  StateSpace ss;
+  if (int e = state_space(c, ss)) return e;
+  std::memset(&kc, 0, sizeof(kc));
+  std::memset(&sc, 0, sizeof(sc));
+  for (int s = 0; s < c.ns; ++s) {
+    kc.f.b0[s] = sc.f.b0[s] = c.b0[s];
+    kc.f.b1[s] = sc.f.b1[s] = c.b1[s];
+    kc.f.b2[s] = sc.f.b2[s] = c.b2[s];
+    kc.f.a1[s] = sc.f.a1[s] = c.a1[s];
+    kc.f.a2[s] = sc.f.a2[s] = c.a2[s];
+    kc.ia2[s] = (double)(1.0L / (R)c.a2[s]);
+    kc.ra[s] = (double)((R)c.a1[s] / (R)c.a2[s]);
+    kc.beta0[s] = (double)((R)c.b1[s] - (R)c.a1[s] * c.b0[s]);
+    kc.beta1[s] = (double)((R)c.b2[s] - (R)c.a2[s] * c.b0[s]);
+  }
+  for (int i = 0; i < n; ++i) kc.Bv[i] = (double)ss.B[i];
+  const Mat T = mpow(ss.A, L - 1);
+  const Mat TL2 = mpow(ss.A, L - 2);
+  const Mat Phi = T * ss.A;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      kc.T[i * MAX_N + j] = (double)T.a[i][j];
+      sc.Phi[i * MAX_N + j] = (double)Phi.a[i][j];
+    }
+  R cAinvB = 0;
+  for (int j = 0; j < n; ++j) {
+    R a = 0, h = 0;
+    for (int i = 0; i < n; ++i) {
+      a += ss.C[i] * TL2.a[i][j];
+      h += ss.C[i] * T.a[i][j];
+    }
+    kc.cp[j] = (double)a;
+    sc.H0[j] = (double)h;
+    R t = 0;
+    for (int i = 0; i < n; ++i) t += ss.Ainv.a[j][i] * ss.B[i];
+    cAinvB += ss.C[j] * t;
+  }
+  kc.d0 = (double)(ss.D - cAinvB);
+  // M and G0 by simulating forward-from-e_j then reverse-from-zero.
+  std::vector<R> yf(L);
+  for (int j = 0; j < n; ++j) {
+    R z[MAX_N], r[MAX_N];
+    for (int i = 0; i < n; ++i) {
+      z[i] = (i == j);
+      r[i] = 0;
+    }
+    for (int m = 0; m < L; ++m) yf[m] = step(c, z, 0);
+    R out0 = 0;
+    for (int m = L - 1; m >= 0; --m) out0 = step(c, r, yf[m]);
+    for (int i = 0; i < n; ++i) sc.M[i * MAX_N + j] = (double)r[i];
+    sc.G0[j] = (double)out0;
+  }
+  double zi[MAX_N];
+  sosfilt_zi(c, zi);
+  for (int i = 0; i < n; ++i) sc.zi[i] = zi[i];
+  return LFD_OK;
+}
+
+inline int64_t floor_div(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+inline int64_t ceil_div(int64_t a, int64_t b) { return -floor_div(-a, b); }
+inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct lfd_lowpass_plan {
+  int device = 0;
+  int n_sec = 0, padlen = 0;
+  int64_t n_ch = 0, n_t = 0, n_grid = 0, n_chunks = 0;
+  lfd::BlockGeom bg{};
+  lfd::BlockConst kc{};
+  lfd::ScanConst sc{};
+  std::vector<lfd::ChunkGeom> chunks;
+  lfd::ChunkGeom *d_chunks = nullptr;
+  int64_t sf_blocks = 0, tp_len = 0;
+  size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  mutable bool timed = false;
+};
+
+extern "C" {
+
+const char *lfd_last_error(void) { return g_err.c_str(); }
+int lfd_version(void) { return 100; }
+
+int lfd_device_count(int *count) {
+  if (!count) return fail(LFD_EINVAL, "count is NULL");
+  LFD_HIP(hipGetDeviceCount(count));
+  return LFD_OK;
+}
+
+int lfd_set_timing(int enable) {
+  g_timing.store(enable ? 1 : 0);
+  return LFD_OK;
+}
+
+int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec,
+                            int padlen, int64_t n_ch, int64_t n_t,
+                            const int64_t *grid_lo, const double *grid_w,
+                            int64_t n_grid, const lfd_chunk *chunks,
+                            int64_t n_chunks) {
+  if (!out) return fail(LFD_EINVAL, "plan out-pointer is NULL");
+  *out = nullptr;
+  Cascade c;
+  if (int e = load_sos(sos, n_sec, c)) return e;
+  if (padlen < 0) padlen = default_padlen(c);
+  if (n_ch < 1 || n_t < 1) return fail(LFD_EINVAL, "n_ch and n_t must be >= 1");
+  if (n_grid < 2 || !grid_lo || !grid_w)
+    return fail(LFD_EUNSUPPORTED, "block plan needs a uniform grid of >= 2 points");
+  if (n_chunks < 1 || !chunks) return fail(LFD_EINVAL, "no chunks");
+  const int64_t Rg = grid_lo[1] - grid_lo[0];
+  for (int64_t j = 0; j < n_grid; ++j) {
+    if (grid_w[j] != 0.0)
+      return fail(LFD_EUNSUPPORTED, "grid points between samples need the general path");
+    if (j > 0 && grid_lo[j] - grid_lo[j - 1] != Rg)
+      return fail(LFD_EUNSUPPORTED, "non-uniform grid spacing needs the general path");
+  }
+  if (Rg < 2 || Rg > (int64_t)1 << 30)
+    return fail(LFD_EUNSUPPORTED, "grid spacing must be in [2, 2^30] samples");
+  const int L = (int)Rg;
+  const int64_t base0 = ((grid_lo[0] % L) + L) % L;
+
+  auto *p = new lfd_lowpass_plan();
+  p->n_sec = n_sec;
+  p->padlen = padlen;
+  p->n_ch = n_ch;
+  p->n_t = n_t;
+  p->n_grid = n_grid;
+  p->n_chunks = n_chunks;
+  int64_t kmin = INT64_MAX, kmax = INT64_MIN;
+  p->chunks.resize(n_chunks);
+  for (int64_t ci = 0; ci < n_chunks; ++ci) {
+    const lfd_chunk &ch = chunks[ci];
+    lfd::ChunkGeom &G = p->chunks[ci];
+    auto bad = [&](int code, const std::string &m) {
+      delete p;
+      return fail(code, "chunk " + std::to_string(ci) + ": " + m);
+    };
+    if (ch.s0 < 0 || ch.s1 >= n_t || ch.s1 < ch.s0) return bad(LFD_EINVAL, "sample range outside the array");
+    if (ch.s1 - ch.s0 + 1 <= padlen)
+      return bad(LFD_EINVAL, "The length of the input vector x must be greater than padlen, which is " +
+                                 std::to_string(padlen) + ".");
+    if (ch.g0 < 0 || ch.g1 > n_grid || ch.g1 < ch.g0) return bad(LFD_EINVAL, "grid range outside the grid");
+    G.s0 = ch.s0;
+    G.s1 = ch.s1;
+    G.kb = ceil_div(ch.s0 - base0, L);
+    G.ke = floor_div(ch.s1 + 1 - base0, L);
+    if (G.ke <= G.kb) return bad(LFD_EUNSUPPORTED, "chunk holds no full block");
+    G.head_end = base0 + G.kb * L;
+    G.tail_begin = base0 + G.ke * L;
+    G.head_out_j = G.tail_out_j = -1;
+    G.head_out_pos = G.tail_out_pos = -1;
+    G.kout0 = G.kout1 = G.kb;
+    G.jout0 = 0;
+    bool any_block = false;
+    for (int64_t j = ch.g0; j < ch.g1; ++j) {
+      const int64_t pos = grid_lo[j];
+      if (pos < ch.s0 || pos > ch.s1) return bad(LFD_EINVAL, "output grid point outside the chunk");
+      const int64_t kj = (pos - base0) / L;
+      if (kj >= G.kb && kj < G.ke) {
+        if (!any_block) {
+          G.kout0 = kj;
+          G.jout0 = j;
+          any_block = true;
+        }
+        G.kout1 = kj + 1;
+      } else if (pos < G.head_end) {
+        G.head_out_pos = pos;
+        G.head_out_j = j;
+      } else {
+        G.tail_out_pos = pos;
+        G.tail_out_j = j;
+      }
+    }
+    kmin = std::min(kmin, G.kb);
+    kmax = std::max(kmax, G.ke);
+    const int64_t nhead = G.head_end - G.s0, ntail = G.s1 + 1 - G.tail_begin;
+    p->tp_len = std::max(p->tp_len, nhead + ntail + padlen);
+  }
+  // shift block indices so the plan's blocks are [0, nb)
+  int64_t sf = 0;
+  for (auto &G : p->chunks) {
+    G.kb -= kmin;
+    G.ke -= kmin;
+    G.kout0 -= kmin;
+    G.kout1 -= kmin;
+    G.sf_off = sf;
+    sf += G.ke - G.kb;
+  }
+  p->sf_blocks = sf;
+  const int n = 2 * n_sec;
+  p->bg.n_ch = n_ch;
+  p->bg.nb = kmax - kmin;
+  p->bg.base = base0 + kmin * L;
+  p->bg.L = L;
+  p->bg.nF = 2 * n + 1;
+  if (int e = block_constants(c, L, p->kc, p->sc)) {
+    delete p;
+    return e;
+  }
+  p->off_F = 0;
+  p->off_SF = align256(p->off_F + sizeof(double) * (size_t)p->bg.nF * p->bg.nb * n_ch);
+  p->off_TP = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * n_ch);
+  p->ws_bytes = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);
+  // Device state.  Without a visible device the plan stays host-only (its
+  // geometry and constants can still be inspected); execute then fails.
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    (void)hipGetLastError();
+    p->device = -1;
+    *out = p;
+    return LFD_OK;
+  }
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess) e = hipMalloc(&p->d_chunks, sizeof(lfd::ChunkGeom) * n_chunks);
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_chunks, p->chunks.data(), sizeof(lfd::ChunkGeom) * n_chunks,
+                  hipMemcpyHostToDevice);
+  for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
+  if (e != hipSuccess) {
+    lfd_lowpass_plan_destroy(p);
+    return fail(LFD_EHIP, std::string("plan allocation: ") + hipGetErrorString(e));
+  }
+  *out = p;
+  return LFD_OK;
+}
+
+int lfd_lowpass_plan_info(const lfd_lowpass_plan *p, size_t *ws, int64_t *nb, int64_t *L) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (ws) *ws = p->ws_bytes;
+  if (nb) *nb = p->bg.nb;
+  if (L) *L = p->bg.L;
+  return LFD_OK;
+}
+
+int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
+                        int64_t s_t, float *y, int64_t ys_ch, int64_t ys_t,
+                        void *workspace, void *stream) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (!x || !y || !workspace) return fail(LFD_EINVAL, "x, y and workspace must be device pointers");
+  if (s_t == 0 || (p->n_ch > 1 && s_ch == 0)) return fail(LFD_EINVAL, "zero stride");
+  if (p->device < 0 || !p->d_chunks) return fail(LFD_EINVAL, "plan has no device state (created without a GPU)");
+  int dev = -1;
+  LFD_HIP(hipGetDevice(&dev));
+  if (dev != p->device) return fail(LFD_EINVAL, "plan was created on another device");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  char *ws = static_cast<char *>(workspace);
+  double *F = reinterpret_cast<double *>(ws + p->off_F);
+  double *SF = reinterpret_cast<double *>(ws + p->off_SF);
+  double *TP = reinterpret_cast<double *>(ws + p->off_TP);
+  const bool timed = g_timing.load() != 0;
+  p->timed = timed;
+  if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
+  LFD_HIP(lfd::launch_block_functionals(p->n_sec, x, s_ch, s_t, p->bg, p->kc, F, st));
+  if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
+  LFD_HIP(lfd::launch_chunk_scan(p->n_sec, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
+                                 p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st));
+  if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
+  return LFD_OK;
+}
+
+int lfd_lowpass_last_timing(const lfd_lowpass_plan *p, float *ms_blocks, float *ms_scan) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (!p->timed) return fail(LFD_EINVAL, "timing was not enabled for the last execute");
+  LFD_HIP(hipEventSynchronize(p->ev[2]));
+  float a = 0, b = 0;
+  LFD_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
+  LFD_HIP(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
+  if (ms_blocks) *ms_blocks = a;
+  if (ms_scan) *ms_scan = b;
+  return LFD_OK;
+}
+
+int lfd_debug_plan_constants(const lfd_lowpass_plan *p, void *block_const, size_t bc_bytes,
+                             void *scan_const, size_t sc_bytes, void *chunk_geom,
+                             size_t cg_bytes) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (bc_bytes != sizeof(lfd::BlockConst) || sc_bytes != sizeof(lfd::ScanConst) ||
+      cg_bytes != sizeof(lfd::ChunkGeom) * p->chunks.size())
+    return fail(LFD_EINVAL, "size mismatch: BlockConst " + std::to_string(sizeof(lfd::BlockConst)) +
+                                " ScanConst " + std::to_string(sizeof(lfd::ScanConst)) +
+                                " ChunkGeom " + std::to_string(sizeof(lfd::ChunkGeom)));
+  std::memcpy(block_const, &p->kc, bc_bytes);
+  std::memcpy(scan_const, &p->sc, sc_bytes);
+  std::memcpy(chunk_geom, p->chunks.data(), cg_bytes);
+  return LFD_OK;
+}
+
+void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
+  if (!p) return;
+  if (p->d_chunks) (void)hipFree(p->d_chunks);
+  for (auto &e : p->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete p;
+}
+
+size_t lfd_sosfiltfilt_workspace_bytes(int64_t n_ch, int64_t n_t, int padlen, int n_sec) {
+  if (padlen < 0) padlen = 3 * (2 * n_sec + 1);
+  return align256(sizeof(double) * (size_t)(n_t + 2 * (int64_t)padlen) * (size_t)n_ch);
+}
+
+int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
+                        int64_t s_t, const double *sos, int n_sec, int padlen,
+                        double *y, int64_t ys_ch, int64_t ys_t, void *workspace,
+                        void *stream) {
+  Cascade c;
+  if (int e = load_sos(sos, n_sec, c)) return e;
+  if (padlen < 0) padlen = default_padlen(c);
+  if (n_ch < 1 || n_t < 1) return fail(LFD_EINVAL, "n_ch and n_t must be >= 1");
+  if (n_t <= padlen)
+    return fail(LFD_EINVAL, "The length of the input vector x must be greater than padlen, which is " +
+                                std::to_string(padlen) + ".");
+  if (!x || !y || !workspace) return fail(LFD_EINVAL, "x, y and workspace must be device pointers");
+  lfd::SosCoef cf{};
+  for (int s = 0; s < n_sec; ++s) {
+    cf.b0[s] = c.b0[s];
+    cf.b1[s] = c.b1[s];
+    cf.b2[s] = c.b2[s];
+    cf.a1[s] = c.a1[s];
+    cf.a2[s] = c.a2[s];
+  }
+  lfd::ZiVec zi{};
+  sosfilt_zi(c, zi.v);
+  LFD_HIP(lfd::launch_sosfiltfilt(n_sec, x, n_ch, n_t, s_ch, s_t, cf, zi, padlen,
+                                  static_cast<double *>(workspace), y, ys_ch, ys_t,
+                                  reinterpret_cast<hipStream_t>(stream)));
+  return LFD_OK;
+}
+
+int lfd_interp_linear_f64(const double *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
+                          int64_t s_t, const int64_t *lo_dev, const double *w_dev,
+                          int64_t n_out, float *y, int64_t ys_ch, int64_t ys_t,
+                          void *stream) {
+  if (n_ch < 1 || n_out < 0) return fail(LFD_EINVAL, "bad sizes");
+  if (n_out == 0) return LFD_OK;
+  LFD_HIP(lfd::launch_interp_linear(x, n_ch, n_t, s_ch, s_t, lo_dev, w_dev, n_out, y, ys_ch,
+                                    ys_t, reinterpret_cast<hipStream_t>(stream)));
+  return LFD_OK;
+}
+
+int lfd_sos_filtfilt_resample_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
+                                  int64_t s_t, const double *sos, int n_sec, int padlen,
+                                  const int64_t *lo, const double *w, int64_t n_out, float *y,
+                                  int64_t ys_ch, int64_t ys_t, void *stream) {
+  if (n_out < 1) return LFD_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  lfd_chunk ck{0, n_t - 1, 0, n_out};
+  lfd_lowpass_plan *plan = nullptr;
+  int rc = lfd_lowpass_plan_create(&plan, sos, n_sec, padlen, n_ch, n_t, lo, w, n_out, &ck, 1);
+  if (rc == LFD_OK) {
+    void *ws = nullptr;
+    hipError_t e = hipMalloc(&ws, std::max<size_t>(plan->ws_bytes, 256));
+    if (e == hipSuccess) rc = lfd_lowpass_execute(plan, x, s_ch, s_t, y, ys_ch, ys_t, ws, st);
+    else rc = fail(LFD_EHIP, std::string("workspace: ") + hipGetErrorString(e));
+    if (e == hipSuccess) {
+      hipError_t e2 = hipStreamSynchronize(st);
+      (void)hipFree(ws);
+      if (rc == LFD_OK && e2 != hipSuccess) rc = fail(LFD_EHIP, hipGetErrorString(e2));
+    }
+    lfd_lowpass_plan_destroy(plan);
+    return rc;
+  }
+  if (rc != LFD_EUNSUPPORTED) return rc;
+  // general path: full-rate zero-phase filter, then a device gather
+  Cascade c;
+  if (int e = load_sos(sos, n_sec, c)) return e;
+  const int pl = padlen < 0 ? default_padlen(c) : padlen;
+  for (int64_t j = 0; j < n_out; ++j)
+    if (lo[j] < 0 || lo[j] >= n_t || (w[j] != 0.0 && lo[j] + 1 >= n_t))
+      return fail(LFD_EINVAL, "interpolation position outside the array");
+  const size_t wsb = lfd_sosfiltfilt_workspace_bytes(n_ch, n_t, pl, n_sec);
+  const size_t yb = align256(sizeof(double) * (size_t)n_ch * n_t);
+  const size_t tb = align256((sizeof(int64_t) + sizeof(double)) * (size_t)n_out);
+  char *buf = nullptr;
+  LFD_HIP(hipMalloc(&buf, wsb + yb + tb));
+  double *yf = reinterpret_cast<double *>(buf + wsb);
+  int64_t *dlo = reinterpret_cast<int64_t *>(buf + wsb + yb);
+  double *dw = reinterpret_cast<double *>(buf + wsb + yb + sizeof(int64_t) * n_out);
+  hipError_t e = hipMemcpy(dlo, lo, sizeof(int64_t) * n_out, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dw, w, sizeof(double) * n_out, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(buf);
+    return fail(LFD_EHIP, hipGetErrorString(e));
+  }
+  rc = lfd_sosfiltfilt_f32(x, n_ch, n_t, s_ch, s_t, sos, n_sec, pl, yf, n_t, 1, buf, stream);
+  if (rc == LFD_OK)
+    rc = lfd_interp_linear_f64(yf, n_ch, n_t, n_t, 1, dlo, dw, n_out, y, ys_ch, ys_t, stream);
+  e = hipStreamSynchronize(st);
+  (void)hipFree(buf);
+  if (rc == LFD_OK && e != hipSuccess) rc = fail(LFD_EHIP, hipGetErrorString(e));
+  return rc;
+}
+
+int lfd_rolling_mean_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
+                         int64_t window, int64_t step, float *y, int64_t ys_ch, int64_t ys_t,
+                         void *stream) {
+  if (window < 1 || step < 1) return fail(LFD_EINVAL, "window and step must be >= 1 samples");
+  if (n_ch < 1 || n_t < 1) return LFD_OK;
+  if (!x || !y) return fail(LFD_EINVAL, "x and y must be device pointers");
+  LFD_HIP(lfd::launch_rolling_mean(x, n_ch, n_t, s_ch, s_t, window, step, y, ys_ch, ys_t,
+                                   reinterpret_cast<hipStream_t>(stream)));
+  return LFD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""ctypes binding of liblfdas.so (include/lfdas.h).
+
+The HIP library is the product: there is no CPU fallback.  If the shared
+object is missing or fails to load, every compute entry point raises
+``LFDLibraryError`` — build it with ``python -c "import __graft_entry__ as g;
+g.build()"`` (or ``make -C low-freq-real-time_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblfdas.so")
+
+LFD_OK = 0
+LFD_EINVAL = -1
+LFD_EHIP = -2
+LFD_EUNSUPPORTED = -3
+LFD_ENOMEM = -4
+
+MAX_SEC = 4
+MAX_N = 2 * MAX_SEC
+
+# numpy mirrors of the internal kernel-constant structs (csrc/lfd_internal.h),
+# used only by lfd_debug_plan_constants in tests.
+_SOS = [("b0", "f8", MAX_SEC), ("b1", "f8", MAX_SEC), ("b2", "f8", MAX_SEC),
+        ("a1", "f8", MAX_SEC), ("a2", "f8", MAX_SEC)]
+BLOCK_CONST_DTYPE = np.dtype(_SOS + [
+    ("ia2", "f8", MAX_SEC), ("ra", "f8", MAX_SEC), ("beta0", "f8", MAX_SEC),
+    ("beta1", "f8", MAX_SEC), ("Bv", "f8", MAX_N), ("T", "f8", (MAX_N, MAX_N)),
+    ("cp", "f8", MAX_N), ("d0", "f8")])
+SCAN_CONST_DTYPE = np.dtype(_SOS + [
+    ("zi", "f8", MAX_N), ("Phi", "f8", (MAX_N, MAX_N)), ("M", "f8", (MAX_N, MAX_N)),
+    ("G0", "f8", MAX_N), ("H0", "f8", MAX_N)])
+CHUNK_GEOM_DTYPE = np.dtype([(n, "i8") for n in (
+    "s0", "s1", "kb", "ke", "head_end", "tail_begin", "kout0", "kout1", "jout0",
+    "sf_off", "head_out_pos", "head_out_j", "tail_out_pos", "tail_out_j")])
+
+
+class LFDLibraryError(RuntimeError):
+    """liblfdas.so is missing or could not be loaded."""
+
+
+class LFDError(RuntimeError):
+    """A liblfdas call returned an error code."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"liblfdas error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class LFDUnsupported(LFDError):
+    pass
+
+
+class lfd_chunk(ctypes.Structure):
+    _fields_ = [("s0", ctypes.c_int64), ("s1", ctypes.c_int64),
+                ("g0", ctypes.c_int64), ("g1", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def load():
+    """Load liblfdas.so once; raise LFDLibraryError if it is not there."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LFDLibraryError(
+            f"{LIB_PATH} not found: the HIP extension is not built (run "
+            "__graft_entry__.build()); lfdas has no CPU fallback")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        raise LFDLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    i64, i32, vp, sz = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    P = ctypes.POINTER
+    sig = {
+        "lfd_last_error": ([], ctypes.c_char_p),
+        "lfd_version": ([], i32),
+        "lfd_device_count": ([P(i32)], i32),
+        "lfd_set_timing": ([i32], i32),
+        "lfd_lowpass_plan_create": ([P(vp), vp, i32, i32, i64, i64, vp, vp, i64,
+                                     vp, i64], i32),
+        "lfd_lowpass_plan_info": ([vp, P(sz), P(i64), P(i64)], i32),
+        "lfd_lowpass_execute": ([vp, vp, i64, i64, vp, i64, i64, vp, vp], i32),
+        "lfd_lowpass_last_timing": ([vp, P(ctypes.c_float), P(ctypes.c_float)], i32),
+        "lfd_lowpass_plan_destroy": ([vp], None),
+        "lfd_debug_plan_constants": ([vp, vp, sz, vp, sz, vp, sz], i32),
+        "lfd_sos_filtfilt_resample_f32": ([vp, i64, i64, i64, i64, vp, i32, i32,
+                                           vp, vp, i64, vp, i64, i64, vp], i32),
+        "lfd_sosfiltfilt_workspace_bytes": ([i64, i64, i32, i32], sz),
+        "lfd_sosfiltfilt_f32": ([vp, i64, i64, i64, i64, vp, i32, i32, vp, i64,
+                                 i64, vp, vp], i32),
+        "lfd_interp_linear_f64": ([vp, i64, i64, i64, i64, vp, vp, i64, vp, i64,
+                                   i64, vp], i32),
+        "lfd_rolling_mean_f32": ([vp, i64, i64, i64, i64, i64, i64, vp, i64, i64,
+                                  vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+EXPORTED = (
+    "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing",
+    "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute",
+    "lfd_lowpass_last_timing", "lfd_lowpass_plan_destroy",
+    "lfd_debug_plan_constants", "lfd_sos_filtfilt_resample_f32",
+    "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32",
+    "lfd_interp_linear_f64", "lfd_rolling_mean_f32",
+)
+
+
+def check(rc: int):
+    if rc == LFD_OK:
+        return
+    msg = load().lfd_last_error().decode("utf-8", "replace")
+    if rc == LFD_EUNSUPPORTED:
+        raise LFDUnsupported(rc, msg)
+    if rc == LFD_EINVAL:
+        raise ValueError(msg)
+    raise LFDError(rc, msg)

@@ -1,0 +1,194 @@
+"""Python handles over the C-ABI plans (include/lfdas.h).
+
+Device buffers are torch CUDA tensors (PyTorch is plumbing here: HBM
+allocation, streams, torch.distributed); every compute call goes through
+liblfdas.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, load
+
+
+def _ptr(a) -> int:
+    """Device pointer of a torch tensor (or None)."""
+    return 0 if a is None else int(a.data_ptr())
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        import torch
+        return int(torch.cuda.current_stream().cuda_stream)
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+def _require_cuda(t, name, dtype=None):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D (channel, time) addressed by strides")
+
+
+class LowpassPlan:
+    """Chunked zero-phase Butterworth low-pass + resample plan
+    (``lfd_lowpass_plan_*``): the device form of
+    ``LFProc.process_time_range`` (lf_das.py:219-290).
+
+    ``grid_lo``/``grid_w``: output positions (sample index + fraction) in the
+    coordinates of the device array; ``chunks``: ``(s0, s1, g0, g1)`` rows —
+    inclusive sample range and output grid range of every chunk.
+    Raises ``LFDUnsupported`` when the grid is not a uniform sample-aligned
+    decimation grid (the host then uses the general full-rate path).
+    """
+
+    def __init__(self, sos, n_ch: int, n_t: int, grid_lo, grid_w, chunks, padlen: int = -1):
+        lib = load()
+        self._lib = lib
+        self.sos = np.ascontiguousarray(sos, dtype=np.float64)
+        self.n_sec = int(self.sos.shape[0])
+        self.n_ch = int(n_ch)
+        self.n_t = int(n_t)
+        self.grid_lo = np.ascontiguousarray(grid_lo, dtype=np.int64)
+        self.grid_w = np.ascontiguousarray(grid_w, dtype=np.float64)
+        ch = np.ascontiguousarray(np.asarray(chunks, dtype=np.int64).reshape(-1, 4))
+        self.chunks = ch
+        h = ctypes.c_void_p()
+        rc = lib.lfd_lowpass_plan_create(
+            ctypes.byref(h), self.sos.ctypes.data, self.n_sec, int(padlen), self.n_ch,
+            self.n_t, self.grid_lo.ctypes.data, self.grid_w.ctypes.data,
+            len(self.grid_lo), ch.ctypes.data, ch.shape[0])
+        check(rc)
+        self._h = h
+        ws = ctypes.c_size_t()
+        nb = ctypes.c_int64()
+        L = ctypes.c_int64()
+        check(lib.lfd_lowpass_plan_info(h, ctypes.byref(ws), ctypes.byref(nb), ctypes.byref(L)))
+        self.workspace_bytes = int(ws.value)
+        self.n_blocks = int(nb.value)
+        self.block_len = int(L.value)
+        self.n_grid = len(self.grid_lo)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.lfd_lowpass_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def alloc_workspace(self, device=None):
+        import torch
+        return torch.empty(max(self.workspace_bytes, 256), dtype=torch.uint8, device=device or "cuda")
+
+    def execute(self, x, y, workspace, stream=None):
+        """Run on device: ``x`` (n_ch, n_t) float32, ``y`` (n_ch, n_grid)
+        float32 (any strides), ``workspace`` >= workspace_bytes."""
+        import torch
+        _require_cuda(x, "x", torch.float32)
+        _require_cuda(y, "y", torch.float32)
+        if tuple(x.shape) != (self.n_ch, self.n_t):
+            raise ValueError(f"x shape {tuple(x.shape)} != plan {(self.n_ch, self.n_t)}")
+        if tuple(y.shape) != (self.n_ch, self.n_grid):
+            raise ValueError(f"y shape {tuple(y.shape)} != {(self.n_ch, self.n_grid)}")
+        if workspace.numel() * workspace.element_size() < self.workspace_bytes:
+            raise ValueError("workspace too small")
+        check(self._lib.lfd_lowpass_execute(
+            self._h, _ptr(x), x.stride(0), x.stride(1), _ptr(y), y.stride(0), y.stride(1),
+            _ptr(workspace), _stream_ptr(stream)))
+
+    def last_timing_ms(self):
+        a = ctypes.c_float()
+        b = ctypes.c_float()
+        check(self._lib.lfd_lowpass_last_timing(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return float(a.value), float(b.value)
+
+    def constants(self):
+        """(BlockConst, ScanConst, ChunkGeom[]) numpy records — testing hook."""
+        bc = np.zeros(1, _lib.BLOCK_CONST_DTYPE)
+        sc = np.zeros(1, _lib.SCAN_CONST_DTYPE)
+        cg = np.zeros(self.chunks.shape[0], _lib.CHUNK_GEOM_DTYPE)
+        check(self._lib.lfd_debug_plan_constants(
+            self._h, bc.ctypes.data, bc.nbytes, sc.ctypes.data, sc.nbytes, cg.ctypes.data, cg.nbytes))
+        return bc[0], sc[0], cg
+
+
+def set_timing(enable: bool):
+    check(load().lfd_set_timing(1 if enable else 0))
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    check(load().lfd_device_count(ctypes.byref(n)))
+    return int(n.value)
+
+
+def sosfiltfilt_device(x, sos, padlen: int = -1, stream=None):
+    """Full-rate zero-phase filter on device → float64 tensor (n_ch, n_t)
+    (``lfd_sosfiltfilt_f32``; DASCore ``pass_filter`` alone)."""
+    import torch
+    _require_cuda(x, "x", torch.float32)
+    lib = load()
+    sos = np.ascontiguousarray(sos, dtype=np.float64)
+    n_ch, n_t = x.shape
+    wsb = lib.lfd_sosfiltfilt_workspace_bytes(n_ch, n_t, int(padlen), sos.shape[0])
+    ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=x.device)
+    y = torch.empty((n_ch, n_t), dtype=torch.float64, device=x.device)
+    check(lib.lfd_sosfiltfilt_f32(_ptr(x), n_ch, n_t, x.stride(0), x.stride(1), sos.ctypes.data,
+                                  sos.shape[0], int(padlen), _ptr(y), y.stride(0), y.stride(1),
+                                  _ptr(ws), _stream_ptr(stream)))
+    return y
+
+
+def interp_device(yfull, lo, w, stream=None):
+    """Device gather ``y[:, lo] + w*(y[:, lo+1]-y[:, lo])`` → float32."""
+    import torch
+    lib = load()
+    lo_d = torch.as_tensor(np.ascontiguousarray(lo, dtype=np.int64), device=yfull.device)
+    w_d = torch.as_tensor(np.ascontiguousarray(w, dtype=np.float64), device=yfull.device)
+    n_ch, n_t = yfull.shape
+    out = torch.empty((n_ch, len(lo)), dtype=torch.float32, device=yfull.device)
+    check(lib.lfd_interp_linear_f64(_ptr(yfull), n_ch, n_t, yfull.stride(0), yfull.stride(1),
+                                    _ptr(lo_d), _ptr(w_d), len(lo), _ptr(out), out.stride(0),
+                                    out.stride(1), _stream_ptr(stream)))
+    return out
+
+
+def filtfilt_resample_device(x, sos, lo, w, padlen: int = -1, stream=None):
+    """One-shot ``pass_filter(...).interpolate(...)`` of one patch on device
+    (``lfd_sos_filtfilt_resample_f32``) → float32 (n_ch, n_out)."""
+    import torch
+    _require_cuda(x, "x", torch.float32)
+    lib = load()
+    sos = np.ascontiguousarray(sos, dtype=np.float64)
+    lo = np.ascontiguousarray(lo, dtype=np.int64)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    n_ch, n_t = x.shape
+    y = torch.empty((n_ch, len(lo)), dtype=torch.float32, device=x.device)
+    check(lib.lfd_sos_filtfilt_resample_f32(
+        _ptr(x), n_ch, n_t, x.stride(0), x.stride(1), sos.ctypes.data, sos.shape[0], int(padlen),
+        lo.ctypes.data, w.ctypes.data, len(lo), _ptr(y), y.stride(0), y.stride(1),
+        _stream_ptr(stream)))
+    return y
+
+
+def rolling_mean_device(x, window: int, step: int, stream=None):
+    """Rolling mean at the subsampled output points → float32 (n_ch, ceil(n_t/step))."""
+    import torch
+    _require_cuda(x, "x", torch.float32)
+    n_ch, n_t = x.shape
+    n_out = -(-n_t // int(step))
+    y = torch.empty((n_ch, n_out), dtype=torch.float32, device=x.device)
+    check(load().lfd_rolling_mean_f32(_ptr(x), n_ch, n_t, x.stride(0), x.stride(1), int(window),
+                                      int(step), _ptr(y), y.stride(0), y.stride(1),
+                                      _stream_ptr(stream)))
+    return y
