@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblfdas.so")
+LIB_PATH = os.environ.get("LFDAS_LIB") or os.path.join(_HERE, "liblfdas.so")
 
 LFD_OK = 0
 LFD_EINVAL = -1
