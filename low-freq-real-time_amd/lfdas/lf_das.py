@@ -1,0 +1,265 @@
+"""Drop-in for the reference's ``lf_das.py`` (DASDAE/low-freq-real-time):
+same entry points, parameters, messages and exceptions; the chunked
+low-pass + resample runs as ONE device pass over the selected time range
+(liblfdas.so ``lfd_lowpass_*``) instead of a per-chunk SciPy loop.
+
+Reference line map: ``_check_merge`` lf_das.py:16-20, ``_get_timestr`` /
+``_get_filename`` :23-31, ``_down_sample_processing`` :34-44,
+``get_edge_effect_time`` :47-87, ``get_patch_time`` :90-107,
+``waterfall_plot`` :110-178, ``LFProc`` :182-295.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+
+import numpy as np
+
+from . import schedule as S
+from .core import FrozenDict, Patch, spool, to_datetime64
+from .design import default_padlen, lowpass_sos
+
+
+# define functions
+def _check_merge(plist):
+    """lf_das.py:16-20."""
+    if len(plist) > 1:
+        raise Exception("patch merge failed! Gap in data exists")
+    return plist[0]
+
+
+def _get_timestr(bgtime) -> str:
+    """lf_das.py:23-26: ISO ms string truncated to 21 chars, ':' removed."""
+    timestr = str(np.datetime64(bgtime).astype("datetime64[ms]"))[:21]
+    return timestr.replace(":", "")
+
+
+def _get_filename(bgtime, edtime) -> str:
+    """lf_das.py:29-31."""
+    return "LFDAS_" + _get_timestr(bgtime) + "_" + _get_timestr(edtime) + ".h5"
+
+
+def _down_sample_processing(patch, freq=5, nqfreq_ratio=0.8, **kargs):
+    """lf_das.py:34-44: low-pass at ``freq*0.5*nqfreq_ratio`` then resample
+    onto ``arange(time_min, time_max, 1/freq s)`` (fused on the device)."""
+    dt = np.timedelta64(int(1 / freq * 1e9), "ns")
+    corner_f = freq * 0.5 * nqfreq_ratio
+    proc_patch = patch.pass_filter(time=(None, corner_f))
+    new_taxis = np.arange(patch.attrs["time_min"], patch.attrs["time_max"], dt)
+    return proc_patch.interpolate(time=new_taxis)
+
+
+def get_edge_effect_time(sampling_interval, total_T, fun=_down_sample_processing, tol=1e-6, **kargs):
+    """lf_das.py:47-87: half-width of the chain's impulse response above
+    ``tol*max`` (raises ValueError when it reaches half the chunk)."""
+    N = int(total_T / sampling_interval)
+    taxis = (np.arange(N) - N // 2) * sampling_interval
+    data = np.zeros_like(taxis)
+    data[N // 2] = 1
+    coords = {"time": to_datetime64(taxis), "distance": [0]}
+    data = data.reshape((-1, 1))
+    attrs = {"d_time": sampling_interval, "d_distance": 1}
+    newdata = Patch(data=data, coords=coords, dims=["time", "distance"], attrs=attrs)
+    process_data = newdata.pipe(fun, **kargs)
+    freq = kargs.get("freq")
+    data = process_data.data[:, 0]
+    max_val = np.max(np.abs(data))
+    ind = np.abs(data) > max_val * tol
+    ind_1 = np.where(ind)[0][0]
+    ind_2 = np.where(ind)[0][-1]
+    new_taxis = process_data.coords["time"]
+    new_taxis = (new_taxis - new_taxis[0]) / np.timedelta64(1, "s") - N // 2 * sampling_interval
+    edge_t = max(np.abs(new_taxis[ind_1]), np.abs(new_taxis[ind_2]))
+    if int(np.ceil(edge_t * freq)) * 2 >= int(total_T * freq):
+        raise ValueError(
+            f"edge_t value ({edge_t} sec) is too close to half of the processing chunk size "
+            f"({total_T} sec). If your spool contains enough data (at least roughly more than "
+            "180 seconds) please increase memory_size or tolerance.")
+    return edge_t
+
+
+def get_patch_time(memory_size, sampling_rate, num_ch, bytes_per_element=8,
+                   processing_factor=5, memory_safety_factor=1.2):
+    """lf_das.py:90-107: chunk length (s) for a memory budget in MB."""
+    mem_size_per_second = (sampling_rate * num_ch * bytes_per_element * processing_factor
+                           * memory_safety_factor / 1e6)
+    return memory_size / mem_size_per_second
+
+
+def waterfall_plot(some_data, min_sec, max_sec, min_ch, max_ch, ch_start, channel_spacing,
+                   surface_fiber, sample_rate, fig_title, fig_dir, fig_name):
+    """lf_das.py:110-178 (visualisation; out of the hot-path scope — kept so
+    ``from lf_das import waterfall_plot`` works).  Returns the figure path."""
+    if min_sec >= max_sec or min_sec < 0 or max_sec * sample_rate > some_data.shape[1]:
+        print(f"ERROR in plotSpaceTime inputs minSec: {min_sec} or maxSec: {max_sec}")
+        return None
+    if min_ch >= max_ch or min_ch < 0 or max_ch > some_data.shape[0]:
+        print(f"Error in plotSpaceTime inputs minCh: {min_ch} or maxCh: {max_ch} referring to "
+              f"array with {some_data.shape[0]} channels.")
+        return None
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    i0, i1 = int(min_sec * sample_rate), int(max_sec * sample_rate)
+    clip = np.percentile(np.abs(some_data), 95)
+    top = (min_ch + ch_start) * channel_spacing - surface_fiber
+    bottom = (max_ch + ch_start) * channel_spacing - surface_fiber
+    fig = plt.figure(figsize=(12, 8))
+    plt.imshow(some_data[min_ch:max_ch, i0:i1], aspect="auto", interpolation="none",
+               cmap="seismic", extent=(min_sec, max_sec, bottom, top), vmin=-clip, vmax=clip)
+    plt.ylabel("MD (ft)", fontsize=10)
+    plt.xlabel("Time (sec)", fontsize=10)
+    plt.title(fig_title, fontsize=14)
+    plt.colorbar().set_label("Strain rate (1/s)", fontsize=10)
+    out = os.path.join(fig_dir, fig_name + ".jpeg")
+    plt.savefig(out, dpi=600, format="jpeg")
+    plt.close(fig)
+    return out
+
+
+class LFProc:
+    """lf_das.py:182-295 — low-frequency processing of a spool.
+
+    ``device``: torch device for the HIP path (default ``cuda``).
+    ``verbose``: print the reference's per-chunk progress lines.
+    Processed patches of the last ``process_time_range`` call are kept in
+    ``self.outputs`` (and written to the output folder like the reference).
+    """
+
+    def __init__(self, sp=None, device=None, verbose=True):
+        self._spool = sp
+        self._para = self._default_process_parameters()
+        self._output_folder = None
+        self._device = device
+        self.verbose = verbose
+        self.outputs = []
+        self.write_files = True
+
+    def set_output_folder(self, folder, delete_existing=False):
+        """lf_das.py:188-195."""
+        self._output_folder = folder
+        if delete_existing and os.path.isdir(folder):
+            shutil.rmtree(folder)
+            print(f"original {folder} deleted")
+        if not os.path.isdir(folder):
+            os.mkdir(folder)
+            print(f"{folder} created")
+
+    def _default_process_parameters(self):
+        """lf_das.py:197-204."""
+        return {
+            "output_sample_interval": 1.0,  # in seconds
+            "process_patch_size": 100,  # in number of output_sample_interval
+            "edge_buff_size": 10,  # in number of output_sample_interval
+            "data_gap_tolorance": 10.0,
+        }
+
+    def update_processing_parameter(self, **kwargs):
+        """lf_das.py:206-212: unknown keys are reported and ignored."""
+        for key, value in kwargs.items():
+            if key not in self._para.keys():
+                print(f"{key} is not default parameter key")
+            else:
+                self._para[key] = value
+        return self.parameters
+
+    def get_last_processed_time(self):
+        """lf_das.py:214-217."""
+        out_sp = spool(self._output_folder).update()
+        return out_sp[-1].attrs["time_max"]
+
+    @property
+    def parameters(self):
+        return FrozenDict(self._para)
+
+    # ------------------------------------------------------------------
+    def process_time_range(self, bgtime, edtime):
+        """lf_das.py:219-290, one device pass for all chunks."""
+        if self._output_folder is None:
+            raise Exception("Please setup output folder first")
+        dt = self._para["output_sample_interval"]
+        patch_size = self._para["process_patch_size"]
+        buff_size = self._para["edge_buff_size"]
+        tg = S.time_grid(bgtime, edtime, dt)
+        sched, self._kinds = S.lfproc_chunks(len(tg), patch_size, buff_size, with_kind=True)
+        self.outputs = []
+
+        # merged, gap-checked data of every chunk (lf_das.py:236-240, 264-266)
+        n_ok, merged = self._merged_span(tg, sched)
+        if n_ok:
+            self._run_chunks(tg, sched[:n_ok], merged, dt)
+        if n_ok < len(sched):
+            if self.verbose:
+                print("Processing patch ", str(n_ok + 1))
+            raise Exception("patch merge failed! Gap in data exists")
+
+    def _merged_span(self, tg, sched):
+        """Largest chunk prefix whose selections are each gap-free; returns
+        (n_ok, merged patch covering those chunks)."""
+        t_lo = np.datetime64(int(tg[sched[0][0]]), "ns")
+        t_hi = np.datetime64(int(tg[max(b for _, b, _, _ in sched)]), "ns")
+        sel = self._spool.select(time=(t_lo, t_hi))
+        plist = spool(sel).chunk(time=None)
+        if len(plist) == 0:
+            raise IndexError("list index out of range")  # _check_merge(plist) on an empty spool
+        n_ok = 0
+        for a, b, _, _ in sched:
+            ta = np.datetime64(int(tg[a]), "ns")
+            tb = np.datetime64(int(tg[b]), "ns")
+            hit = [p for p in plist if not (p.coords["time"][-1] < ta or p.coords["time"][0] > tb)]
+            if len(hit) != 1:
+                break
+            n_ok += 1
+        if n_ok == 0:
+            return 0, None
+        ta = np.datetime64(int(tg[sched[0][0]]), "ns")
+        first = [p for p in plist if p.coords["time"][-1] >= ta][0]
+        return n_ok, first
+
+    def _run_chunks(self, tg, sched, data_patch, dt):
+        import torch
+
+        from .plan import LowpassPlan, filtfilt_resample_device
+        from .proc import to_device_ct
+        from ._lib import LFDUnsupported
+
+        t_ns = data_patch.sample_times_ns()
+        t0, dt_ns, n = int(t_ns[0]), data_patch.sampling_interval_ns(), len(t_ns)
+        fs = 1.0 / (dt_ns / 1e9)
+        sos = lowpass_sos(fs, 1 / dt / 2 * 0.9, 4)
+        padlen = default_padlen(sos)
+        x = to_device_ct(data_patch, self._device)
+        n_ch = x.shape[0]
+        chunks = []
+        for a, b, oa, ob in sched:
+            s0, s1 = S.select_range(t0, dt_ns, n, tg[a], tg[b])
+            chunks.append((s0, s1, oa, ob))
+        lo, w = S.grid_positions(t0, dt_ns, tg)
+        y = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float32, device=x.device)
+        try:
+            plan = LowpassPlan(sos, n_ch, n, np.clip(lo, 0, n - 1), w, chunks, padlen)
+            plan.execute(x, y, plan.alloc_workspace(x.device))
+            plan.close()
+        except LFDUnsupported:
+            # general grid: per-chunk fused call (still on the device)
+            for s0, s1, oa, ob in chunks:
+                xs = x[:, s0:s1 + 1]
+                y[:, oa:ob] = filtfilt_resample_device(xs, sos, lo[oa:ob] - s0, w[oa:ob], padlen)
+        yh = y.cpu().numpy()
+        tdim = data_patch.dims.index("time")
+        for i, (s0, s1, oa, ob) in enumerate(chunks, start=1):
+            if self.verbose:
+                if self._kinds[i - 1] == "tail":
+                    print(f"Processing patch {i} (Last portion of data)")
+                else:
+                    print("Processing patch ", str(i))
+            seg = yh[:, oa:ob].astype(np.float64)
+            data = seg.T.copy() if tdim == 0 else seg
+            coords = dict(data_patch.coords.coord_map)
+            coords["time"] = tg[oa:ob].astype("datetime64[ns]")
+            out = Patch(data=data, coords=coords, dims=data_patch.dims,
+                        attrs=data_patch._attrs_wo_coords()).update_attrs(d_time=dt)
+            self.outputs.append(out)
+            if self.write_files:
+                fn = _get_filename(out.attrs["time_min"], out.attrs["time_max"])
+                out.io.write(self._output_folder + "/" + fn, "dasdae")

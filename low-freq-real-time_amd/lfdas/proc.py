@@ -1,0 +1,194 @@
+"""Patch processing ops of the hot path, DASCore-compatible *(DASCore,
+external)*, computed on the GPU by liblfdas.so:
+
+* ``pass_filter(time=(lo, hi), corners=4, zerophase=True)`` — Butterworth SOS
+  + ``sosfiltfilt`` semantics (lf_das.py:40, :223).  Lazy: the returned patch
+  holds the filter; ``.interpolate`` fuses filter + resample into one device
+  pass, touching ``.data`` runs the full-rate device filter.
+* ``interpolate(time=array, kind='linear')`` — interp1d semantics
+  (lf_das.py:42, :223-225).
+* ``decimate(time=q, filter_type=None)`` — stride sub-sampling.
+* ``rolling(time=w, step=s, engine='numpy').mean()`` — pandas-compatible
+  right-aligned windows (rolling_mean_dascore.ipynb:148).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import schedule as S
+from .core import Patch, to_timedelta64
+from .design import default_padlen, pass_filter_sos
+
+
+def _get_torch_device(device=None):
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("lfdas needs a HIP device (MI355X); no CPU fallback")
+    return torch.device(device if device is not None else "cuda")
+
+
+def to_device_ct(patch: Patch, device=None, dtype=None):
+    """Patch data as a float32 device tensor viewed as (channel, time) —
+    strided view for dims ("time", ...), no host transpose."""
+    import torch
+    dev = _get_torch_device(device)
+    d = patch.device_data()
+    if patch.dims.index("time") == 0:
+        perm = (1, 0)
+    else:
+        perm = (0, 1)
+    dtype = dtype or torch.float32
+    if isinstance(d, torch.Tensor):
+        t = d.to(device=dev, dtype=dtype)
+    else:
+        a = np.asarray(d)
+        if a.ndim != 2:
+            raise ValueError("lfdas patches are 2-D (distance, time)")
+        npdt = np.float32 if dtype == torch.float32 else np.float64
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=npdt)).to(dev)
+    return t.permute(*perm)
+
+
+def _from_ct(y_ct, patch_dims):
+    """(channel, time) device tensor → host array in the patch's dim order."""
+    y = y_ct.detach().cpu().numpy()
+    return y.T.copy() if patch_dims.index("time") == 0 else y
+
+
+def _sampling_rate(patch: Patch) -> float:
+    return 1.0 / (patch.sampling_interval_ns() / 1e9)
+
+
+class _LazyFiltfilt:
+    """Pending zero-phase filter of ``src`` (materialised on demand)."""
+
+    def __init__(self, src: Patch, sos, padlen: int):
+        self.src = src
+        self.sos = np.ascontiguousarray(sos, dtype=np.float64)
+        self.padlen = int(padlen)
+        self.shape = src.shape
+
+    def materialize(self, patch: Patch):
+        from .plan import sosfiltfilt_device
+        x = to_device_ct(self.src)
+        y = sosfiltfilt_device(x, self.sos, self.padlen)
+        return _from_ct(y, patch.dims)
+
+
+def pass_filter(patch: Patch, corners=4, zerophase=True, **kwargs):
+    if len(kwargs) != 1:
+        raise ValueError("pass_filter takes exactly one dimension keyword, e.g. time=(None, 1.0)")
+    (dim, rng), = kwargs.items()
+    if dim != "time":
+        raise NotImplementedError("only time-axis filtering is on the device path")
+    if not zerophase:
+        raise NotImplementedError("zerophase=False (causal sosfilt) is not on the device path")
+    lo, hi = rng
+    sos = pass_filter_sos(_sampling_rate(patch), lo, hi, corners)
+    padlen = default_padlen(sos)
+    n_t = patch.shape[patch.dims.index("time")]
+    if n_t <= padlen:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {padlen}.")
+    return Patch(data=None, coords=patch.coords, dims=patch.dims,
+                 attrs=patch._attrs_wo_coords(), _lazy=_LazyFiltfilt(patch, sos, padlen))
+
+
+def _positions(patch: Patch, new_times):
+    """(lo, w) of each requested time in the patch's sample grid, exact in
+    integer ns; raises like interp1d(bounds_error=True) outside the data."""
+    t = patch.sample_times_ns()
+    tq = np.asarray(new_times).astype("datetime64[ns]").astype(np.int64)
+    if tq.size and (tq.min() < t[0] or tq.max() > t[-1]):
+        raise ValueError("A value in x_new is outside the interpolation range.")
+    if tq.size > 1 and np.any(np.diff(tq) <= 0):
+        raise ValueError("Interpolate requires monotonic increasing samples")
+    dt = patch.sampling_interval_ns()
+    lo, w = S.grid_positions(int(t[0]), dt, tq)
+    # a point on the last sample has w == 0 at lo == n-1
+    return lo, w
+
+
+def interpolate(patch: Patch, kind="linear", **kwargs):
+    if kind != "linear":
+        raise NotImplementedError("only linear interpolation is on the device path")
+    if len(kwargs) != 1:
+        raise ValueError("interpolate takes exactly one dimension keyword, e.g. time=array")
+    (dim, new), = kwargs.items()
+    if dim != "time":
+        raise NotImplementedError("only time-axis interpolation is on the device path")
+    new = np.asarray(new).astype("datetime64[ns]")
+    lo, w = _positions(patch, new)
+    coords = dict(patch.coords.coord_map)
+    coords["time"] = new
+    lazy = patch._lazy
+    if isinstance(lazy, _LazyFiltfilt):
+        from .plan import filtfilt_resample_device
+        x = to_device_ct(lazy.src)
+        y = filtfilt_resample_device(x, lazy.sos, lo, w, lazy.padlen)
+        data = _from_ct(y, patch.dims).astype(np.float64)
+    else:
+        from .plan import interp_device
+        x = to_device_ct(patch, dtype=__import__("torch").float64)
+        y = interp_device(x, lo, w)
+        data = _from_ct(y, patch.dims).astype(np.float64)
+    return Patch(data=data, coords=coords, dims=patch.dims, attrs=patch._attrs_wo_coords())
+
+
+def decimate(patch: Patch, filter_type=None, **kwargs):
+    if filter_type not in (None, False):
+        raise NotImplementedError("decimate with an anti-alias filter is a next-row item; "
+                                  "use pass_filter(...).interpolate(...) (the LFProc path)")
+    (dim, q), = kwargs.items()
+    q = int(q)
+    ax = patch.dims.index(dim)
+    idx = [slice(None)] * len(patch.dims)
+    idx[ax] = slice(None, None, q)
+    coords = dict(patch.coords.coord_map)
+    coords[dim] = coords[dim][::q]
+    return Patch(data=patch.device_data()[tuple(idx)], coords=coords, dims=patch.dims,
+                 attrs=patch._attrs_wo_coords())
+
+
+def _to_samples(patch: Patch, v) -> int:
+    if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
+        # DASCore treats plain numbers as coordinate units (seconds for time)
+        v = float(v)
+    td = to_timedelta64(v)
+    dt = patch.sampling_interval_ns()
+    n = int(round(int(td.astype(np.int64)) / dt))
+    if n < 1:
+        raise ValueError("rolling window/step shorter than one sample")
+    return n
+
+
+class _Roller:
+    def __init__(self, patch: Patch, W: int, S_: int):
+        self.patch = patch
+        self.W = W
+        self.S = S_
+
+    def mean(self):
+        from .plan import rolling_mean_device
+        p = self.patch
+        x = to_device_ct(p)
+        y = rolling_mean_device(x, self.W, self.S)
+        data = _from_ct(y, p.dims)
+        src = p.device_data()
+        if hasattr(src, "dtype") and np.dtype(str(src.dtype).replace("torch.", "")) == np.float64:
+            data = data.astype(np.float64)
+        coords = dict(p.coords.coord_map)
+        coords["time"] = p.coords["time"][:: self.S]
+        return Patch(data=data, coords=coords, dims=p.dims, attrs=p._attrs_wo_coords())
+
+
+def rolling(patch: Patch, step=None, center=False, engine="numpy", **kwargs):
+    if center:
+        raise NotImplementedError("center=True rolling is not on the device path")
+    if len(kwargs) != 1:
+        raise ValueError("rolling takes one dimension keyword, e.g. time=10")
+    (dim, window), = kwargs.items()
+    if dim != "time":
+        raise NotImplementedError("only time-axis rolling is on the device path")
+    W = _to_samples(patch, window)
+    S_ = 1 if step is None else _to_samples(patch, step)
+    return _Roller(patch, W, S_)

@@ -31,7 +31,7 @@ def time_grid(bgtime, edtime, dt_s: float) -> np.ndarray:
     return np.arange(to_ns(bgtime), to_ns(edtime), step, dtype=np.int64)
 
 
-def lfproc_chunks(n_grid: int, patch_size: int, buff_size: int):
+def lfproc_chunks(n_grid: int, patch_size: int, buff_size: int, with_kind: bool = False):
     """Chunk schedule of lf_das.py:258-290: list of
     ``(read_first, read_last, out_begin, out_end)`` grid indices.  Chunk k
     selects ``time_grid[read_first] .. time_grid[read_last]`` (inclusive) and
@@ -45,18 +45,21 @@ def lfproc_chunks(n_grid: int, patch_size: int, buff_size: int):
     if L <= P:
         P = L - 1
     out = [(0, P, B, P - B)]
+    kinds = ["first"]
     data_end = P
     new_data_end = data_end + P - 2 * B
     if new_data_end <= data_end and new_data_end < L:
         raise ValueError("process_patch_size must be larger than 2*edge_buff_size")
     while new_data_end < L:
         out.append((data_end - 2 * B, new_data_end, data_end - B, new_data_end - B))
+        kinds.append("body")
         data_end = new_data_end
         new_data_end = data_end + P - 2 * B
     if (L - data_end) > 1:
         new_data_end = L - 1
         out.append((data_end - 2 * B, new_data_end, data_end - B, new_data_end - B))
-    return out
+        kinds.append("tail")
+    return (out, kinds) if with_kind else out
 
 
 def grid_positions(t0_ns: int, dt_ns: int, times_ns) -> tuple[np.ndarray, np.ndarray]:

@@ -1,0 +1,130 @@
+"""Host logic on CPU: C-ABI exports, schedule/index arithmetic, plan geometry
+and the plan's kernel constants (via the NumPy kernel model in emulate.py)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import synth
+from emulate import emulate
+from lfdas import _lib
+from lfdas import schedule as S
+from lfdas.design import default_padlen, lowpass_sos
+from lfdas.plan import LowpassPlan
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_library_exports_every_header_symbol():
+    hdr = open(os.path.join(ROOT, "include", "lfdas.h")).read()
+    names = set(re.findall(r"\b(lfd_[a-z0-9_]+)\s*\(", hdr))
+    assert names, "no functions parsed from include/lfdas.h"
+    lib = _lib.load()
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+    assert names == set(_lib.EXPORTED)
+    assert lib.lfd_version() >= 100
+
+
+def test_design_matches_oracle():
+    for fs, fc in [(250.0, 1.0), (500.0, 0.45), (200.0, 0.045), (2000.0, 0.45)]:
+        np.testing.assert_array_equal(lowpass_sos(fs, fc), oracle.butter_sos(4, fc / (fs / 2)))
+        assert default_padlen(lowpass_sos(fs, fc)) == 15
+
+
+def test_time_grid_ms_truncation():
+    tg = S.time_grid(0, 10_000_000_000, 0.0015)  # int(1.5) ms step
+    assert tg[1] - tg[0] == 1_000_000
+    np.testing.assert_array_equal(S.time_grid(0, 5_000_000_000, 1.0), np.arange(5) * 1_000_000_000)
+
+
+@pytest.mark.parametrize("L,P,B", [(120, 40, 6), (3600, 600, 7), (30, 40, 6), (96, 40, 6), (8640, 2, 0), (7, 3, 1)])
+def test_schedule_matches_oracle(L, P, B):
+    assert S.lfproc_chunks(L, P, B) == oracle.lfproc_schedule(L, P, B)
+    sched, kinds = S.lfproc_chunks(L, P, B, with_kind=True)
+    assert kinds[0] == "first" and all(k in ("body", "tail") for k in kinds[1:])
+    # outputs contiguous, disjoint
+    outs = [(a, b) for _, _, a, b in sched]
+    for (a0, b0), (a1, b1) in zip(outs, outs[1:]):
+        assert b0 == a1
+
+
+def test_schedule_rejects_non_advancing():
+    with pytest.raises(ValueError):
+        S.lfproc_chunks(100, 10, 5)
+
+
+def test_grid_positions_and_select():
+    lo, w = S.grid_positions(1000, 4, [1000, 1004, 1006, 1400])
+    np.testing.assert_array_equal(lo, [0, 1, 1, 100])
+    np.testing.assert_allclose(w, [0, 0, 0.5, 0])
+    assert S.select_range(1000, 4, 50, 1001, 1008) == (1, 2)
+    assert S.select_range(1000, 4, 50, 0, 10 ** 6) == (0, 49)
+
+
+def _plan_for(fs, dt_out, P, B, n_ch, n):
+    dt_ns = int(round(1e9 / fs))
+    t0 = synth.T0_NS
+    tg = S.time_grid(t0, t0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    lo, w = S.grid_positions(t0, dt_ns, tg)
+    chunks = [(*S.select_range(t0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    sos = lowpass_sos(fs, 1 / dt_out / 2 * 0.9)
+    return LowpassPlan(sos, n_ch, n, lo, w, chunks), sched, tg
+
+
+def test_plan_geometry_cfg3():
+    plan, sched, tg = _plan_for(500.0, 1.0, 600, 7, 10_000, 1_800_000)
+    assert plan.block_len == 500 and plan.n_blocks == 3599
+    bc, sc, cg = plan.constants()
+    assert len(cg) == 7
+    # every output grid point maps to exactly one chunk output
+    produced = np.zeros(len(tg), int)
+    for G_, (a, b, oa, ob) in zip(cg, sched):
+        assert G_["head_end"] == G_["s0"] and G_["tail_begin"] == G_["s1"]  # 1-sample tail
+        produced[oa:ob] += 1
+        assert G_["kout1"] - G_["kout0"] == ob - oa
+    assert produced.sum() == 3585 and produced.max() == 1
+    # workspace: F (9 doubles/block/ch) + SF + TP
+    assert plan.workspace_bytes >= 9 * 8 * plan.n_blocks * 10_000
+
+
+def test_plan_rejects_unsupported_grids():
+    sos = lowpass_sos(250.0, 1.0)
+    with pytest.raises(_lib.LFDUnsupported):
+        LowpassPlan(sos, 2, 1000, [0, 10, 25], [0, 0, 0], [(0, 999, 0, 3)])
+    with pytest.raises(_lib.LFDUnsupported):
+        LowpassPlan(sos, 2, 1000, [0, 10, 20], [0, 0.5, 0], [(0, 999, 0, 3)])
+    with pytest.raises(ValueError, match="padlen"):
+        LowpassPlan(sos, 2, 1000, [0, 10, 20], [0, 0, 0], [(0, 12, 0, 1)])
+
+
+@pytest.mark.parametrize("name", ["lfproc_cfg1.npz", "lfproc_cfg5_slice.npz"])
+def test_plan_constants_reproduce_golden(name):
+    """Host-only plan → NumPy model of the kernels → SciPy golden vectors."""
+    g = np.load(os.path.join(G, name), allow_pickle=False)
+    if "cfg1" in name:
+        x = synth.random_das_spool_data().astype(np.float32)[:24]
+        ref = g["y"][:24]
+    else:
+        x = synth.noise_sine(4, 600_000, 200.0, seed=5, dc=1000.0)
+        ref = g["y"]
+    fs, dt_out, P, B = float(g["fs"]), float(g["dt_out"]), int(g["P"]), int(g["B"])
+    plan, sched, tg = _plan_for(fs, dt_out, P, B, x.shape[0], x.shape[1])
+    y = emulate(plan, x, 15)
+    m = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(y), ~m)
+    rel = np.sqrt(np.sum((y[m] - ref[m]) ** 2) / np.sum(ref[m] ** 2))
+    assert rel < 1e-6
+
+
+def test_host_only_plan_cannot_execute():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    plan, _, _ = _plan_for(250.0, 0.2, 40, 6, 2, 6000)
+    with pytest.raises((ValueError, TypeError)):
+        plan.execute(torch.zeros(2, 6000), torch.zeros(2, 120), torch.zeros(10, dtype=torch.uint8))
