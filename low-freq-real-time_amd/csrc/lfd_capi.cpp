@@ -91,18 +91,6 @@ void sosfilt_zi(const Cascade &c, double *zi) {
   }
 }
 
-// One TDF-II cascade step in extended precision (same state layout as the
-// device and as SciPy's zi: [z_s0, z_s1] per section).
-R step(const Cascade &c, R *z, R x) {
-  for (int s = 0; s < c.ns; ++s) {
-    const R v = c.b0[s] * x + z[2 * s];
-    z[2 * s] = c.b1[s] * x - c.a1[s] * v + z[2 * s + 1];
-    z[2 * s + 1] = c.b2[s] * x - c.a2[s] * v;
-    x = v;
-  }
-  return x;
-}
-
 struct Mat {
   int n;
   R a[MAX_N][MAX_N];
@@ -159,86 +147,193 @@ bool minv(const Mat &A, Mat &out) {
   return true;
 }
 
-struct StateSpace {
-  Mat A, Ainv;
-  R B[MAX_N], C[MAX_N], D;
+// ---------------------------------------------------------------------------
+// Realization R (lfd_internal.h): factored numerator FIR + all-pole sections.
+// Every kernel constant is obtained by simulating the same recurrences in
+// extended precision (so host and device agree on coordinates by
+// construction).
+// ---------------------------------------------------------------------------
+struct RModel {
+  int ns = 0, J = 0;
+  R a1[MAX_SEC], a2[MAX_SEC];
+  R c[lfd::MAX_J + 1];
+  R G = 0;
 };
 
-int state_space(const Cascade &c, StateSpace &ss) {
-  const int n = 2 * c.ns;
-  ss.A = Mat(n);
-  R z[MAX_N];
-  for (int j = 0; j < n; ++j) {
-    for (int i = 0; i < n; ++i) z[i] = (i == j);
-    ss.C[j] = step(c, z, 0);
-    for (int i = 0; i < n; ++i) ss.A.a[i][j] = z[i];
+int make_rmodel(const Cascade &cs, RModel &m) {
+  m.ns = cs.ns;
+  m.J = 2 * cs.ns;
+  R N[lfd::MAX_J + 1] = {0};
+  N[0] = 1;
+  int deg = 0;
+  for (int s = 0; s < cs.ns; ++s) {
+    const R b[3] = {cs.b0[s], cs.b1[s], cs.b2[s]};
+    R out[lfd::MAX_J + 1] = {0};
+    for (int i = 0; i <= deg; ++i)
+      for (int j = 0; j < 3; ++j) out[i + j] += N[i] * b[j];
+    deg += 2;
+    for (int i = 0; i <= deg; ++i) N[i] = out[i];
   }
-  for (int i = 0; i < n; ++i) z[i] = 0;
-  ss.D = step(c, z, 1);
-  for (int i = 0; i < n; ++i) ss.B[i] = z[i];
-  if (!minv(ss.A, ss.Ainv))
-    return fail(LFD_EUNSUPPORTED, "singular TDF-II transition (a section has a2 == 0)");
+  if (N[0] == 0) return fail(LFD_EUNSUPPORTED, "numerator with a zero leading coefficient");
+  m.G = N[0];
+  for (int j = 0; j <= m.J; ++j) m.c[j] = N[j] / N[0];
+  for (int s = 0; s < cs.ns; ++s) {
+    m.a1[s] = cs.a1[s];
+    m.a2[s] = cs.a2[s];
+    if (cs.a2[s] == 0.0)
+      return fail(LFD_EUNSUPPORTED, "a section with a2 == 0 (odd order) needs the full-rate path");
+    if ((1.0L + m.a1[s]) + m.a2[s] == 0)
+      return fail(LFD_EUNSUPPORTED, "a section with a pole at z = 1");
+  }
   return LFD_OK;
 }
 
+// forward all-pole (S[2s] = v_s[n-1], S[2s+1] = v_s[n-2]); returns v_last
+R r_allpole(const RModel &m, R *S, R v) {
+  for (int s = 0; s < m.ns; ++s) {
+    const R vn = v - m.a1[s] * S[2 * s] - m.a2[s] * S[2 * s + 1];
+    S[2 * s + 1] = S[2 * s];
+    S[2 * s] = vn;
+    v = vn;
+  }
+  return v;
+}
+
+struct BlockSim {
+  R ef[MAX_N], er0[MAX_N], p0;
+};
+
+// One block of L samples with given initial forward state, reverse state
+// entering from the right and an optional unit impulse in w at offset imp.
+BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp) {
+  const int n = 2 * m.ns;
+  R S[MAX_N], T[MAX_N];
+  for (int i = 0; i < n; ++i) {
+    S[i] = Sf0 ? Sf0[i] : 0;
+    T[i] = Tr0 ? Tr0[i] : 0;
+  }
+  std::vector<R> yf(L), ql(L);
+  for (int k = 0; k < L; ++k) yf[k] = m.G * r_allpole(m, S, k == imp ? 1.0L : 0.0L);
+  for (int k = L - 1; k >= 0; --k) ql[k] = r_allpole(m, T, yf[k]);
+  BlockSim o;
+  for (int i = 0; i < n; ++i) {
+    o.ef[i] = S[i];
+    o.er0[i] = T[i];
+  }
+  R acc = 0;
+  for (int j = 0; j <= m.J; ++j) acc += m.c[j] * ql[j];
+  o.p0 = m.G * acc;
+  return o;
+}
+
 // Fill the block-functional and scan constants for block length L.
-int block_constants(const Cascade &c, int L, lfd::BlockConst &kc, lfd::ScanConst &sc) {
-  const int n = 2 * c.ns;
-  StateSpace ss;
-  if (int e = state_space(c, ss)) return e;
+int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanConst &sc,
+                    bool &fir32) {
+  RModel m;
+  if (int e = make_rmodel(cs, m)) return e;
+  const int n = 2 * m.ns, J = m.J;
+  if (L < J + 1) return fail(LFD_EUNSUPPORTED, "grid spacing shorter than the FIR span");
   std::memset(&kc, 0, sizeof(kc));
   std::memset(&sc, 0, sizeof(sc));
-  for (int s = 0; s < c.ns; ++s) {
-    kc.f.b0[s] = sc.f.b0[s] = c.b0[s];
-    kc.f.b1[s] = sc.f.b1[s] = c.b1[s];
-    kc.f.b2[s] = sc.f.b2[s] = c.b2[s];
-    kc.f.a1[s] = sc.f.a1[s] = c.a1[s];
-    kc.f.a2[s] = sc.f.a2[s] = c.a2[s];
-    kc.ia2[s] = (double)(1.0L / (R)c.a2[s]);
-    kc.ra[s] = (double)((R)c.a1[s] / (R)c.a2[s]);
-    kc.beta0[s] = (double)((R)c.b1[s] - (R)c.a1[s] * c.b0[s]);
-    kc.beta1[s] = (double)((R)c.b2[s] - (R)c.a2[s] * c.b0[s]);
+  lfd::RCoef rc{};
+  R csum = 0;
+  fir32 = true;
+  for (int j = 0; j <= J; ++j) {
+    rc.c64[j] = (double)m.c[j];
+    rc.c32[j] = (float)m.c[j];
+    csum += m.c[j];
+    if (m.c[j] < 0) fir32 = false;  // cancellation: keep the FIR in float64
   }
-  for (int i = 0; i < n; ++i) kc.Bv[i] = (double)ss.B[i];
-  const Mat T = mpow(ss.A, L - 1);
-  const Mat TL2 = mpow(ss.A, L - 2);
-  const Mat Phi = T * ss.A;
+  rc.G = (double)m.G;
+  rc.csum = (double)csum;
+  for (int s = 0; s < m.ns; ++s) {
+    rc.na1[s] = (double)-m.a1[s];
+    rc.na2[s] = (double)-m.a2[s];
+    rc.nia2[s] = (double)(-1.0L / m.a2[s]);
+    rc.nra[s] = (double)(-m.a1[s] / m.a2[s]);
+    rc.dcg[s] = (double)(1.0L / ((1.0L + m.a1[s]) + m.a2[s]));
+  }
+  kc.r = rc;
+  sc.r = rc;
+  // reverse state-space in T coordinates (T(m) = A T(m+1) + B y)
+  Mat A(n), Ai(n);
+  R B[MAX_N];
+  for (int j = 0; j < n; ++j) {
+    R T[MAX_N] = {0};
+    T[j] = 1;
+    r_allpole(m, T, 0);
+    for (int i = 0; i < n; ++i) A.a[i][j] = T[i];
+  }
+  {
+    R T[MAX_N] = {0};
+    r_allpole(m, T, 1);
+    for (int i = 0; i < n; ++i) B[i] = T[i];
+  }
+  if (!minv(A, Ai)) return fail(LFD_EUNSUPPORTED, "singular reverse transition");
+  const Mat Tm = mpow(A, L - 1);
   for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      kc.T[i * MAX_N + j] = (double)T.a[i][j];
-      sc.Phi[i * MAX_N + j] = (double)Phi.a[i][j];
-    }
-  R cAinvB = 0;
-  for (int j = 0; j < n; ++j) {
-    R a = 0, h = 0;
+    for (int j = 0; j < n; ++j) kc.T[i * MAX_N + j] = (double)(m.G * Tm.a[i][j]);
+  // p0 as a linear function of (u, y0[0..J-1]) (unscaled v_last inputs):
+  // T(0) = Tm u, T(j) = A^{-j} (T(0) - sum_{q<j} A^q B y0[q]),
+  // p0 = G * G * sum_j c_j T(j)[2(ns-1)]
+  auto p0_of = [&](const R *u, const R *y0) {
+    R T0[MAX_N];
     for (int i = 0; i < n; ++i) {
-      a += ss.C[i] * TL2.a[i][j];
-      h += ss.C[i] * T.a[i][j];
+      T0[i] = 0;
+      for (int j = 0; j < n; ++j) T0[i] += Tm.a[i][j] * u[j];
     }
-    kc.cp[j] = (double)a;
-    sc.H0[j] = (double)h;
-    R t = 0;
-    for (int i = 0; i < n; ++i) t += ss.Ainv.a[j][i] * ss.B[i];
-    cAinvB += ss.C[j] * t;
-  }
-  kc.d0 = (double)(ss.D - cAinvB);
-  // M and G0 by simulating forward-from-e_j then reverse-from-zero.
-  std::vector<R> yf(L);
-  for (int j = 0; j < n; ++j) {
-    R z[MAX_N], r[MAX_N];
-    for (int i = 0; i < n; ++i) {
-      z[i] = (i == j);
-      r[i] = 0;
+    R val = 0;
+    for (int j = 0; j <= J; ++j) {
+      R acc[MAX_N];
+      for (int i = 0; i < n; ++i) acc[i] = T0[i];
+      Mat Aq = Mat::eye(n);
+      for (int q = 0; q < j; ++q) {
+        for (int i = 0; i < n; ++i) {
+          R t = 0;
+          for (int l = 0; l < n; ++l) t += Aq.a[i][l] * B[l];
+          acc[i] -= t * y0[q];
+        }
+        Aq = Aq * A;
+      }
+      const Mat Aij = mpow(Ai, j);
+      R tj = 0;
+      for (int l = 0; l < n; ++l) tj += Aij.a[2 * (m.ns - 1)][l] * acc[l];
+      val += m.c[j] * tj;
     }
-    for (int m = 0; m < L; ++m) yf[m] = step(c, z, 0);
-    R out0 = 0;
-    for (int m = L - 1; m >= 0; --m) out0 = step(c, r, yf[m]);
-    for (int i = 0; i < n; ++i) sc.M[i * MAX_N + j] = (double)r[i];
-    sc.G0[j] = (double)out0;
+    return m.G * m.G * val;
+  };
+  for (int i = 0; i < n; ++i) {
+    R u[MAX_N] = {0}, y0[lfd::MAX_J] = {0};
+    u[i] = 1;
+    kc.cp[i] = (double)p0_of(u, y0);
   }
-  double zi[MAX_N];
-  sosfilt_zi(c, zi);
-  for (int i = 0; i < n; ++i) sc.zi[i] = zi[i];
+  for (int q = 0; q < J; ++q) {
+    R u[MAX_N] = {0}, y0[lfd::MAX_J] = {0};
+    y0[q] = 1;
+    kc.dp[q] = (double)p0_of(u, y0);
+  }
+  // scan matrices
+  for (int i = 0; i < n; ++i) {
+    R e[MAX_N] = {0};
+    e[i] = 1;
+    const BlockSim bf = sim_block(m, L, e, nullptr, -1);
+    const BlockSim br = sim_block(m, L, nullptr, e, -1);
+    for (int r = 0; r < n; ++r) {
+      sc.PhiF[r * MAX_N + i] = (double)bf.ef[r];
+      sc.M[r * MAX_N + i] = (double)bf.er0[r];
+      sc.PhiR[r * MAX_N + i] = (double)br.er0[r];
+    }
+    sc.G0[i] = (double)bf.p0;
+    sc.H0[i] = (double)br.p0;
+  }
+  for (int q = 0; q < J; ++q) {
+    const BlockSim bi = sim_block(m, L, nullptr, nullptr, q);
+    for (int r = 0; r < n; ++r) {
+      sc.Kc[r * lfd::MAX_J + q] = (double)bi.ef[r];
+      sc.Kc[(n + r) * lfd::MAX_J + q] = (double)bi.er0[r];
+    }
+    sc.Kc[(2 * n) * lfd::MAX_J + q] = (double)bi.p0;
+  }
   return LFD_OK;
 }
 
@@ -259,6 +354,7 @@ struct lfd_lowpass_plan {
   lfd::BlockGeom bg{};
   lfd::BlockConst kc{};
   lfd::ScanConst sc{};
+  bool fir32 = true;
   std::vector<lfd::ChunkGeom> chunks;
   lfd::ChunkGeom *d_chunks = nullptr;
   int64_t sf_blocks = 0, tp_len = 0;
@@ -337,8 +433,8 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     if (G.ke <= G.kb) return bad(LFD_EUNSUPPORTED, "chunk holds no full block");
     G.head_end = base0 + G.kb * L;
     G.tail_begin = base0 + G.ke * L;
-    G.head_out_j = G.tail_out_j = -1;
-    G.head_out_pos = G.tail_out_pos = -1;
+    G.tail_out_j = -1;
+    G.tail_out_pos = -1;
     G.kout0 = G.kout1 = G.kb;
     G.jout0 = 0;
     bool any_block = false;
@@ -354,8 +450,8 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
         }
         G.kout1 = kj + 1;
       } else if (pos < G.head_end) {
-        G.head_out_pos = pos;
-        G.head_out_j = j;
+        // unreachable: grid points are block starts and blocks start >= s0
+        return bad(LFD_EINVAL, "internal: output grid point inside a chunk head");
       } else {
         G.tail_out_pos = pos;
         G.tail_out_j = j;
@@ -383,7 +479,7 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   p->bg.base = base0 + kmin * L;
   p->bg.L = L;
   p->bg.nF = 2 * n + 1;
-  if (int e = block_constants(c, L, p->kc, p->sc)) {
+  if (int e = block_constants(c, L, p->kc, p->sc, p->fir32)) {
     delete p;
     return e;
   }
@@ -440,9 +536,9 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   const bool timed = g_timing.load() != 0;
   p->timed = timed;
   if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
-  LFD_HIP(lfd::launch_block_functionals(p->n_sec, x, s_ch, s_t, p->bg, p->kc, F, st));
+  LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
   if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
-  LFD_HIP(lfd::launch_chunk_scan(p->n_sec, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
+  LFD_HIP(lfd::launch_chunk_scan(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
                                  p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st));
   if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
   return LFD_OK;

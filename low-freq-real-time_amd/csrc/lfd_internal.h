@@ -11,35 +11,53 @@ constexpr int MAX_SEC = 4;            // up to 8th-order cascades
 constexpr int MAX_N = 2 * MAX_SEC;    // state dimension (TDF-II, 2 per section)
 
 // Transposed-direct-form-II cascade, a0 normalised to 1 (SciPy's sos rows,
-// scipy/signal/_signaltools.py:4706 `_sosfilt`).
+// scipy/signal/_signaltools.py:4706 `_sosfilt`) — used by the full-rate path.
 struct SosCoef {
   double b0[MAX_SEC], b1[MAX_SEC], b2[MAX_SEC], a1[MAX_SEC], a2[MAX_SEC];
 };
 
-// Constants of the block-functional kernel (k_block_functionals).  One
-// "block" is L consecutive samples of one channel; the kernel runs the
-// forward recurrence from zero state and, in the same sweep, the reverse
-// recurrence's zero-state exit state via the inverse-time accumulator
-//     u <- A^{-1} u + B y_f[m]          (u_L = sum_m A^{-(L-1-m)} B y_f[m])
-// so the block is read once and nothing per-sample is stored.
+constexpr int MAX_J = 2 * MAX_SEC;    // FIR taps - 1 of the factored numerator
+
+// Realization "R" of the same cascade used by the decimating path:
+//   w[n]   = x[n] + sum_{j=1..J} c[j] x[n-j]           (numerator / N0, FIR)
+//   v_s[n] = v_{s-1}[n] - a1_s v_s[n-1] - a2_s v_s[n-2] (all-pole sections)
+//   y_f[n] = G v_last[n],  G = N0 = prod_s b0_s          (forward output)
+// and the reverse pass in the mirrored form on q (backward in time) with the
+// FIR applied on its output: y[m] = G sum_j c[j] q_last[m+j].
+// Forward state S = (v_s[n-1], v_s[n-2]) per section; reverse state
+// T(m) = (q_s[m], q_s[m+1]) per section (state after processing sample m).
+// Same filter as SciPy's TDF-II in exact arithmetic; the loop-carried chain
+// is one FMA per section and the FIR runs in float32 for non-negative taps.
+struct RCoef {
+  double na1[MAX_SEC], na2[MAX_SEC];   // -a1, -a2
+  double nia2[MAX_SEC], nra[MAX_SEC];  // -1/a2, -a1/a2 (inverse accumulator)
+  double dcg[MAX_SEC];                 // 1/(1+a1+a2): steady-state gains
+  double c64[MAX_J + 1];               // FIR taps (c[0] = 1)
+  float c32[MAX_J + 1];
+  double G, csum;                      // N0, sum_j c[j]
+};
+
+// Constants of the block-functional kernel (k_block_functionals*).  One
+// block = L consecutive samples of one channel; the kernel runs the forward
+// recurrence from zero all-pole state (true FIR history) and, in the same
+// sweep, the reverse pass's zero-state exit state through the inverse-time
+// accumulator  u <- A_r^{-1} u + B_r v_last[m]  (unscaled; G folded below).
 struct BlockConst {
-  SosCoef f;
-  double ia2[MAX_SEC], ra[MAX_SEC];        // A_i^{-1} = [[0, -ia2], [1, -ra]]
-  double beta0[MAX_SEC], beta1[MAX_SEC];   // section input vectors
-  double Bv[MAX_N];                        // cascade input vector B
-  double T[MAX_N * MAX_N];                 // A^{L-1}: u -> reverse exit state
-  double cp[MAX_N];                        // C A^{L-2}
-  double d0;                               // D - C A^{-1} B
+  RCoef r;
+  double T[MAX_N * MAX_N];   // G A_r^{L-1}: u -> e_r0
+  double cp[MAX_N];          // p0 = cp.u + dp.y0  (output at offset 0)
+  double dp[MAX_J];
 };
 
 // Constants of the per-chunk scan kernel (k_chunk_scan).
 struct ScanConst {
-  SosCoef f;
-  double zi[MAX_N];                        // sosfilt_zi(sos) (flattened)
-  double Phi[MAX_N * MAX_N];               // A^L
-  double M[MAX_N * MAX_N];                 // reverse exit-state response to s_f
-  double G0[MAX_N];                        // output(offset 0) response to s_f
-  double H0[MAX_N];                        // output(offset 0) response to r(b)
+  RCoef r;
+  double PhiF[MAX_N * MAX_N];  // forward all-pole state over one block
+  double PhiR[MAX_N * MAX_N];  // reverse state over one block
+  double M[MAX_N * MAX_N];     // reverse exit state response to S_f
+  double G0[MAX_N];            // output(offset 0) response to S_f
+  double H0[MAX_N];            // output(offset 0) response to T entering
+  double Kc[(2 * MAX_N + 1) * MAX_J];  // functionals' response to w[0..J-1]
 };
 
 struct ZiVec {
@@ -55,7 +73,6 @@ struct ChunkGeom {
   int64_t kout0, kout1;  // blocks whose offset-0 sample is an output
   int64_t jout0;         // grid index of block kout0's output
   int64_t sf_off;        // offset (in blocks) of this chunk in the s_f scratch
-  int64_t head_out_pos, head_out_j;  // output inside the head (j < 0: none)
   int64_t tail_out_pos, tail_out_j;  // output inside the tail (j < 0: none)
 };
 
@@ -66,11 +83,11 @@ struct BlockGeom {
 };
 
 // Launchers (lfd_kernels.hip).  All return hipError_t of the launch.
-hipError_t launch_block_functionals(int n_sec, const float *x, int64_t s_ch,
+hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g,
                                     const BlockConst &kc, double *F,
                                     hipStream_t st);
-hipError_t launch_chunk_scan(int n_sec, const float *x, int64_t s_ch,
+hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch,
                              int64_t s_t, const BlockGeom &g, int padlen,
                              const ScanConst &sc, const ChunkGeom *cg_dev,
                              int64_t n_chunks, const double *F, double *SF,

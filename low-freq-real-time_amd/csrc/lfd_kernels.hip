@@ -1,24 +1,26 @@
 // gfx950 (MI355X / CDNA4) kernels of the low-frequency DAS hot path.
 //
-//   k_block_functionals  — the HBM-streaming kernel: every input sample is read
-//                          exactly once; per block of L samples it emits the
-//                          2n+1 float64 numbers that summarise the block for a
-//                          zero-phase (forward+reverse) TDF-II cascade:
-//                          forward exit state e_f, reverse exit state e_r0 and
-//                          the reverse output at the block's first sample p0.
-//   k_chunk_scan         — per (chunk, channel): SciPy's odd-extension padding
-//                          and sosfilt_zi initial conditions at the chunk edges,
-//                          the forward scan s_f(k+1) = Phi s_f(k) + e_f(k), the
-//                          backward scan r(k) = Phi r(k+1) + e_r0(k) + M s_f(k)
-//                          and the decimated outputs y = p0 + H0 r + G0 s_f.
-//   k_sosfiltfilt_full   — full-rate zero-phase filter (Patch.pass_filter alone).
-//   k_interp_linear      — linear gather (Patch.interpolate on a full-rate array).
-//   k_rolling_*          — windowed mean at the subsampled output points only.
+//   k_block_functionals_lds — the HBM-streaming kernel for time-contiguous
+//        rows: every input sample is read once (coalesced, LDS-staged); per
+//        block of L samples it emits the 2n+1 float64 numbers that summarise
+//        the block for the zero-phase (forward + reverse) cascade: forward
+//        all-pole state e_f, reverse exit state e_r0 and the reverse output at
+//        the block's first sample p0.
+//   k_block_functionals_gen — same for any strides (lanes = channels).
+//   k_chunk_scan — per (chunk, channel): SciPy's odd-extension padding and
+//        steady-state initial conditions at the chunk edges, the FIR-history
+//        correction of the chunk's first block, the forward scan
+//        S_f(k+1) = PhiF S_f(k) + e_f(k), the backward scan
+//        T(k) = PhiR T(k+1) + e_r0(k) + M S_f(k) and the decimated outputs
+//        y = p0 + H0 T(k+1) + G0 S_f(k).
+//   k_sosfiltfilt_full — full-rate zero-phase filter (Patch.pass_filter alone).
+//   k_interp_linear — linear gather (Patch.interpolate on a full-rate array).
+//   k_rolling_* — windowed mean at the subsampled output points only.
 //
 // Reference semantics: scipy/signal/_signaltools.py:4718-4828 (sosfiltfilt),
 // _arraytools.py:57-107 (odd_ext), _signaltools.py:4103-4175 (sosfilt_zi),
 // scipy/interpolate/_interpolate.py:457-484 (linear interp1d); DASCore rolling.
-// The math of the block decomposition is derived in DESIGN.md §Kernels.
+// The block decomposition and realization R are derived in DESIGN.md §2.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -30,8 +32,10 @@
 namespace lfd {
 namespace {
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
 // ---------------------------------------------------------------------------
-// Recurrences (fp64)
+// TDF-II cascade step, SciPy's `_sosfilt` form (full-rate path only)
 // ---------------------------------------------------------------------------
 template <int NS>
 struct FwdRec {
@@ -46,7 +50,6 @@ struct FwdRec {
       na2[i] = -c.a2[i];
     }
   }
-  // One TDF-II cascade step on state z (2*NS), returns the cascade output.
   __device__ __forceinline__ double step(double (&z)[2 * NS], double v) const {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -59,282 +62,130 @@ struct FwdRec {
   }
 };
 
-template <int NS>
-struct InvAcc {
-  double nia2[NS], nra[NS], nbeta0[NS], nbeta1[NS], b0[NS], Bv[2 * NS];
-  __device__ __forceinline__ void load(const BlockConst &k) {
+// ---------------------------------------------------------------------------
+// Realization R recurrences (see lfd_internal.h)
+// ---------------------------------------------------------------------------
+template <int NS, bool FIR32>
+struct RRec {
+  static constexpr int J = 2 * NS;
+  double na1[NS], na2[NS], nia2[NS], nra[NS];
+  float c32[J + 1];
+  double c64[J + 1];
+  __device__ __forceinline__ void load(const RCoef &r) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      nia2[i] = -k.ia2[i];
-      nra[i] = -k.ra[i];
-      nbeta0[i] = -k.beta0[i];
-      nbeta1[i] = -k.beta1[i];
-      b0[i] = k.f.b0[i];
-      Bv[2 * i] = k.Bv[2 * i];
-      Bv[2 * i + 1] = k.Bv[2 * i + 1];
+      na1[i] = r.na1[i];
+      na2[i] = r.na2[i];
+      nia2[i] = r.nia2[i];
+      nra[i] = r.nra[i];
+    }
+#pragma unroll
+    for (int j = 0; j <= J; ++j) {
+      c32[j] = r.c32[j];
+      c64[j] = r.c64[j];
     }
   }
-  // u <- A^{-1} u + B y   (A block lower-triangular: forward substitution)
-  __device__ __forceinline__ void step(double (&u)[2 * NS], double y) const {
-    double g = 0.0;  // section input generated by A^{-1}u with zero x
+  // FIR on the newest sample xv with history h[0..J-1] = x[n-1..n-J]
+  // (float32 when every tap is non-negative, else float64); shifts h.
+  __device__ __forceinline__ double fir(float xv, float (&h)[J]) const {
+    double w;
+    if (FIR32) {
+      float a = xv;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double t0 = u[2 * i], t1 = u[2 * i + 1];
-      if (i > 0) {
-        t0 = fma(nbeta0[i], g, t0);
-        t1 = fma(nbeta1[i], g, t1);
-      }
-      const double w0 = nia2[i] * t1;
-      const double w1 = fma(nra[i], t1, t0);
-      if (i + 1 < NS) g = (i == 0) ? w0 : fma(b0[i], g, w0);
-      u[2 * i] = fma(Bv[2 * i], y, w0);
-      u[2 * i + 1] = fma(Bv[2 * i + 1], y, w1);
+      for (int j = 1; j <= J; ++j) a = fmaf(c32[j], h[j - 1], a);
+      w = (double)a;
+    } else {
+      double a = (double)xv;
+#pragma unroll
+      for (int j = 1; j <= J; ++j) a = fma(c64[j], (double)h[j - 1], a);
+      w = a;
+    }
+#pragma unroll
+    for (int j = J - 1; j > 0; --j) h[j] = h[j - 1];
+    h[0] = xv;
+    return w;
+  }
+  // all-pole cascade: S[2s] = v_s[n-1], S[2s+1] = v_s[n-2]; returns v_last
+  __device__ __forceinline__ double allpole(double (&S)[2 * NS], double v) const {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double vn = fma(na1[s], S[2 * s], fma(na2[s], S[2 * s + 1], v));
+      S[2 * s + 1] = S[2 * s];
+      S[2 * s] = vn;
+      v = vn;
+    }
+    return v;
+  }
+  // inverse-time accumulator u <- A_r^{-1} u + B_r y   (7 ops for NS = 2)
+  __device__ __forceinline__ void invacc(double (&u)[2 * NS], double y) const {
+    double t[2 * NS];
+#pragma unroll
+    for (int i = 0; i < 2 * NS; ++i) t[i] = u[i];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double d = s == 0 ? t[0] : t[2 * s] - t[2 * s - 2];
+      u[2 * s] = t[2 * s + 1] + y;
+      u[2 * s + 1] = fma(nia2[s], d, nra[s] * t[2 * s + 1]);
     }
   }
 };
 
-// ---------------------------------------------------------------------------
-// k_block_functionals
-// ---------------------------------------------------------------------------
-// LAYOUT 0 (time-contiguous, s_t == 1): workgroup = 16 channels x 32 blocks;
-//   a wave holds 4 channels x 16 lanes and each lane runs RB = 2 blocks (k and
-//   k+16) interleaved, so a wave's loads span 4 contiguous 32-block runs (TLB
-//   friendly) and the workgroup completes 128-B lines of F = [k][comp][ch].
-// LAYOUT 1 (any strides, e.g. channel-contiguous s_ch == 1): workgroup = 64
-//   channels x 8 blocks; a wave is 64 consecutive channels of blocks w and
-//   w+4, so a load is 64 consecutive floats when s_ch == 1.
-// Two interleaved recurrences per lane double the independent fp64 FMA
-// chains in flight: a dependent v_fma_f64 takes ~32 cycles on gfx950 and one
-// chain per wave reaches only half the fp64 issue rate even at 8 waves/SIMD
-// (tools/ubench_fp64.hip).  The hot loop is branch-free: groups of D float4
-// per stream are consumed from a register ring refilled D groups ahead.
-constexpr int RB = 2;
-#ifndef LFD_K1_D
-#define LFD_K1_D 2     // float4 ring depth per stream
-#endif
-#ifndef LFD_K1_MINW
-#define LFD_K1_MINW 6  // waves/SIMD the register budget must allow (80 VGPRs)
-#endif
+// Full scalar sample step of K1 (FIR -> all-pole -> accumulator).
+#define LFD_R_SAMPLE(rec, xv, h, S, u, yv)    \
+  do {                                       \
+    const double w_ = rec.fir((xv), h);      \
+    yv = rec.allpole(S, w_);                 \
+    rec.invacc(u, yv);                       \
+  } while (0)
 
-template <int NS, int LAYOUT, bool VEC4>
-__global__ __launch_bounds__(256, LFD_K1_MINW) void k_block_functionals(
-    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g,
-    const BlockConst kc, double *__restrict__ F) {
+// Block epilogue: e_f, e_r0 = T u, p0 = cp.u + dp.y0
+template <int NS>
+__device__ __forceinline__ void store_functionals(const BlockConst &kc, const double (&S)[2 * NS],
+                                                  const double (&u)[2 * NS],
+                                                  const double (&y0)[2 * NS], double *F,
+                                                  int64_t k, int64_t ch, int64_t n_ch) {
   constexpr int N = 2 * NS;
-  constexpr int TC = LAYOUT == 0 ? 16 : 64;
-  constexpr int TKL = 256 / TC;  // lanes along k per workgroup
-  constexpr int TK = TKL * RB;   // blocks per workgroup
-  const int64_t n_ct = (g.n_ch + TC - 1) / TC;
-  const int64_t tile = blockIdx.x;
-  const int64_t ct = tile % n_ct, kt = tile / n_ct;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int cl, kl;
-  if (LAYOUT == 0) {
-    cl = wave * 4 + (lane >> 4);
-    kl = lane & 15;
-  } else {
-    cl = lane;
-    kl = wave;
-  }
-  const int64_t ch = ct * TC + cl;
-  int64_t kr[RB];
-  bool live[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    kr[r] = kt * TK + r * TKL + kl;
-    live[r] = kr[r] < g.nb;
-    if (!live[r]) kr[r] = g.nb - 1;  // duplicate work, result discarded
-  }
-  if (ch >= g.n_ch || !live[0]) return;
-
-  FwdRec<NS> fr;
-  fr.load(kc.f);
-  InvAcc<NS> ia;
-  ia.load(kc);
-  double z[RB][N], u[RB][N], yf0[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    yf0[r] = 0.0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) z[r][i] = u[r][i] = 0.0;
-  }
-
-  const int L = g.L;
-  const float *p[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) p[r] = x + ch * s_ch + (g.base + kr[r] * (int64_t)L) * s_t;
-
-#define LFD_SAMPLE(r, xv)                        \
-  do {                                           \
-    const double y_ = fr.step(z[r], (double)(xv)); \
-    ia.step(u[r], y_);                           \
-  } while (0)
-#define LFD_FIRST(r, xv)                         \
-  do {                                           \
-    const double y_ = fr.step(z[r], (double)(xv)); \
-    yf0[r] = y_;                                 \
-    ia.step(u[r], y_);                           \
-  } while (0)
-
-  if (VEC4) {
-    // 16-B aligned rows, L % 4 == 0 (checked by the host)
-    constexpr int D = LFD_K1_D;
-    const int n4 = L >> 2;
-    const int G = n4 / D;
-    const float4 *p4[RB];
-    float4 buf[RB][D];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      p4[r] = reinterpret_cast<const float4 *>(p[r]);
-#pragma unroll
-      for (int d = 0; d < D; ++d) buf[r][d] = p4[r][min(d, n4 - 1)];
-    }
-    if (G >= 1) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const float4 v = buf[r][d];
-          buf[r][d] = p4[r][min(D + d, n4 - 1)];
-          if (d == 0) {
-            LFD_FIRST(r, v.x);
-          } else {
-            LFD_SAMPLE(r, v.x);
-          }
-          LFD_SAMPLE(r, v.y);
-          LFD_SAMPLE(r, v.z);
-          LFD_SAMPLE(r, v.w);
-        }
-      }
-      for (int gi = 1; gi < G; ++gi) {
-        const int nxt = (gi + 1) * D;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-#pragma unroll
-          for (int r = 0; r < RB; ++r) {
-            const float4 v = buf[r][d];
-            buf[r][d] = p4[r][min(nxt + d, n4 - 1)];
-            LFD_SAMPLE(r, v.x);
-            LFD_SAMPLE(r, v.y);
-            LFD_SAMPLE(r, v.z);
-            LFD_SAMPLE(r, v.w);
-          }
-        }
-      }
-    }
-    const int rem = n4 - G * D;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (d < rem) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const float4 v = buf[r][d];
-          if (G == 0 && d == 0) {
-            LFD_FIRST(r, v.x);
-          } else {
-            LFD_SAMPLE(r, v.x);
-          }
-          LFD_SAMPLE(r, v.y);
-          LFD_SAMPLE(r, v.z);
-          LFD_SAMPLE(r, v.w);
-        }
-      }
-    }
-  } else {
-    constexpr int D = 8;
-    const int G = L / D;
-    float buf[RB][D];
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int d = 0; d < D; ++d) buf[r][d] = p[r][(int64_t)min(d, L - 1) * s_t];
-    if (G >= 1) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const float v = buf[r][d];
-          buf[r][d] = p[r][(int64_t)min(D + d, L - 1) * s_t];
-          if (d == 0) {
-            LFD_FIRST(r, v);
-          } else {
-            LFD_SAMPLE(r, v);
-          }
-        }
-      }
-      for (int gi = 1; gi < G; ++gi) {
-        const int nxt = (gi + 1) * D;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-#pragma unroll
-          for (int r = 0; r < RB; ++r) {
-            const float v = buf[r][d];
-            buf[r][d] = p[r][(int64_t)min(nxt + d, L - 1) * s_t];
-            LFD_SAMPLE(r, v);
-          }
-        }
-      }
-    }
-    const int rem = L - G * D;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (d < rem) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          if (G == 0 && d == 0) {
-            LFD_FIRST(r, buf[r][d]);
-          } else {
-            LFD_SAMPLE(r, buf[r][d]);
-          }
-        }
-      }
-    }
-  }
-#undef LFD_SAMPLE
-#undef LFD_FIRST
-
-  // reverse exit state e_r0 = A^{L-1} u, output at offset 0 p0
   const int64_t nF = 2 * N + 1;
+  double *Fo = F + (k * nF) * n_ch + ch;
 #pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    if (!live[r]) continue;
-    double *Fo = F + (kr[r] * nF) * g.n_ch + ch;
+  for (int i = 0; i < N; ++i) Fo[i * n_ch] = S[i];
 #pragma unroll
-    for (int i = 0; i < N; ++i) Fo[i * g.n_ch] = z[r][i];
+  for (int i = 0; i < N; ++i) {
+    double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < N; ++j) acc = fma(kc.T[i * MAX_N + j], u[r][j], acc);
-      Fo[(N + i) * g.n_ch] = acc;
-    }
-    double p0 = kc.d0 * yf0[r];
-#pragma unroll
-    for (int j = 0; j < N; ++j) p0 = fma(kc.cp[j], u[r][j], p0);
-    Fo[2 * N * g.n_ch] = p0;
+    for (int j = 0; j < N; ++j) acc = fma(kc.T[i * MAX_N + j], u[j], acc);
+    Fo[(N + i) * n_ch] = acc;
   }
+  double p0 = 0.0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) p0 = fma(kc.cp[j], u[j], p0);
+#pragma unroll
+  for (int m = 0; m < N; ++m) p0 = fma(kc.dp[m], y0[m], p0);
+  Fo[2 * N * n_ch] = p0;
 }
 
 // ---------------------------------------------------------------------------
-// k_block_functionals_lds — time-contiguous rows, 16-B aligned (the DASCore
-// ("distance","time") layout).  Same lane -> (channel, block) mapping as
-// LAYOUT 0 (wave = 4 channels x 16 consecutive blocks, one block per lane),
-// but global loads are coalesced: each wave-instruction loads 16 consecutive
-// rows x 64 B (4 lanes per row piece) into a wave-private LDS tile
-// [64 rows][TS + 4 floats]; each lane then reads its own row with
-// conflict-free ds_read_b128 (row stride 20 dwords: 4*(5*lane mod 16) banks).
-// The next slice's loads are in flight (registers) while the current slice is
-// filtered.  LDS ops of one wave execute in order, so no barrier is needed.
+// k_block_functionals_lds — time-contiguous rows, 16-B aligned, L % 4 == 0
+// (the DASCore ("distance","time") layout).  Wave = 4 channels x 16
+// consecutive blocks (one block per lane; TLB-local; the 4 waves of a
+// workgroup complete 128-B lines of F = [k][comp][ch]).  Global loads are
+// coalesced: each wave-instruction loads 16 consecutive rows x 64 B (4 lanes
+// per row piece) into a wave-private LDS tile [64 rows][TS + 4 floats]; each
+// lane then reads its own row with conflict-free ds_read_b128 (row stride 20
+// dwords: banks 4*(5*lane mod 16)).  The next slice's loads are in flight in
+// registers while the current slice is filtered.  LDS ops of one wave execute
+// in order, so no barrier is needed.
 // ---------------------------------------------------------------------------
-typedef float f4v __attribute__((ext_vector_type(4)));
-constexpr int TS = 16;            // samples per row per slice
-constexpr int TSP = TS + 4;       // padded LDS row stride (floats)
+constexpr int TS = 16;       // samples per row per slice
+constexpr int TSP = TS + 4;  // padded LDS row stride (floats)
 
-template <int NS>
+template <int NS, bool FIR32>
 __global__ __launch_bounds__(256) void k_block_functionals_lds(
     const float *__restrict__ x, int64_t s_ch, BlockGeom g, const BlockConst kc,
     double *__restrict__ F) {
   constexpr int N = 2 * NS;
+  constexpr int J = 2 * NS;
+  static_assert(J <= 4 * (TS / 4), "history must fit one slice");
   __shared__ __attribute__((aligned(16))) float lds_all[4][64 * TSP];
   const int64_t n_ct = (g.n_ch + 15) / 16;
   const int64_t tile = blockIdx.x;
@@ -343,10 +194,11 @@ __global__ __launch_bounds__(256) void k_block_functionals_lds(
   float *lds = lds_all[wave];
   const int L = g.L;
 
-  // row owned by this lane (for filtering / storing)
   const int64_t ch = ct * 16 + wave * 4 + (lane >> 4);
   const int64_t k = kt * 16 + (lane & 15);
   const bool live = ch < g.n_ch && k < g.nb;
+  const int64_t chc = ch < g.n_ch ? ch : g.n_ch - 1;
+  const int64_t kc_ = k < g.nb ? k : g.nb - 1;
 
   // rows this lane stages: instruction i covers channel wave*4+i, block
   // kt*16 + lane/4, samples [t + 4*(lane%4), +4)
@@ -364,106 +216,232 @@ __global__ __launch_bounds__(256) void k_block_functionals_lds(
   for (int i = 0; i < 4; ++i) wr[i] = lds + (16 * i + (lane >> 2)) * TSP + 4 * (lane & 3);
   const float *rd = lds + lane * TSP;
 
-  FwdRec<NS> fr;
-  fr.load(kc.f);
-  InvAcc<NS> ia;
-  ia.load(kc);
-  double z[N], u[N];
+  RRec<NS, FIR32> rec;
+  rec.load(kc.r);
+  double S[N], u[N], y0[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) z[i] = u[i] = 0.0;
-  double yf0 = 0.0;
-
-  const int nsl = (L + TS - 1) / TS;  // slices (the last may be partial)
-  const int last_t = (nsl - 1) * TS;
-  f4v stage[4];
+  for (int i = 0; i < N; ++i) S[i] = u[i] = y0[i] = 0.0;
+  // FIR history: the J samples before the block (0 before the channel start)
+  float h[J];
+  {
+    const int64_t a = g.base + kc_ * (int64_t)L;
+    const float *row = x + chc * s_ch;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) stage[i] = *reinterpret_cast<const f4v *>(src[i]);
+    for (int j = 0; j < J; ++j) h[j] = (a - 1 - j >= 0) ? row[a - 1 - j] : 0.0f;
+  }
 
-#define LFD_QUAD(v)                      \
-  do {                                   \
-    double y_ = fr.step(z, (double)v.x); \
-    ia.step(u, y_);                      \
-    y_ = fr.step(z, (double)v.y);        \
-    ia.step(u, y_);                      \
-    y_ = fr.step(z, (double)v.z);        \
-    ia.step(u, y_);                      \
-    y_ = fr.step(z, (double)v.w);        \
-    ia.step(u, y_);                      \
+  const int nfull = L / TS;              // full slices
+  const int rem4 = (L - nfull * TS) >> 2;  // float4s of the partial slice (L % 4 == 0)
+  const int last_t = (nfull + (rem4 ? 1 : 0) - 1) * TS;
+  // two register stages keep two slices of loads in flight per wave
+  f4v stA[4], stB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) stA[i] = *reinterpret_cast<const f4v *>(src[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) stB[i] = *reinterpret_cast<const f4v *>(src[i] + min(TS, last_t));
+
+#define LFD_QUAD(v)                          \
+  do {                                       \
+    double yv_;                              \
+    LFD_R_SAMPLE(rec, v.x, h, S, u, yv_);    \
+    LFD_R_SAMPLE(rec, v.y, h, S, u, yv_);    \
+    LFD_R_SAMPLE(rec, v.z, h, S, u, yv_);    \
+    LFD_R_SAMPLE(rec, v.w, h, S, u, yv_);    \
+  } while (0)
+// stage -> LDS, refill the stage with slice sl+2, read this lane's row
+#define LFD_STAGE(st, sl)                                                              \
+  do {                                                                                 \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) *reinterpret_cast<f4v *>(wr[i]) = st[i]; \
+    const int tn_ = min(((sl) + 2) * TS, last_t);                                      \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) st[i] =                              \
+        *reinterpret_cast<const f4v *>(src[i] + tn_);                                  \
+  } while (0)
+#define LFD_FULL_SLICE(st, sl)                                  \
+  do {                                                          \
+    LFD_STAGE(st, sl);                                          \
+    const f4v v0_ = *reinterpret_cast<const f4v *>(rd);         \
+    const f4v v1_ = *reinterpret_cast<const f4v *>(rd + 4);     \
+    const f4v v2_ = *reinterpret_cast<const f4v *>(rd + 8);     \
+    const f4v v3_ = *reinterpret_cast<const f4v *>(rd + 12);    \
+    LFD_QUAD(v0_);                                              \
+    LFD_QUAD(v1_);                                              \
+    LFD_QUAD(v2_);                                              \
+    LFD_QUAD(v3_);                                              \
   } while (0)
 
-  for (int sl = 0; sl < nsl; ++sl) {
+  // slice 0 (peeled): capture the first J forward outputs for p0
+  {
+    LFD_STAGE(stA, 0);
+    const int nq = nfull ? TS / 4 : rem4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<f4v *>(wr[i]) = stage[i];
-    // prefetch the next slice (clamped: always a valid address)
-    const int tn = min((sl + 1) * TS, last_t);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) stage[i] = *reinterpret_cast<const f4v *>(src[i] + tn);
-    const int nq = min(TS, L - sl * TS) >> 2;  // f4vs available (L % 4 == 0)
-    if (sl == 0) {
-      const f4v v0 = *reinterpret_cast<const f4v *>(rd);
-      const double y0 = fr.step(z, (double)v0.x);
-      yf0 = y0;
-      ia.step(u, y0);
-      double y_ = fr.step(z, (double)v0.y);
-      ia.step(u, y_);
-      y_ = fr.step(z, (double)v0.z);
-      ia.step(u, y_);
-      y_ = fr.step(z, (double)v0.w);
-      ia.step(u, y_);
-#pragma unroll
-      for (int j = 1; j < TS / 4; ++j) {
-        if (j < nq) {
-          const f4v v = *reinterpret_cast<const f4v *>(rd + 4 * j);
-          LFD_QUAD(v);
-        }
-      }
-    } else if (nq == TS / 4) {
-#pragma unroll
-      for (int j = 0; j < TS / 4; ++j) {
+    for (int j = 0; j < TS / 4; ++j) {
+      if (j < nq) {
         const f4v v = *reinterpret_cast<const f4v *>(rd + 4 * j);
-        LFD_QUAD(v);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < TS / 4; ++j) {
-        if (j < nq) {
-          const f4v v = *reinterpret_cast<const f4v *>(rd + 4 * j);
-          LFD_QUAD(v);
-        }
+        double yv;
+        LFD_R_SAMPLE(rec, v.x, h, S, u, yv);
+        if (4 * j + 0 < J) y0[4 * j + 0] = yv;
+        LFD_R_SAMPLE(rec, v.y, h, S, u, yv);
+        if (4 * j + 1 < J) y0[4 * j + 1] = yv;
+        LFD_R_SAMPLE(rec, v.z, h, S, u, yv);
+        if (4 * j + 2 < J) y0[4 * j + 2] = yv;
+        LFD_R_SAMPLE(rec, v.w, h, S, u, yv);
+        if (4 * j + 3 < J) y0[4 * j + 3] = yv;
       }
     }
   }
-#undef LFD_QUAD
-  if (!live) return;
-  const int64_t nF = 2 * N + 1;
-  double *Fo = F + (k * nF) * g.n_ch + ch;
-#pragma unroll
-  for (int i = 0; i < N; ++i) Fo[i * g.n_ch] = z[i];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    double acc = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) acc = fma(kc.T[i * MAX_N + j], u[j], acc);
-    Fo[(N + i) * g.n_ch] = acc;
+  // full slices 1..nfull-1, two per iteration (static stage indices)
+  int sl = 1;
+  for (; sl + 1 < nfull; sl += 2) {
+    LFD_FULL_SLICE(stB, sl);
+    LFD_FULL_SLICE(stA, sl + 1);
   }
-  double p0 = kc.d0 * yf0;
+  bool next_in_A = false;  // stage holding slice `sl`
+  if (sl < nfull) {
+    LFD_FULL_SLICE(stB, sl);
+    ++sl;
+    next_in_A = true;
+  }
+  // partial last slice
+  if (rem4 && nfull >= 1) {
+    if (next_in_A) {
 #pragma unroll
-  for (int j = 0; j < N; ++j) p0 = fma(kc.cp[j], u[j], p0);
-  Fo[2 * N * g.n_ch] = p0;
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<f4v *>(wr[i]) = stA[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<f4v *>(wr[i]) = stB[i];
+    }
+#pragma unroll
+    for (int j = 0; j < TS / 4; ++j) {
+      if (j < rem4) {
+        const f4v v = *reinterpret_cast<const f4v *>(rd + 4 * j);
+        LFD_QUAD(v);
+      }
+    }
+  }
+#undef LFD_FULL_SLICE
+#undef LFD_STAGE
+#undef LFD_QUAD
+  if (live) store_functionals<NS>(kc, S, u, y0, F, k, ch, g.n_ch);
+}
+
+// ---------------------------------------------------------------------------
+// k_block_functionals_gen — any strides.  Workgroup = 64 channels x 4 blocks;
+// a wave is 64 consecutive channels of one block, so a load is 64 consecutive
+// floats when s_ch == 1 (the real-file ("time","distance") layout).  A ring of
+// D samples per lane stays in flight (clamped indices, branch-free body).
+// ---------------------------------------------------------------------------
+template <int NS, bool FIR32>
+__global__ __launch_bounds__(256) void k_block_functionals_gen(
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, const BlockConst kc,
+    double *__restrict__ F) {
+  constexpr int N = 2 * NS;
+  constexpr int J = 2 * NS;
+  constexpr int D = 8;
+  const int64_t n_ct = (g.n_ch + 63) / 64;
+  const int64_t tile = blockIdx.x;
+  const int64_t ct = tile % n_ct, kt = tile / n_ct;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t ch = ct * 64 + lane;
+  const int64_t k = kt * 4 + wave;
+  if (ch >= g.n_ch || k >= g.nb) return;
+  RRec<NS, FIR32> rec;
+  rec.load(kc.r);
+  double S[N], u[N], y0[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) S[i] = u[i] = y0[i] = 0.0;
+  const int L = g.L;
+  const int64_t a = g.base + k * (int64_t)L;
+  const float *row = x + ch * s_ch;
+  float h[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) h[j] = (a - 1 - j >= 0) ? row[(a - 1 - j) * s_t] : 0.0f;
+  const float *p = row + a * s_t;
+  float buf[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) buf[d] = p[(int64_t)min(d, L - 1) * s_t];
+  const int Gn = L / D;
+  for (int gi = 0; gi < Gn; ++gi) {
+    const int nxt = (gi + 1) * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float v = buf[d];
+      buf[d] = p[(int64_t)min(nxt + d, L - 1) * s_t];
+      double yv;
+      LFD_R_SAMPLE(rec, v, h, S, u, yv);
+      if (gi == 0 && d < J) y0[d < J ? d : 0] = yv;
+    }
+  }
+  const int rem = L - Gn * D;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    if (d < rem) {
+      double yv;
+      LFD_R_SAMPLE(rec, buf[d], h, S, u, yv);
+      const int m = Gn * D + d;
+      if (m < J) y0[m < J ? m : 0] = yv;
+    }
+  }
+  store_functionals<NS>(kc, S, u, y0, F, k, ch, g.n_ch);
 }
 
 // ---------------------------------------------------------------------------
 // k_chunk_scan: one thread per (chunk, channel), channel fastest.
 // ---------------------------------------------------------------------------
 template <int NS>
+struct SeqR {  // sequential realization-R steps in float64 (edges)
+  static constexpr int J = 2 * NS;
+  const RCoef &r;
+  __device__ explicit SeqR(const RCoef &rr) : r(rr) {}
+  __device__ __forceinline__ double fwd(double (&S)[2 * NS], double (&h)[J], double xv) const {
+    double w = xv;
+#pragma unroll
+    for (int j = 1; j <= J; ++j) w = fma(r.c64[j], h[j - 1], w);
+#pragma unroll
+    for (int j = J - 1; j > 0; --j) h[j] = h[j - 1];
+    h[0] = xv;
+    double v = w;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double vn = fma(r.na1[s], S[2 * s], fma(r.na2[s], S[2 * s + 1], v));
+      S[2 * s + 1] = S[2 * s];
+      S[2 * s] = vn;
+      v = vn;
+    }
+    return r.G * v;  // y_f
+  }
+  __device__ __forceinline__ double rev(double (&T)[2 * NS], double y) const {
+    double v = y;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double qn = fma(r.na1[s], T[2 * s], fma(r.na2[s], T[2 * s + 1], v));
+      T[2 * s + 1] = T[2 * s];
+      T[2 * s] = qn;
+      v = qn;
+    }
+    return v;  // q_last
+  }
+  // steady state of the cascade for a constant input c (what SciPy's
+  // sosfilt_zi * c encodes): every section at v = c * csum * prod dcg
+  __device__ __forceinline__ double steady(double (&S)[2 * NS], double c, bool with_fir) const {
+    double v = with_fir ? c * r.csum : c;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      v *= r.dcg[s];
+      S[2 * s] = S[2 * s + 1] = v;
+    }
+    return v;
+  }
+};
+
+template <int NS>
 __global__ __launch_bounds__(256) void k_chunk_scan(
-    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g,
-    int padlen, const ScanConst sc,
-    const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
-    const double *__restrict__ F, double *__restrict__ SF,
-    double *__restrict__ TP, int64_t tp_len, float *__restrict__ y,
-    int64_t ys_ch, int64_t ys_t) {
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
+    const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
+    const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
+    int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = 2 * NS;
+  constexpr int J = 2 * NS;
+  constexpr int NF = 2 * N + 1;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n_thr = n_chunks * g.n_ch;
   if (tid >= n_thr) return;
@@ -471,90 +449,119 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   const int64_t c = tid / g.n_ch;
   const ChunkGeom G = cgs[c];
   const float *xc = x + ch * s_ch;
-  const int64_t nF = 2 * N + 1;
   const int E = padlen;
+  const SeqR<NS> R(sc.r);
+  (void)tp_len;
 
-  FwdRec<NS> fr;
-  fr.load(sc.f);
-
-  // ---- left edge: odd extension (float32 arithmetic like numpy), zi*ext[0]
-  double s[N];
+  // ---- left edge: odd extension (float32 like numpy), steady state of ext[0]
+  double S[N], h[J];
   const float xl = xc[G.s0 * s_t];
-  if (E > 0) {
-    const double e0 = (double)(2.0f * xl - xc[(G.s0 + E) * s_t]);
+  {
+    const double e0 = E > 0 ? (double)(2.0f * xl - xc[(G.s0 + E) * s_t]) : (double)xl;
+    R.steady(S, e0, true);
 #pragma unroll
-    for (int i = 0; i < N; ++i) s[i] = sc.zi[i] * e0;
-    for (int i = 0; i < E; ++i) {
-      const double e = (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]);
-      fr.step(s, e);
+    for (int j = 0; j < J; ++j) h[j] = e0;
+    for (int i = 0; i < E; ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
+  }
+  for (int64_t t = G.s0; t < G.head_end; ++t) R.fwd(S, h, (double)xc[t * s_t]);
+
+  // ---- FIR-history correction of block kb: K1 used the raw samples before
+  // head_end (0 before the channel start); this chunk saw pad / head values.
+  double corr[NF];
+  {
+    double dh[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int64_t t = G.head_end - 1 - j;
+      dh[j] = h[j] - (t >= 0 ? (double)xc[t * s_t] : 0.0);
     }
-  } else {
-    const double e0 = (double)xl;
+    double dw[J];
 #pragma unroll
-    for (int i = 0; i < N; ++i) s[i] = sc.zi[i] * e0;
+    for (int m = 0; m < J; ++m) {
+      double acc = 0.0;
+#pragma unroll
+      for (int jj = m + 1; jj <= J; ++jj) acc = fma(sc.r.c64[jj], dh[jj - m - 1], acc);
+      dw[m] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < J; ++m) acc = fma(sc.Kc[i * MAX_J + m], dw[m], acc);
+      corr[i] = acc;
+    }
   }
-  // head samples (before the first full block): forward values kept in TP
-  double *tp = TP + tid;
-  int64_t ntp = 0;
-  double ylast = 0.0;
-  for (int64_t t = G.s0; t < G.head_end; ++t) {
-    ylast = fr.step(s, (double)xc[t * s_t]);
-    tp[(ntp++) * n_thr] = ylast;
-  }
-  const int64_t nhead = ntp;
 
   // ---- forward scan over the full blocks
+  const int64_t nF = NF;
   for (int64_t k = G.kb; k < G.ke; ++k) {
     double *sf = SF + ((G.sf_off + (k - G.kb)) * N) * g.n_ch + ch;
     const double *f = F + (k * nF) * g.n_ch + ch;
     double ns[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      sf[i * g.n_ch] = s[i];
-      double acc = f[i * g.n_ch];
+      sf[i * g.n_ch] = S[i];
+      double acc = f[i * g.n_ch] + (k == G.kb ? corr[i] : 0.0);
 #pragma unroll
-      for (int j = 0; j < N; ++j) acc = fma(sc.Phi[i * MAX_N + j], s[j], acc);
+      for (int j = 0; j < N; ++j) acc = fma(sc.PhiF[i * MAX_N + j], S[j], acc);
       ns[i] = acc;
     }
 #pragma unroll
-    for (int i = 0; i < N; ++i) s[i] = ns[i];
+    for (int i = 0; i < N; ++i) S[i] = ns[i];
   }
 
   // ---- right edge: tail samples + odd extension, forward, stored
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int64_t t = G.tail_begin - 1 - j;
+    h[j] = (double)xc[t * s_t];
+  }
+  double *tp = TP + tid;
+  int64_t ntp = 0;
+  double ylast = 0.0;
   for (int64_t t = G.tail_begin; t <= G.s1; ++t) {
-    ylast = fr.step(s, (double)xc[t * s_t]);
+    ylast = R.fwd(S, h, (double)xc[t * s_t]);
     tp[(ntp++) * n_thr] = ylast;
   }
   const float xr = xc[G.s1 * s_t];
   for (int i = 0; i < E; ++i) {
-    const double e = (double)(2.0f * xr - xc[(G.s1 - 1 - i) * s_t]);
-    ylast = fr.step(s, e);
+    ylast = R.fwd(S, h, (double)(2.0f * xr - xc[(G.s1 - 1 - i) * s_t]));
     tp[(ntp++) * n_thr] = ylast;
   }
-  (void)tp_len;
 
-  // ---- reverse pass over pad + tail, from zi * y_f[-1]
-  double r[N];
+  // ---- reverse pass over pad + tail from the steady state of y_f[-1]
+  double T[N], qw[J];  // qw[j] = q_last[m+1+j] (future values for the FIR)
+  {
+    const double qss = R.steady(T, ylast, false);
 #pragma unroll
-  for (int i = 0; i < N; ++i) r[i] = sc.zi[i] * ylast;
-  for (int64_t i = ntp - 1; i >= nhead; --i) {
-    const double v = fr.step(r, tp[i * n_thr]);
-    if (G.tail_out_j >= 0 && G.tail_begin + (i - nhead) == G.tail_out_pos)
-      y[ch * ys_ch + G.tail_out_j * ys_t] = (float)v;
+    for (int j = 0; j < J; ++j) qw[j] = qss;
+  }
+  for (int64_t i = ntp - 1; i >= 0; --i) {
+    const double q = R.rev(T, tp[i * n_thr]);
+    if (G.tail_out_j >= 0 && G.tail_begin + i == G.tail_out_pos) {
+      double acc = q;  // c[0] = 1
+#pragma unroll
+      for (int j = 1; j <= J; ++j) acc = fma(sc.r.c64[j], qw[j - 1], acc);
+      y[ch * ys_ch + G.tail_out_j * ys_t] = (float)(sc.r.G * acc);
+    }
+#pragma unroll
+    for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
+    qw[0] = q;
   }
 
   // ---- backward scan, outputs at block starts
   for (int64_t k = G.ke - 1; k >= G.kb; --k) {
     const double *sf = SF + ((G.sf_off + (k - G.kb)) * N) * g.n_ch + ch;
     const double *f = F + (k * nF) * g.n_ch + ch;
+    const bool first = (k == G.kb);
     double sfv[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) sfv[i] = sf[i * g.n_ch];
     if (k >= G.kout0 && k < G.kout1) {
-      double acc = f[2 * N * g.n_ch];
+      double acc = f[2 * N * g.n_ch] + (first ? corr[2 * N] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        acc = fma(sc.H0[j], r[j], acc);
+        acc = fma(sc.H0[j], T[j], acc);
         acc = fma(sc.G0[j], sfv[j], acc);
       }
       y[ch * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t] = (float)acc;
@@ -562,27 +569,16 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     double nr[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      double acc = f[(N + i) * g.n_ch];
+      double acc = f[(N + i) * g.n_ch] + (first ? corr[N + i] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        acc = fma(sc.Phi[i * MAX_N + j], r[j], acc);
+        acc = fma(sc.PhiR[i * MAX_N + j], T[j], acc);
         acc = fma(sc.M[i * MAX_N + j], sfv[j], acc);
       }
       nr[i] = acc;
     }
 #pragma unroll
-    for (int i = 0; i < N; ++i) r[i] = nr[i];
-  }
-
-  // ---- reverse pass through the head samples (only if one is an output)
-  if (G.head_out_j >= 0) {
-    for (int64_t i = nhead - 1; i >= 0; --i) {
-      const double v = fr.step(r, tp[i * n_thr]);
-      if (G.s0 + i == G.head_out_pos) {
-        y[ch * ys_ch + G.head_out_j * ys_t] = (float)v;
-        break;
-      }
-    }
+    for (int i = 0; i < N; ++i) T[i] = nr[i];
   }
 }
 
@@ -721,59 +717,50 @@ inline bool getenv_flag(const char *name) {
   return v && v[0] && v[0] != '0';
 }
 
-template <int NS>
-hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t,
-                                const BlockGeom &g, const BlockConst &kc,
-                                double *F, hipStream_t st) {
-  const bool tc = (s_t == 1);
-  const bool vec = tc && (g.L % 4 == 0) && (g.base % 4 == 0) &&
-                   (s_ch % 4 == 0) &&
-                   ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
-  if (tc && vec && !getenv_flag("LFD_K1_NOLDS")) {
+template <int NS, bool FIR32>
+hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
+                                const BlockConst &kc, double *F, hipStream_t st) {
+  const bool lds = (s_t == 1) && (g.L % 4 == 0) && (g.base % 4 == 0) && (s_ch % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && !getenv_flag("LFD_K1_NOLDS");
+  if (lds) {
     const int64_t tiles = ((g.n_ch + 15) / 16) * ((g.nb + 15) / 16);
-    k_block_functionals_lds<NS><<<dim3((unsigned)tiles), 256, 0, st>>>(x, s_ch, g, kc, F);
-  } else if (tc) {
-    const int64_t tiles = ((g.n_ch + 15) / 16) * ((g.nb + 16 * RB - 1) / (16 * RB));
-    if (vec)
-      k_block_functionals<NS, 0, true><<<dim3((unsigned)tiles), 256, 0, st>>>(
-          x, s_ch, s_t, g, kc, F);
-    else
-      k_block_functionals<NS, 0, false><<<dim3((unsigned)tiles), 256, 0, st>>>(
-          x, s_ch, s_t, g, kc, F);
+    k_block_functionals_lds<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(x, s_ch, g, kc, F);
   } else {
-    const int64_t tiles = ((g.n_ch + 63) / 64) * ((g.nb + 4 * RB - 1) / (4 * RB));
-    k_block_functionals<NS, 1, false><<<dim3((unsigned)tiles), 256, 0, st>>>(
-        x, s_ch, s_t, g, kc, F);
+    const int64_t tiles = ((g.n_ch + 63) / 64) * ((g.nb + 3) / 4);
+    k_block_functionals_gen<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(x, s_ch, s_t, g,
+                                                                             kc, F);
   }
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_block_functionals(int n_sec, const float *x, int64_t s_ch,
-                                    int64_t s_t, const BlockGeom &g,
-                                    const BlockConst &kc, double *F,
-                                    hipStream_t st) {
+hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
+                                    int64_t s_t, const BlockGeom &g, const BlockConst &kc,
+                                    double *F, hipStream_t st) {
+#define LFD_BF(NS)                                                        \
+  return fir32 ? block_functionals_ns<NS, true>(x, s_ch, s_t, g, kc, F, st) \
+               : block_functionals_ns<NS, false>(x, s_ch, s_t, g, kc, F, st)
   switch (n_sec) {
-    case 1: return block_functionals_ns<1>(x, s_ch, s_t, g, kc, F, st);
-    case 2: return block_functionals_ns<2>(x, s_ch, s_t, g, kc, F, st);
-    case 3: return block_functionals_ns<3>(x, s_ch, s_t, g, kc, F, st);
-    case 4: return block_functionals_ns<4>(x, s_ch, s_t, g, kc, F, st);
+    case 1: LFD_BF(1);
+    case 2: LFD_BF(2);
+    case 3: LFD_BF(3);
+    case 4: LFD_BF(4);
   }
+#undef LFD_BF
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_chunk_scan(int n_sec, const float *x, int64_t s_ch,
-                             int64_t s_t, const BlockGeom &g, int padlen,
-                             const ScanConst &sc, const ChunkGeom *cg,
-                             int64_t n_chunks, const double *F, double *SF,
-                             double *TP, int64_t tp_len, float *y,
-                             int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch, int64_t s_t,
+                             const BlockGeom &g, int padlen, const ScanConst &sc,
+                             const ChunkGeom *cg, int64_t n_chunks, const double *F, double *SF,
+                             double *TP, int64_t tp_len, float *y, int64_t ys_ch, int64_t ys_t,
+                             hipStream_t st) {
+  (void)fir32;
   const unsigned nb = nblk(n_chunks * g.n_ch, 256);
-#define LFD_SCAN(NS)                                                         \
-  k_chunk_scan<NS><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg,     \
-                                        n_chunks, F, SF, TP, tp_len, y, ys_ch, \
-                                        ys_t)
+#define LFD_SCAN(NS)                                                                  \
+  k_chunk_scan<NS><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, F, SF, TP, \
+                                        tp_len, y, ys_ch, ys_t)
   switch (n_sec) {
     case 1: LFD_SCAN(1); break;
     case 2: LFD_SCAN(2); break;

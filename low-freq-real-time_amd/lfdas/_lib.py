@@ -26,18 +26,19 @@ MAX_N = 2 * MAX_SEC
 
 # numpy mirrors of the internal kernel-constant structs (csrc/lfd_internal.h),
 # used only by lfd_debug_plan_constants in tests.
-_SOS = [("b0", "f8", MAX_SEC), ("b1", "f8", MAX_SEC), ("b2", "f8", MAX_SEC),
-        ("a1", "f8", MAX_SEC), ("a2", "f8", MAX_SEC)]
-BLOCK_CONST_DTYPE = np.dtype(_SOS + [
-    ("ia2", "f8", MAX_SEC), ("ra", "f8", MAX_SEC), ("beta0", "f8", MAX_SEC),
-    ("beta1", "f8", MAX_SEC), ("Bv", "f8", MAX_N), ("T", "f8", (MAX_N, MAX_N)),
-    ("cp", "f8", MAX_N), ("d0", "f8")])
-SCAN_CONST_DTYPE = np.dtype(_SOS + [
-    ("zi", "f8", MAX_N), ("Phi", "f8", (MAX_N, MAX_N)), ("M", "f8", (MAX_N, MAX_N)),
-    ("G0", "f8", MAX_N), ("H0", "f8", MAX_N)])
+MAX_J = 2 * MAX_SEC
+_RCOEF = np.dtype([("na1", "f8", MAX_SEC), ("na2", "f8", MAX_SEC), ("nia2", "f8", MAX_SEC),
+                   ("nra", "f8", MAX_SEC), ("dcg", "f8", MAX_SEC), ("c64", "f8", MAX_J + 1),
+                   ("c32", "f4", MAX_J + 1), ("G", "f8"), ("csum", "f8")], align=True)
+BLOCK_CONST_DTYPE = np.dtype([("r", _RCOEF), ("T", "f8", (MAX_N, MAX_N)), ("cp", "f8", MAX_N),
+                              ("dp", "f8", MAX_J)], align=True)
+SCAN_CONST_DTYPE = np.dtype([("r", _RCOEF), ("PhiF", "f8", (MAX_N, MAX_N)),
+                             ("PhiR", "f8", (MAX_N, MAX_N)), ("M", "f8", (MAX_N, MAX_N)),
+                             ("G0", "f8", MAX_N), ("H0", "f8", MAX_N),
+                             ("Kc", "f8", (2 * MAX_N + 1, MAX_J))], align=True)
 CHUNK_GEOM_DTYPE = np.dtype([(n, "i8") for n in (
     "s0", "s1", "kb", "ke", "head_end", "tail_begin", "kout0", "kout1", "jout0",
-    "sf_off", "head_out_pos", "head_out_j", "tail_out_pos", "tail_out_j")])
+    "sf_off", "tail_out_pos", "tail_out_j")])
 
 
 class LFDLibraryError(RuntimeError):

@@ -1,75 +1,136 @@
-"""Test-side NumPy model of the two device kernels (k_block_functionals and
-k_chunk_scan), driven by the constants a host-only plan computed in C++
-(``lfd_debug_plan_constants``).  It lets the CPU suite check the plan's host
-math (state-space matrices, zi, chunk geometry) against the oracle without a
-GPU.  Not product code."""
+"""Test-side NumPy model of the two device kernels (k_block_functionals_* and
+k_chunk_scan, realization R of csrc/lfd_internal.h), driven by the constants
+a host-only plan computed in C++ (``lfd_debug_plan_constants``).  It lets the
+CPU suite check the plan's host math (state-space matrices, p0 coefficients,
+FIR-history correction, chunk geometry) against SciPy's golden vectors
+without a GPU.  Not product code."""
 import numpy as np
 
 
-def emulate(plan, x, padlen):
+def emulate(plan, x, padlen, fir32=True):
     bc, sc, cg = plan.constants()
-    ns = plan.n_sec; n = 2*ns; L = plan.block_len
+    ns = plan.n_sec
+    n = 2 * ns
+    J = 2 * ns
+    L = plan.block_len
+    r = bc["r"]
+    na1, na2, nia2, nra = r["na1"][:ns], r["na2"][:ns], r["nia2"][:ns], r["nra"][:ns]
+    c64 = r["c64"][:J + 1]
+    c32 = r["c32"][:J + 1]
+    G = float(r["G"])
     n_ch, n_t = x.shape
-    f = dict(b0=bc['b0'][:ns], b1=bc['b1'][:ns], b2=bc['b2'][:ns], a1=bc['a1'][:ns], a2=bc['a2'][:ns])
-    def fstep(z, v):
-        for i in range(ns):
-            vi = f['b0'][i]*v + z[2*i]
-            z[2*i] = f['b1'][i]*v - f['a1'][i]*vi + z[2*i+1]
-            z[2*i+1] = f['b2'][i]*v - f['a2'][i]*vi
-            v = vi
-        return v
-    def istep(u, y):
-        g = 0.0
-        for i in range(ns):
-            t0, t1 = u[2*i], u[2*i+1]
-            if i > 0: t0 = t0 - bc['beta0'][i]*g; t1 = t1 - bc['beta1'][i]*g
-            w0 = -bc['ia2'][i]*t1; w1 = t0 - bc['ra'][i]*t1
-            if i+1 < ns: g = w0 if i == 0 else bc['b0'][i]*g + w0
-            u[2*i] = bc['Bv'][2*i]*y + w0; u[2*i+1] = bc['Bv'][2*i+1]*y + w1
-    # K1 (vectorised over channels and blocks)
-    nb = plan.n_blocks; base = None
-    # recover base from chunk geometry: head_end = base + kb*L
-    base = cg[0]['head_end'] - cg[0]['kb']*L
-    X = np.stack([x[:, base + k*L: base + (k+1)*L] for k in range(nb)], 1).astype(np.float64)  # ch, nb, L
-    z = np.zeros((n,)+X.shape[:2]); u = np.zeros((n,)+X.shape[:2])
-    yf0 = None
+    nb = plan.n_blocks
+    base = int(cg[0]["head_end"] - cg[0]["kb"] * L)
+    # ---------------- K1 (vectorised over channels x blocks)
+    X = np.stack([x[:, base + k * L: base + (k + 1) * L] for k in range(nb)], 1)
+    H = np.zeros((J, n_ch, nb), np.float32)
+    for k in range(nb):
+        for j in range(J):
+            t = base + k * L - 1 - j
+            H[j, :, k] = x[:, t] if t >= 0 else 0.0
+    S = np.zeros((n, n_ch, nb))
+    u = np.zeros((n, n_ch, nb))
+    y0 = np.zeros((J, n_ch, nb))
     for m in range(L):
-        yv = fstep(z, X[:, :, m])
-        if m == 0: yf0 = yv.copy()
-        istep(u, yv)
-    T = bc['T'][:n, :n]; er0 = np.einsum('ij,jab->iab', T, u)
-    p0 = bc['d0']*yf0 + np.einsum('j,jab->ab', bc['cp'][:n], u)
-    # K2
+        xm = X[:, :, m]
+        if fir32:
+            w = xm.astype(np.float32)
+            for j in range(1, J + 1):
+                w = (np.float32(c32[j]) * H[j - 1] + w).astype(np.float32)
+            w = w.astype(np.float64)
+        else:
+            w = xm.astype(np.float64) + sum(c64[j] * H[j - 1].astype(np.float64) for j in range(1, J + 1))
+        H[1:] = H[:-1].copy()
+        H[0] = xm
+        v = w
+        for s in range(ns):
+            vn = na1[s] * S[2 * s] + na2[s] * S[2 * s + 1] + v
+            S[2 * s + 1] = S[2 * s].copy()
+            S[2 * s] = vn
+            v = vn
+        if m < J:
+            y0[m] = v
+        t = u.copy()
+        for s in range(ns):
+            d = t[0] if s == 0 else t[2 * s] - t[2 * s - 2]
+            u[2 * s] = t[2 * s + 1] + v
+            u[2 * s + 1] = nia2[s] * d + nra[s] * t[2 * s + 1]
+    ef = S
+    er0 = np.einsum("ij,jab->iab", bc["T"][:n, :n], u)
+    p0 = np.einsum("j,jab->ab", bc["cp"][:n], u) + np.einsum("m,mab->ab", bc["dp"][:J], y0)
+    # ---------------- K2
+    PhiF, PhiR, M = sc["PhiF"][:n, :n], sc["PhiR"][:n, :n], sc["M"][:n, :n]
+    G0, H0, Kc = sc["G0"][:n], sc["H0"][:n], sc["Kc"][: 2 * n + 1, :J]
     y = np.full((n_ch, plan.n_grid), np.nan, np.float32)
     E = padlen
-    Phi = sc['Phi'][:n,:n]; M = sc['M'][:n,:n]; zi = sc['zi'][:n]
-    for G in cg:
-        s0, s1 = G['s0'], G['s1']
-        xl = x[:, s0]
-        e0 = (2*xl - x[:, s0+E]).astype(np.float32).astype(np.float64)
-        s = zi[:, None]*e0[None]
-        for i in range(E):
-            fstep(s, (2*xl - x[:, s0+E-i]).astype(np.float32).astype(np.float64))
-        tp = []
-        for t in range(s0, G['head_end']): tp.append(fstep(s, x[:, t].astype(np.float64)))
-        nhead = len(tp)
-        SF = {}
-        for k in range(G['kb'], G['ke']):
-            SF[k] = s.copy(); s = Phi@s + z[:, :, k]
-        for t in range(G['tail_begin'], s1+1): tp.append(fstep(s, x[:, t].astype(np.float64)))
-        xr = x[:, s1]
-        for i in range(E): tp.append(fstep(s, (2*xr - x[:, s1-1-i]).astype(np.float32).astype(np.float64)))
-        r = zi[:, None]*tp[-1][None]
-        for i in range(len(tp)-1, nhead-1, -1):
-            v = fstep(r, tp[i])
-            if G['tail_out_j'] >= 0 and G['tail_begin'] + (i-nhead) == G['tail_out_pos']: y[:, G['tail_out_j']] = v
-        for k in range(G['ke']-1, G['kb']-1, -1):
-            if G['kout0'] <= k < G['kout1']:
-                y[:, G['jout0'] + k - G['kout0']] = p0[:, k] + sc['H0'][:n]@r + sc['G0'][:n]@SF[k]
-            r = Phi@r + er0[:, :, k] + M@SF[k]
-        if G['head_out_j'] >= 0:
-            for i in range(nhead-1, -1, -1):
-                v = fstep(r, tp[i])
-                if s0 + i == G['head_out_pos']: y[:, G['head_out_j']] = v; break
-    return y
 
+    def fwd(Sf, h, xv):
+        w = xv + sum(c64[j] * h[j - 1] for j in range(1, J + 1))
+        h[1:] = h[:-1].copy()
+        h[0] = xv
+        v = w
+        for s in range(ns):
+            vn = na1[s] * Sf[2 * s] + na2[s] * Sf[2 * s + 1] + v
+            Sf[2 * s + 1] = Sf[2 * s].copy()
+            Sf[2 * s] = vn
+            v = vn
+        return G * v
+
+    def rev(T, yv):
+        v = yv
+        for s in range(ns):
+            qn = na1[s] * T[2 * s] + na2[s] * T[2 * s + 1] + v
+            T[2 * s + 1] = T[2 * s].copy()
+            T[2 * s] = qn
+            v = qn
+        return v
+
+    def steady(c, with_fir):
+        v = c * float(r["csum"]) if with_fir else c
+        St = np.zeros((n,) + np.shape(c))
+        for s in range(ns):
+            v = v * r["dcg"][s]
+            St[2 * s] = v
+            St[2 * s + 1] = v
+        return St, v
+
+    for Gc in cg:
+        s0, s1 = int(Gc["s0"]), int(Gc["s1"])
+        kb, ke = int(Gc["kb"]), int(Gc["ke"])
+        xl = x[:, s0]
+        e0 = (2 * xl - x[:, s0 + E]).astype(np.float32).astype(np.float64)
+        Sf, _ = steady(e0, True)
+        h = np.stack([e0] * J, 0)
+        for i in range(E):
+            fwd(Sf, h, (2 * xl - x[:, s0 + E - i]).astype(np.float32).astype(np.float64))
+        for t in range(s0, int(Gc["head_end"])):
+            fwd(Sf, h, x[:, t].astype(np.float64))
+        he = int(Gc["head_end"])
+        raw = np.stack([x[:, he - 1 - j] if he - 1 - j >= 0 else np.zeros(n_ch) for j in range(J)], 0)
+        dh = h - raw.astype(np.float64)
+        dw = np.stack([sum(c64[jj] * dh[jj - m - 1] for jj in range(m + 1, J + 1)) for m in range(J)], 0)
+        corr = Kc @ dw
+        SFs = {}
+        for k in range(kb, ke):
+            SFs[k] = Sf.copy()
+            Sf = PhiF @ Sf + ef[:, :, k] + (corr[:n] if k == kb else 0)
+        tb = int(Gc["tail_begin"])
+        h = np.stack([x[:, tb - 1 - j] for j in range(J)], 0).astype(np.float64)
+        tp = [fwd(Sf, h, x[:, t].astype(np.float64)) for t in range(tb, s1 + 1)]
+        xr = x[:, s1]
+        for i in range(E):
+            tp.append(fwd(Sf, h, (2 * xr - x[:, s1 - 1 - i]).astype(np.float32).astype(np.float64)))
+        T, qss = steady(tp[-1], False)
+        qw = [qss] * J
+        for i in range(len(tp) - 1, -1, -1):
+            q = rev(T, tp[i])
+            if Gc["tail_out_j"] >= 0 and tb + i == Gc["tail_out_pos"]:
+                y[:, Gc["tail_out_j"]] = G * (q + sum(c64[j] * qw[j - 1] for j in range(1, J + 1)))
+            qw = [q] + qw[:-1]
+        for k in range(ke - 1, kb - 1, -1):
+            sf = SFs[k]
+            if Gc["kout0"] <= k < Gc["kout1"]:
+                pk = p0[:, k] + (corr[2 * n] if k == kb else 0)
+                y[:, Gc["jout0"] + k - Gc["kout0"]] = pk + H0 @ T + G0 @ sf
+            T = PhiR @ T + er0[:, :, k] + (corr[n:2 * n] if k == kb else 0) + M @ sf
+    return y
