@@ -123,9 +123,11 @@ struct RRec {
     for (int i = 0; i < 2 * NS; ++i) t[i] = u[i];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
+      // loop-carried chain through u[2s+1] is a single FMA: the nia2*d
+      // product depends only on the previous step's u[2s] (ready earlier)
       const double d = s == 0 ? t[0] : t[2 * s] - t[2 * s - 2];
       u[2 * s] = t[2 * s + 1] + y;
-      u[2 * s + 1] = fma(nia2[s], d, nra[s] * t[2 * s + 1]);
+      u[2 * s + 1] = fma(nra[s], t[2 * s + 1], nia2[s] * d);
     }
   }
 };
@@ -141,9 +143,9 @@ struct RRec {
 // Block epilogue: e_f, e_r0 = T u, p0 = cp.u + dp.y0
 template <int NS>
 __device__ __forceinline__ void store_functionals(const BlockConst &kc, const double (&S)[2 * NS],
-                                                  const double (&u)[2 * NS],
-                                                  const double (&y0)[2 * NS], double *F,
-                                                  int64_t k, int64_t ch, int64_t n_ch) {
+                                                  const double (&u)[2 * NS], double p0y,
+                                                  double *F, int64_t k, int64_t ch,
+                                                  int64_t n_ch) {
   constexpr int N = 2 * NS;
   const int64_t nF = 2 * N + 1;
   double *Fo = F + (k * nF) * n_ch + ch;
@@ -156,11 +158,9 @@ __device__ __forceinline__ void store_functionals(const BlockConst &kc, const do
     for (int j = 0; j < N; ++j) acc = fma(kc.T[i * MAX_N + j], u[j], acc);
     Fo[(N + i) * n_ch] = acc;
   }
-  double p0 = 0.0;
+  double p0 = p0y;  // sum_m dp[m] y0[m], accumulated during the first samples
 #pragma unroll
   for (int j = 0; j < N; ++j) p0 = fma(kc.cp[j], u[j], p0);
-#pragma unroll
-  for (int m = 0; m < N; ++m) p0 = fma(kc.dp[m], y0[m], p0);
   Fo[2 * N * n_ch] = p0;
 }
 
@@ -179,17 +179,32 @@ __device__ __forceinline__ void store_functionals(const BlockConst &kc, const do
 constexpr int TS = 16;       // samples per row per slice
 constexpr int TSP = TS + 4;  // padded LDS row stride (floats)
 
+#ifndef LFD_K1_MINW
+#define LFD_K1_MINW 4  // waves/SIMD the LDS kernel's register budget must allow
+#endif
+
 template <int NS, bool FIR32>
-__global__ __launch_bounds__(256) void k_block_functionals_lds(
+__global__ __launch_bounds__(256, LFD_K1_MINW) void k_block_functionals_lds(
     const float *__restrict__ x, int64_t s_ch, BlockGeom g, const BlockConst kc,
-    double *__restrict__ F) {
+    double *__restrict__ F, int chan_fast) {
   constexpr int N = 2 * NS;
   constexpr int J = 2 * NS;
   static_assert(J <= 4 * (TS / 4), "history must fit one slice");
   __shared__ __attribute__((aligned(16))) float lds_all[4][64 * TSP];
+  // tile order: time-fastest (default) keeps the resident workgroups on a few
+  // channel groups, so the pages in flight stay few (TLB); channel-fastest
+  // spreads them over every channel (LFD_K1_CHAN_FAST=1, for A/B).
   const int64_t n_ct = (g.n_ch + 15) / 16;
+  const int64_t n_kt = (g.nb + 15) / 16;
   const int64_t tile = blockIdx.x;
-  const int64_t ct = tile % n_ct, kt = tile / n_ct;
+  int64_t ct, kt;
+  if (chan_fast) {
+    ct = tile % n_ct;
+    kt = tile / n_ct;
+  } else {
+    kt = tile % n_kt;
+    ct = tile / n_kt;
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float *lds = lds_all[wave];
   const int L = g.L;
@@ -218,9 +233,9 @@ __global__ __launch_bounds__(256) void k_block_functionals_lds(
 
   RRec<NS, FIR32> rec;
   rec.load(kc.r);
-  double S[N], u[N], y0[N];
+  double S[N], u[N], p0y = 0.0;
 #pragma unroll
-  for (int i = 0; i < N; ++i) S[i] = u[i] = y0[i] = 0.0;
+  for (int i = 0; i < N; ++i) S[i] = u[i] = 0.0;
   // FIR history: the J samples before the block (0 before the channel start)
   float h[J];
   {
@@ -279,13 +294,13 @@ __global__ __launch_bounds__(256) void k_block_functionals_lds(
         const f4v v = *reinterpret_cast<const f4v *>(rd + 4 * j);
         double yv;
         LFD_R_SAMPLE(rec, v.x, h, S, u, yv);
-        if (4 * j + 0 < J) y0[4 * j + 0] = yv;
+        if (4 * j + 0 < J) p0y = fma(kc.dp[4 * j + 0], yv, p0y);
         LFD_R_SAMPLE(rec, v.y, h, S, u, yv);
-        if (4 * j + 1 < J) y0[4 * j + 1] = yv;
+        if (4 * j + 1 < J) p0y = fma(kc.dp[4 * j + 1], yv, p0y);
         LFD_R_SAMPLE(rec, v.z, h, S, u, yv);
-        if (4 * j + 2 < J) y0[4 * j + 2] = yv;
+        if (4 * j + 2 < J) p0y = fma(kc.dp[4 * j + 2], yv, p0y);
         LFD_R_SAMPLE(rec, v.w, h, S, u, yv);
-        if (4 * j + 3 < J) y0[4 * j + 3] = yv;
+        if (4 * j + 3 < J) p0y = fma(kc.dp[4 * j + 3], yv, p0y);
       }
     }
   }
@@ -321,7 +336,7 @@ __global__ __launch_bounds__(256) void k_block_functionals_lds(
 #undef LFD_FULL_SLICE
 #undef LFD_STAGE
 #undef LFD_QUAD
-  if (live) store_functionals<NS>(kc, S, u, y0, F, k, ch, g.n_ch);
+  if (live) store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.n_ch);
 }
 
 // ---------------------------------------------------------------------------
@@ -337,18 +352,18 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
   constexpr int N = 2 * NS;
   constexpr int J = 2 * NS;
   constexpr int D = 8;
-  const int64_t n_ct = (g.n_ch + 63) / 64;
+  const int64_t n_kt = (g.nb + 3) / 4;
   const int64_t tile = blockIdx.x;
-  const int64_t ct = tile % n_ct, kt = tile / n_ct;
+  const int64_t kt = tile % n_kt, ct = tile / n_kt;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t ch = ct * 64 + lane;
   const int64_t k = kt * 4 + wave;
   if (ch >= g.n_ch || k >= g.nb) return;
   RRec<NS, FIR32> rec;
   rec.load(kc.r);
-  double S[N], u[N], y0[N];
+  double S[N], u[N], p0y = 0.0;
 #pragma unroll
-  for (int i = 0; i < N; ++i) S[i] = u[i] = y0[i] = 0.0;
+  for (int i = 0; i < N; ++i) S[i] = u[i] = 0.0;
   const int L = g.L;
   const int64_t a = g.base + k * (int64_t)L;
   const float *row = x + ch * s_ch;
@@ -368,7 +383,7 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
       buf[d] = p[(int64_t)min(nxt + d, L - 1) * s_t];
       double yv;
       LFD_R_SAMPLE(rec, v, h, S, u, yv);
-      if (gi == 0 && d < J) y0[d < J ? d : 0] = yv;
+      if (gi == 0 && d < J) p0y = fma(kc.dp[d < J ? d : 0], yv, p0y);
     }
   }
   const int rem = L - Gn * D;
@@ -378,10 +393,10 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
       double yv;
       LFD_R_SAMPLE(rec, buf[d], h, S, u, yv);
       const int m = Gn * D + d;
-      if (m < J) y0[m < J ? m : 0] = yv;
+      if (m < J) p0y = fma(kc.dp[m < J ? m : 0], yv, p0y);
     }
   }
-  store_functionals<NS>(kc, S, u, y0, F, k, ch, g.n_ch);
+  store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.n_ch);
 }
 
 // ---------------------------------------------------------------------------
@@ -724,7 +739,8 @@ hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t, const
                    ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && !getenv_flag("LFD_K1_NOLDS");
   if (lds) {
     const int64_t tiles = ((g.n_ch + 15) / 16) * ((g.nb + 15) / 16);
-    k_block_functionals_lds<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(x, s_ch, g, kc, F);
+    k_block_functionals_lds<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(
+        x, s_ch, g, kc, F, getenv_flag("LFD_K1_CHAN_FAST") ? 1 : 0);
   } else {
     const int64_t tiles = ((g.n_ch + 63) / 64) * ((g.nb + 3) / 4);
     k_block_functionals_gen<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(x, s_ch, s_t, g,

@@ -54,7 +54,7 @@ def emulate(plan, x, padlen, fir32=True):
         for s in range(ns):
             d = t[0] if s == 0 else t[2 * s] - t[2 * s - 2]
             u[2 * s] = t[2 * s + 1] + v
-            u[2 * s + 1] = nia2[s] * d + nra[s] * t[2 * s + 1]
+            u[2 * s + 1] = nra[s] * t[2 * s + 1] + nia2[s] * d
     ef = S
     er0 = np.einsum("ij,jab->iab", bc["T"][:n, :n], u)
     p0 = np.einsum("j,jab->ab", bc["cp"][:n], u) + np.einsum("m,mab->ab", bc["dp"][:J], y0)
