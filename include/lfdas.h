@@ -94,6 +94,19 @@ int lfd_lowpass_last_timing(const lfd_lowpass_plan *plan, float *ms_blocks,
                             float *ms_scan);
 void lfd_lowpass_plan_destroy(lfd_lowpass_plan *plan);
 int lfd_set_timing(int enable);
+/* Which block-functional kernel the last execute ran: LFD_K1_MFMA (fp64
+ * matrix cores over the plan's block taps; time-contiguous float32 rows,
+ * 16-B aligned, channel stride a multiple of 4) or LFD_K1_RECURRENCE (any
+ * strides, or cascades above 6th order); 0 before the first execute. */
+#define LFD_K1_RECURRENCE 1
+#define LFD_K1_MFMA 2
+int lfd_lowpass_last_kernel(const lfd_lowpass_plan *plan);
+/* Testing hook: the plan's block taps Kx[n_comp][row_len] in natural layout,
+ * F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p] (row_len = L + J).  With
+ * taps == NULL only the sizes are returned.  LFD_EUNSUPPORTED when the plan
+ * runs the recurrence kernel only. */
+int lfd_debug_block_taps(const lfd_lowpass_plan *plan, double *taps, size_t n_taps,
+                         int *n_comp, int64_t *row_len);
 /* Testing hook (not a stable interface): copies the plan's kernel constants
  * (lfd::BlockConst, lfd::ScanConst, lfd::ChunkGeom[n_chunks] of
  * csrc/lfd_internal.h) so CPU tests can check the host math without a GPU.

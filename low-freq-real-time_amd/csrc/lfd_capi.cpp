@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -39,6 +40,11 @@ int fail(int code, const std::string &m) {
   } while (0)
 
 typedef long double R;
+
+bool env_flag(const char *name) {
+  const char *v = std::getenv(name);
+  return v && v[0] && v[0] != '0';
+}
 
 struct Cascade {
   int ns = 0;
@@ -337,6 +343,59 @@ int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanCons
   return LFD_OK;
 }
 
+// The 2n+1 block functionals are linear in the block's extended samples
+// x[a-J .. a+L-1] (J samples of FIR history): F_c = sum_p Kx[c][p] x[a-J+p].
+// Taps are computed in extended precision from impulse responses (O(L)):
+//   hS[t], hv[t]  state / v_last output t samples after a unit impulse;
+//   e_f  : Kw[i][k]    = hS[L-1-k][i]
+//   e_r0 : Kw[n+i][k]  = G sum_t hv[t] hS[k+t][i]                 (adjoint)
+//   p0   : Kw[2n][k]   = G^2 sum_t hv[t] z[k+t],  z[m] = sum_j c_j hv[m-j]
+// (sum_t hv[t] s[k+t] is the all-pole cascade run backward over s), and
+//   Kx[c][p] = sum_j c_j Kw[c][p-J+j].
+// Same definitions as sim_block (impulse at w[k], zero states).
+int block_taps(const Cascade &cs, int L, std::vector<long double> &Kx, int &nc, int &row) {
+  RModel m;
+  if (int e = make_rmodel(cs, m)) return e;
+  const int n = 2 * m.ns, J = m.J;
+  nc = 2 * n + 1;
+  row = L + J;
+  std::vector<R> hS((size_t)L * n), hv(L), Kw((size_t)nc * L, 0.0L);
+  {
+    R S[MAX_N] = {0};
+    for (int t = 0; t < L; ++t) {
+      hv[t] = r_allpole(m, S, t == 0 ? 1.0L : 0.0L);
+      for (int i = 0; i < n; ++i) hS[(size_t)t * n + i] = S[i];
+    }
+  }
+  auto backward = [&](const std::vector<R> &s, R scale, R *out) {
+    R T[MAX_N] = {0};
+    for (int k = L - 1; k >= 0; --k) out[k] = scale * r_allpole(m, T, s[k]);
+  };
+  std::vector<R> s(L);
+  for (int i = 0; i < n; ++i) {
+    for (int k = 0; k < L; ++k) Kw[(size_t)i * L + k] = hS[(size_t)(L - 1 - k) * n + i];
+    for (int k = 0; k < L; ++k) s[k] = hS[(size_t)k * n + i];
+    backward(s, m.G, &Kw[(size_t)(n + i) * L]);
+  }
+  for (int k = 0; k < L; ++k) {
+    R z = 0;
+    for (int j = 0; j <= J && j <= k; ++j) z += m.c[j] * hv[k - j];
+    s[k] = z;
+  }
+  backward(s, m.G * m.G, &Kw[(size_t)(2 * n) * L]);
+  Kx.assign((size_t)nc * row, 0.0L);
+  for (int c = 0; c < nc; ++c)
+    for (int p = 0; p < row; ++p) {
+      R acc = 0;
+      for (int j = 0; j <= J; ++j) {
+        const int k = p - J + j;
+        if (k >= 0 && k < L) acc += m.c[j] * Kw[(size_t)c * L + k];
+      }
+      Kx[(size_t)c * row + p] = acc;
+    }
+  return LFD_OK;
+}
+
 inline int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b;
   if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
@@ -357,10 +416,15 @@ struct lfd_lowpass_plan {
   bool fir32 = true;
   std::vector<lfd::ChunkGeom> chunks;
   lfd::ChunkGeom *d_chunks = nullptr;
+  // block taps for the MFMA block-functional kernel (empty: recurrence kernel)
+  std::vector<double> taps;      // natural layout [nc][L+J]
+  lfd::TapGeom tg{};
+  double *d_taps = nullptr;      // device layout (lfd_internal.h TapGeom)
   int64_t sf_blocks = 0, tp_len = 0;
   size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   mutable bool timed = false;
+  mutable int last_k1 = 0;
 };
 
 extern "C" {
@@ -483,6 +547,23 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     delete p;
     return e;
   }
+  if (2 * n + 1 <= 16) {
+    std::vector<long double> Kx;
+    int nc = 0, row = 0;
+    if (int e = block_taps(c, L, Kx, nc, row)) {
+      delete p;
+      return e;
+    }
+    const int J = 2 * n_sec;
+    const int nvar = L % 4 == 0 ? 1 : 4;
+    const int v0 = (int)(((p->bg.base - J) % 4 + 4) % 4);
+    const int Lp = (row + (nvar == 1 ? v0 : 3) + 63) / 64 * 64;
+    if ((size_t)Lp * nc * nvar * sizeof(double) <= (size_t)lfd::TAP_LDS_MAX) {
+      p->taps.resize(Kx.size());
+      for (size_t i = 0; i < Kx.size(); ++i) p->taps[i] = (double)Kx[i];
+      p->tg = lfd::TapGeom{Lp, J, nc, nvar, v0};
+    }
+  }
   p->off_F = 0;
   p->off_SF = align256(p->off_F + sizeof(double) * (size_t)p->bg.nF * p->bg.nb * n_ch);
   p->off_TP = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * n_ch);
@@ -501,6 +582,28 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   if (e == hipSuccess)
     e = hipMemcpy(p->d_chunks, p->chunks.data(), sizeof(lfd::ChunkGeom) * n_chunks,
                   hipMemcpyHostToDevice);
+  if (e == hipSuccess && !p->taps.empty()) {
+    // device layout (lfd_internal.h TapGeom): one table per row shift v
+    const lfd::TapGeom &tg = p->tg;
+    const int row = (int)(p->taps.size() / tg.nc);
+    const size_t tab = (size_t)tg.Lp * tg.nc;
+    std::vector<double> dev(tab * tg.nvar, 0.0);
+    for (int vi = 0; vi < tg.nvar; ++vi) {
+      const int v = tg.nvar == 1 ? tg.v0 : vi;
+      for (int t = 0; t < tg.Lp / 16; ++t)
+        for (int q = 0; q < 4; ++q)
+          for (int cc = 0; cc < tg.nc; ++cc)
+            for (int el = 0; el < 4; ++el) {
+              const int pos = 16 * t + 4 * q + el - v;
+              if (pos >= 0 && pos < row)
+                dev[vi * tab + ((size_t)(t * 4 + q) * tg.nc + cc) * 4 + el] =
+                    p->taps[(size_t)cc * row + pos];
+            }
+    }
+    e = hipMalloc(&p->d_taps, dev.size() * sizeof(double));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_taps, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice);
+  }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
   if (e != hipSuccess) {
     lfd_lowpass_plan_destroy(p);
@@ -536,7 +639,14 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   const bool timed = g_timing.load() != 0;
   p->timed = timed;
   if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
-  LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
+  // K1: fp64-MFMA block taps when the layout allows, else the recurrence
+  const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !env_flag("LFD_K1_REC");
+  p->last_k1 = mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE;
+  if (mfma)
+    LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, F, st));
+  else
+    LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
   if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
   LFD_HIP(lfd::launch_chunk_scan(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
                                  p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st));
@@ -571,9 +681,30 @@ int lfd_debug_plan_constants(const lfd_lowpass_plan *p, void *block_const, size_
   return LFD_OK;
 }
 
+int lfd_debug_block_taps(const lfd_lowpass_plan *p, double *taps, size_t n_taps, int *n_comp,
+                         int64_t *row_len) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (p->taps.empty()) return fail(LFD_EUNSUPPORTED, "plan has no block taps (recurrence kernel only)");
+  const int64_t row = (int64_t)(p->taps.size() / p->tg.nc);
+  if (n_comp) *n_comp = p->tg.nc;
+  if (row_len) *row_len = row;
+  if (taps) {
+    if (n_taps != p->taps.size())
+      return fail(LFD_EINVAL, "taps buffer must hold n_comp * row_len doubles");
+    std::memcpy(taps, p->taps.data(), n_taps * sizeof(double));
+  }
+  return LFD_OK;
+}
+
+int lfd_lowpass_last_kernel(const lfd_lowpass_plan *p) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  return p->last_k1;
+}
+
 void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   if (!p) return;
   if (p->d_chunks) (void)hipFree(p->d_chunks);
+  if (p->d_taps) (void)hipFree(p->d_taps);
   for (auto &e : p->ev)
     if (e) (void)hipEventDestroy(e);
   delete p;

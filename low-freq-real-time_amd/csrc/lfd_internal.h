@@ -82,7 +82,28 @@ struct BlockGeom {
   int nF;                  // functionals per block (2n+1)
 };
 
+// Block taps of the MFMA block-functional kernel.  The functionals are linear
+// in the block's extended samples: F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p]
+// (lfd_capi.cpp block_taps).  Block k's row is read from the 16-B aligned
+// sample floor4(base + k*L - J), i.e. shifted by v = (base + k*L - J) mod 4;
+// the device table holds the taps for each shift that occurs (nvar = 1 when
+// L % 4 == 0, else 4), zero-padded to Lp samples:
+//   taps[v][((t*4 + q)*nc + c)*4 + e] = Kx[c][16t + 4q + e - v]
+// (t: 16-sample group, q: MFMA k-lane group, e: MFMA step within the group).
+struct TapGeom {
+  int Lp;       // padded row length (multiple of 64 samples)
+  int J;        // FIR history samples
+  int nc;       // functionals per block (<= 16: one MFMA row tile)
+  int nvar;     // 1: single shift v0 for every block; 4: table index = shift
+  int v0;
+};
+constexpr int TAP_LDS_MAX = 160 * 1024;  // taps must fit one workgroup's LDS
+
 // Launchers (lfd_kernels.hip).  All return hipError_t of the launch.
+// MFMA block functionals: s_t == 1, s_ch % 4 == 0, 16-B aligned x.
+hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n_t,
+                                         const BlockGeom &g, const double *taps,
+                                         const TapGeom &tg, double *F, hipStream_t st);
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g,
                                     const BlockConst &kc, double *F,

@@ -725,6 +725,155 @@ __global__ __launch_bounds__(256) void k_rolling_generic(
   *out = (float)(acc / (double)W);
 }
 
+
+// ---------------------------------------------------------------------------
+// k_block_functionals_mfma — the block functionals as a skinny GEMM on the
+// fp64 matrix cores (lfd_internal.h TapGeom):
+//   F[k][c][ch] = sum_p Kx[c][p] x[ch][base + k*L + row_off + p].
+// A wave owns 16 channels x MF_RUN consecutive blocks.  One
+// v_mfma_f64_16x16x4_f64 multiplies taps (A: 16 functionals x 4 samples; rows
+// >= nc are zero) by samples (B: 4 samples x 16 channels): lane l supplies
+// A[c = l&15][k = l>>4] from the LDS tap table and B[k = l>>4][ch = l&15] from
+// one 16-B load of its channel per 16-sample group, so a wave-instruction
+// loads 16 rows x 64 B and every float feeds exactly one MFMA.  D[c][ch]
+// lands with the channel on the lane, so F stores are 16 consecutive
+// channels.  The next iteration's 4 loads (64 samples) are in flight behind
+// the current iteration's 16 MFMAs; the VALU only converts f32 -> f64.
+// ---------------------------------------------------------------------------
+typedef double d4v __attribute__((ext_vector_type(4)));
+constexpr int MF_RUN = 32;  // blocks per wave
+
+// guarded 4-sample load (edge blocks only): FIR history is 0 before the
+// channel start; the zero-tap padding after the block may run past n_t
+__device__ __forceinline__ f4v mf_load_guarded(const float *__restrict__ xr, int64_t off,
+                                               int64_t n_t) {
+  f4v v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = off + e;
+    const int64_t ic = i < 0 ? 0 : (i >= n_t ? n_t - 1 : i);
+    const float xv = xr[ic];
+    v[e] = (i >= 0 && i < n_t) ? xv : 0.0f;
+  }
+  return v;
+}
+
+// 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur
+__device__ __forceinline__ void mf_iter(const double *kt, int kstride, bool colv,
+                                        const f4v (&cur)[4], d4v &acc0, d4v &acc1) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double2 b01 = *reinterpret_cast<const double2 *>(kt + j * kstride);
+    const double2 b23 = *reinterpret_cast<const double2 *>(kt + j * kstride + 2);
+    const double a0 = colv ? b01.x : 0.0, a1 = colv ? b01.y : 0.0;
+    const double a2 = colv ? b23.x : 0.0, a3 = colv ? b23.y : 0.0;
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, (double)cur[j].x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, (double)cur[j].y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, (double)cur[j].z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, (double)cur[j].w, acc1, 0, 0, 0);
+  }
+}
+
+// lane holds D[c = q + 4r][ch]: 16 consecutive channels per (block, c)
+__device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, double *F, int64_t k,
+                                         int nc, int q, int64_t ch, int64_t n_ch) {
+  if (ch >= n_ch) return;
+  const d4v acc = acc0 + acc1;
+  double *Fo = F + (k * nc) * n_ch + ch;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (q + 4 * r < nc) Fo[(int64_t)(q + 4 * r) * n_ch] = acc[r];
+}
+
+__global__ __launch_bounds__(1024) void k_block_functionals_mfma(
+    const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
+    const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs) {
+  extern __shared__ double Ks[];
+  const int tab = tg.Lp * tg.nc;  // doubles per shift table (even)
+  for (int i = 2 * threadIdx.x; i < tab * tg.nvar; i += 2 * blockDim.x)
+    *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t n_cg = (g.n_ch + 15) / 16;
+  const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (unit >= n_cg * n_runs) return;
+  const int64_t cg = unit % n_cg, run = unit / n_cg;
+  const int64_t k0 = run * MF_RUN;
+  const int64_t k1 = k0 + MF_RUN < g.nb ? k0 + MF_RUN : g.nb;
+  const int col = lane & 15, q = lane >> 4;
+  const int64_t ch = cg * 16 + col;
+  const float *xr = x + (ch < g.n_ch ? ch : g.n_ch - 1) * s_ch;  // channel row
+  const bool colv = col < tg.nc;
+  const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
+  const int nit = tg.Lp / 64;
+  const int kstride = 16 * tg.nc;  // doubles per 16-sample group
+  const int64_t s0 = g.base - tg.J;  // first extended sample of block 0
+  const int L = g.L;
+  // shift table of a block whose row starts at sample s (s >= 0 in the interior)
+  auto table = [&](int64_t s) { return tg.nvar == 1 ? kl : kl + (int)(s & 3) * tab; };
+
+  // blocks whose row may leave [0, n_t) (channel start / end) take the guarded
+  // path; the rest run the pipelined loop with plain 16-B loads
+  int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;                        // s_k >= 0
+  int64_t kb = n_t - tg.Lp - s0 >= 0 ? (n_t - tg.Lp - s0) / L + 1 : 0;  // s_k + Lp <= n_t
+  ka = ka < k0 ? k0 : (ka > k1 ? k1 : ka);
+  kb = kb > k1 ? k1 : (kb < ka ? ka : kb);
+  for (int64_t k = k0; k < k1; ++k) {
+    if (k == ka) k = kb;  // skip the interior
+    if (k >= k1) break;
+    const int64_t s = s0 + k * L;
+    const int v = (int)(((s % 4) + 4) % 4);
+    const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
+    const int64_t a = s - v + 4 * q;
+    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int it = 0; it < nit; ++it) {
+      f4v cur[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+      mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+    }
+    mf_store(acc0, acc1, F, k, tg.nc, q, ch, g.n_ch);
+  }
+  if (ka >= kb) return;
+
+  // interior: flattened (block, iteration) loop, next iteration's loads in flight
+  const float *xl = xr + 4 * q;
+  int64_t k = ka;
+  int64_t s = s0 + ka * L;
+  const float *p = xl + (s & ~(int64_t)3);
+  const double *kt = table(s);
+  int it = 0;
+  f4v cur[4], nxt[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cur[j] = *reinterpret_cast<const f4v *>(p + 16 * j);
+  d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  while (true) {
+    const bool last_it = it == nit - 1;
+    const bool more = !(last_it && k + 1 >= kb);
+    const float *pn = last_it ? xl + ((s + L) & ~(int64_t)3) : p + 64;
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nxt[j] = *reinterpret_cast<const f4v *>(pn + 16 * j);
+    }
+    mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+    if (last_it) {
+      mf_store(acc0, acc1, F, k, tg.nc, q, ch, g.n_ch);
+      acc0 = d4v{0.0, 0.0, 0.0, 0.0};
+      acc1 = d4v{0.0, 0.0, 0.0, 0.0};
+      ++k;
+      s += L;
+      kt = table(s);
+      it = 0;
+    } else {
+      ++it;
+    }
+    if (!more) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    p = pn;
+  }
+}
+
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 inline bool getenv_flag(const char *name) {
@@ -765,6 +914,30 @@ hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64
   }
 #undef LFD_BF
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n_t,
+                                         const BlockGeom &g, const double *taps,
+                                         const TapGeom &tg, double *F, hipStream_t st) {
+  if (tg.nc < 1 || tg.nc > 16 || tg.Lp % 64 != 0 || g.nb < 1 || !(tg.nvar == 1 || tg.nvar == 4) ||
+      (tg.nvar == 1 && g.L % 4 != 0))
+    return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * (size_t)tg.Lp * tg.nc * tg.nvar;
+  if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_functionals_mfma),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  // 16 waves per CU whatever the table size: 4 x 256, 2 x 512 or 1 x 1024 threads
+  const int threads = lds <= 40 * 1024 ? 256 : (lds <= 80 * 1024 ? 512 : 1024);
+  const int64_t n_runs = (g.nb + MF_RUN - 1) / MF_RUN;
+  const int64_t units = ((g.n_ch + 15) / 16) * n_runs;
+  k_block_functionals_mfma<<<nblk(units, threads / 64), threads, lds, st>>>(x, s_ch, n_t, g, taps,
+                                                                            tg, F, n_runs);
+  return hipGetLastError();
 }
 
 hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch, int64_t s_t,

@@ -93,6 +93,8 @@ def load():
         "lfd_lowpass_last_timing": ([vp, P(ctypes.c_float), P(ctypes.c_float)], i32),
         "lfd_lowpass_plan_destroy": ([vp], None),
         "lfd_debug_plan_constants": ([vp, vp, sz, vp, sz, vp, sz], i32),
+        "lfd_debug_block_taps": ([vp, vp, sz, P(i32), P(i64)], i32),
+        "lfd_lowpass_last_kernel": ([vp], i32),
         "lfd_sos_filtfilt_resample_f32": ([vp, i64, i64, i64, i64, vp, i32, i32,
                                            vp, vp, i64, vp, i64, i64, vp], i32),
         "lfd_sosfiltfilt_workspace_bytes": ([i64, i64, i32, i32], sz),
@@ -115,7 +117,8 @@ EXPORTED = (
     "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing",
     "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute",
     "lfd_lowpass_last_timing", "lfd_lowpass_plan_destroy",
-    "lfd_debug_plan_constants", "lfd_sos_filtfilt_resample_f32",
+    "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel",
+    "lfd_sos_filtfilt_resample_f32",
     "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32",
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32",
 )

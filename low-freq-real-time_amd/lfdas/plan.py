@@ -112,6 +112,24 @@ class LowpassPlan:
         check(self._lib.lfd_lowpass_last_timing(self._h, ctypes.byref(a), ctypes.byref(b)))
         return float(a.value), float(b.value)
 
+    def last_kernel(self) -> str:
+        """Block-functional kernel of the last execute: "mfma" or "recurrence"."""
+        k = self._lib.lfd_lowpass_last_kernel(self._h)
+        return {1: "recurrence", 2: "mfma"}.get(k, "none")
+
+    def block_taps(self):
+        """Kx[n_comp, L + J] (F_c(k) = sum_p Kx[c, p] x[base + k L - J + p]) or
+        None when the plan runs the recurrence kernel only — testing hook."""
+        nc = ctypes.c_int()
+        row = ctypes.c_int64()
+        rc = self._lib.lfd_debug_block_taps(self._h, None, 0, ctypes.byref(nc), ctypes.byref(row))
+        if rc == _lib.LFD_EUNSUPPORTED:
+            return None
+        check(rc)
+        out = np.zeros((nc.value, row.value), np.float64)
+        check(self._lib.lfd_debug_block_taps(self._h, out.ctypes.data, out.size, None, None))
+        return out
+
     def constants(self):
         """(BlockConst, ScanConst, ChunkGeom[]) numpy records — testing hook."""
         bc = np.zeros(1, _lib.BLOCK_CONST_DTYPE)

@@ -7,7 +7,22 @@ without a GPU.  Not product code."""
 import numpy as np
 
 
-def emulate(plan, x, padlen, fir32=True):
+def block_functionals_taps(plan, x):
+    """Model of k_block_functionals_mfma: F[c, ch, k] = sum_p Kx[c, p]
+    x[ch, base + k L - J + p] (samples before the channel start are 0),
+    accumulated in float64."""
+    Kx = plan.block_taps()
+    _, _, cg = plan.constants()
+    L, nb, J = plan.block_len, plan.n_blocks, 2 * plan.n_sec
+    base = int(cg[0]["head_end"] - cg[0]["kb"] * L)
+    n_ch = x.shape[0]
+    pad = np.zeros((n_ch, J), np.float64)
+    xe = np.concatenate([pad, x.astype(np.float64)], 1)  # xe[:, i + J] = x[:, i]
+    rows = np.stack([xe[:, base + k * L: base + k * L + L + J] for k in range(nb)], 1)
+    return np.einsum("cp,akp->cak", Kx, rows)
+
+
+def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
     bc, sc, cg = plan.constants()
     ns = plan.n_sec
     n = 2 * ns
@@ -58,6 +73,9 @@ def emulate(plan, x, padlen, fir32=True):
     ef = S
     er0 = np.einsum("ij,jab->iab", bc["T"][:n, :n], u)
     p0 = np.einsum("j,jab->ab", bc["cp"][:n], u) + np.einsum("m,mab->ab", bc["dp"][:J], y0)
+    if k1 == "taps":
+        F = block_functionals_taps(plan, x)
+        ef, er0, p0 = F[:n], F[n:2 * n], F[2 * n]
     # ---------------- K2
     PhiF, PhiR, M = sc["PhiF"][:n, :n], sc["PhiR"][:n, :n], sc["M"][:n, :n]
     G0, H0, Kc = sc["G0"][:n], sc["H0"][:n], sc["Kc"][: 2 * n + 1, :J]

@@ -36,6 +36,7 @@ def _run(x, fs, dt_out, P, B, layout="tc"):
     yd = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float32, device="cuda")
     plan.execute(xd, yd, plan.alloc_workspace())
     torch.cuda.synchronize()
+    _run.last_kernel = plan.last_kernel()
     y = yd.cpu().numpy()
     ref = oracle.lfproc_process(x, T0, dt_ns, tg[0], tg[-1] + 1, dt_out, P, B)
     return y, ref, sched
@@ -65,6 +66,76 @@ def test_lfproc_parity(cfg, dc, layout):
         produced[oa:ob] = True
     assert (num / den) ** 0.5 < 1e-4
     assert np.all(np.isnan(y[:, ~produced]))  # trimmed edges untouched
+    # contiguous rows run the fp64-MFMA block taps; strided rows the recurrence
+    assert _run.last_kernel == ("mfma" if layout == "tc" else "recurrence")
+
+
+def _plan_cfg(fs, dt_out, P, B, n_ch, n):
+    from lfdas.plan import LowpassPlan
+    dt_ns = int(round(1e9 / fs))
+    tg = S.time_grid(T0, T0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    lo, w = S.grid_positions(T0, dt_ns, tg)
+    chunks = [(*S.select_range(T0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    sos = oracle.butter_sos(4, (1 / dt_out / 2 * 0.9) / (fs / 2))
+    return LowpassPlan(sos, n_ch, n, lo, w, chunks), len(tg)
+
+
+@pytest.mark.parametrize("cfg", [
+    (250.0, 0.2, 40, 6, 37, 6000),      # L = 50: four row-shift tap tables
+    (500.0, 1.0, 600, 7, 33, 750_000),  # L = 500
+    (200.0, 10.0, 100, 7, 5, 600_000),  # L = 2000: 147 KB of taps, 1024-thread workgroups
+    (1000.0, 0.5, 40, 4, 18, 100_003),  # L = 500, odd n_t (channel stride % 4 != 0 -> recurrence)
+])
+def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
+    """Both block-functional kernels feed the same scan: outputs agree to
+    float32 rounding; the dispatch picks MFMA only for aligned rows."""
+    import torch
+    fs, dt_out, P, B, n_ch, n = cfg
+    rng = np.random.default_rng(7)
+    x = (rng.standard_normal((n_ch, n)) + 300.0).astype(np.float32)
+    plan, n_grid = _plan_cfg(fs, dt_out, P, B, n_ch, n)
+    xd = torch.from_numpy(x).cuda()
+    ws = plan.alloc_workspace()
+    out = {}
+    for mode in ("default", "rec"):
+        if mode == "rec":
+            monkeypatch.setenv("LFD_K1_REC", "1")
+        yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
+        plan.execute(xd, yd, ws)
+        torch.cuda.synchronize()
+        out[mode] = (yd.cpu().numpy(), plan.last_kernel())
+    aligned = n % 4 == 0
+    assert out["default"][1] == ("mfma" if aligned else "recurrence")
+    assert out["rec"][1] == "recurrence"
+    a, b = out["default"][0], out["rec"][0]
+    m = ~np.isnan(b)
+    assert np.array_equal(np.isnan(a), ~m)
+    assert _relrms(a[m], b[m]) < 1e-6
+
+
+def test_k1_unaligned_base_pointer():
+    """A view starting one sample in (not 16-B aligned) takes the recurrence
+    kernel and still matches the oracle."""
+    import torch
+    fs, dt_out, P, B = 500.0, 1.0, 60, 7
+    n_ch, n = 9, 40_000
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal((n_ch, n + 4)) + 1.0).astype(np.float32)
+    plan, n_grid = _plan_cfg(fs, dt_out, P, B, n_ch, n)
+    full = torch.from_numpy(x).cuda()
+    xd = full[:, 1:n + 1]
+    yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
+    plan.execute(xd, yd, plan.alloc_workspace())
+    assert plan.last_kernel() == "recurrence"
+    y_ok = yd.cpu().numpy()
+    xa = torch.from_numpy(np.ascontiguousarray(x[:, 1:n + 1])).cuda()
+    yd2 = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
+    plan.execute(xa, yd2, plan.alloc_workspace())
+    assert plan.last_kernel() == "mfma"
+    y2 = yd2.cpu().numpy()
+    m = ~np.isnan(y2)
+    assert _relrms(y_ok[m], y2[m]) < 1e-6
 
 
 def test_cfg1_random_das():
