@@ -40,7 +40,7 @@ def _args():
     p.add_argument("--dt-out", type=float, default=1.0)
     p.add_argument("--patch-size", type=int, default=600)
     p.add_argument("--edge-buff", type=int, default=7)
-    p.add_argument("--cpu-channels", type=int, default=192,
+    p.add_argument("--cpu-channels", type=int, default=768,
                    help="channels of the bounded CPU-baseline sample (full hour each)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-rolling", action="store_true")

@@ -564,9 +564,13 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
       p->tg = lfd::TapGeom{Lp, J, nc, nvar, v0};
     }
   }
+  p->bg.n_sf = p->sf_blocks;
+  // channel-group-major layouts (lfd_internal.h f_index / sf_index): channels
+  // padded to 16 (F) and 64 (SF)
+  const size_t ch16 = (size_t)((n_ch + 15) / 16) * 16, ch64 = (size_t)((n_ch + 63) / 64) * 64;
   p->off_F = 0;
-  p->off_SF = align256(p->off_F + sizeof(double) * (size_t)p->bg.nF * p->bg.nb * n_ch);
-  p->off_TP = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * n_ch);
+  p->off_SF = align256(p->off_F + sizeof(double) * (size_t)p->bg.nF * p->bg.nb * ch16);
+  p->off_TP = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * ch64);
   p->ws_bytes = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);
   // Device state.  Without a visible device the plan stays host-only (its
   // geometry and constants can still be inspected); execute then fails.

@@ -80,7 +80,21 @@ struct BlockGeom {
   int64_t n_ch, nb, base;  // blocks k in [0, nb) start at sample base + k*L
   int L;
   int nF;                  // functionals per block (2n+1)
+  int64_t n_sf;            // forward-state slots (sum over chunks of their blocks)
 };
+
+// Workspace layouts, channel-group major so that each wave's writes form one
+// contiguous stream (a wave owns one channel group and walks blocks in order):
+//   F  (block functionals): [ch / 16][block][comp][ch % 16]
+//   SF (forward states)   : [ch / 64][chunk-block][state][ch % 64]
+__host__ __device__ inline int64_t f_index(int64_t k, int c, int64_t ch, int64_t nb, int nF) {
+  return (((ch >> 4) * nb + k) * nF + c) * 16 + (ch & 15);
+}
+__host__ __device__ inline int64_t sf_index(int64_t j, int i, int64_t ch, int64_t n_sf, int n) {
+  return (((ch >> 6) * n_sf + j) * n + i) * 64 + (ch & 63);
+}
+constexpr int F_CSTRIDE = 16;   // element stride between comps of one (block, channel)
+constexpr int SF_ISTRIDE = 64;  // element stride between states of one (block, channel)
 
 // Block taps of the MFMA block-functional kernel.  The functionals are linear
 // in the block's extended samples: F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p]

@@ -23,6 +23,8 @@
 // The block decomposition and realization R are derived in DESIGN.md §2.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -145,23 +147,23 @@ template <int NS>
 __device__ __forceinline__ void store_functionals(const BlockConst &kc, const double (&S)[2 * NS],
                                                   const double (&u)[2 * NS], double p0y,
                                                   double *F, int64_t k, int64_t ch,
-                                                  int64_t n_ch) {
+                                                  int64_t nb) {
   constexpr int N = 2 * NS;
   const int64_t nF = 2 * N + 1;
-  double *Fo = F + (k * nF) * n_ch + ch;
+  double *Fo = F + f_index(k, 0, ch, nb, (int)nF);
 #pragma unroll
-  for (int i = 0; i < N; ++i) Fo[i * n_ch] = S[i];
+  for (int i = 0; i < N; ++i) Fo[i * F_CSTRIDE] = S[i];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < N; ++j) acc = fma(kc.T[i * MAX_N + j], u[j], acc);
-    Fo[(N + i) * n_ch] = acc;
+    Fo[(N + i) * F_CSTRIDE] = acc;
   }
   double p0 = p0y;  // sum_m dp[m] y0[m], accumulated during the first samples
 #pragma unroll
   for (int j = 0; j < N; ++j) p0 = fma(kc.cp[j], u[j], p0);
-  Fo[2 * N * n_ch] = p0;
+  Fo[2 * N * F_CSTRIDE] = p0;
 }
 
 // ---------------------------------------------------------------------------
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(256, LFD_K1_MINW) void k_block_functionals_lds(
 #undef LFD_FULL_SLICE
 #undef LFD_STAGE
 #undef LFD_QUAD
-  if (live) store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.n_ch);
+  if (live) store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.nb);
 }
 
 // ---------------------------------------------------------------------------
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
       if (m < J) p0y = fma(kc.dp[m < J ? m : 0], yv, p0y);
     }
   }
-  store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.n_ch);
+  store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.nb);
 }
 
 // ---------------------------------------------------------------------------
@@ -510,13 +512,13 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // ---- forward scan over the full blocks
   const int64_t nF = NF;
   for (int64_t k = G.kb; k < G.ke; ++k) {
-    double *sf = SF + ((G.sf_off + (k - G.kb)) * N) * g.n_ch + ch;
-    const double *f = F + (k * nF) * g.n_ch + ch;
+    double *sf = SF + sf_index(G.sf_off + (k - G.kb), 0, ch, g.n_sf, N);
+    const double *f = F + f_index(k, 0, ch, g.nb, nF);
     double ns[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      sf[i * g.n_ch] = S[i];
-      double acc = f[i * g.n_ch] + (k == G.kb ? corr[i] : 0.0);
+      sf[i * SF_ISTRIDE] = S[i];
+      double acc = f[i * F_CSTRIDE] + (k == G.kb ? corr[i] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) acc = fma(sc.PhiF[i * MAX_N + j], S[j], acc);
       ns[i] = acc;
@@ -566,14 +568,14 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 
   // ---- backward scan, outputs at block starts
   for (int64_t k = G.ke - 1; k >= G.kb; --k) {
-    const double *sf = SF + ((G.sf_off + (k - G.kb)) * N) * g.n_ch + ch;
-    const double *f = F + (k * nF) * g.n_ch + ch;
+    const double *sf = SF + sf_index(G.sf_off + (k - G.kb), 0, ch, g.n_sf, N);
+    const double *f = F + f_index(k, 0, ch, g.nb, nF);
     const bool first = (k == G.kb);
     double sfv[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) sfv[i] = sf[i * g.n_ch];
+    for (int i = 0; i < N; ++i) sfv[i] = sf[i * SF_ISTRIDE];
     if (k >= G.kout0 && k < G.kout1) {
-      double acc = f[2 * N * g.n_ch] + (first ? corr[2 * N] : 0.0);
+      double acc = f[2 * N * F_CSTRIDE] + (first ? corr[2 * N] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         acc = fma(sc.H0[j], T[j], acc);
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     double nr[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      double acc = f[(N + i) * g.n_ch] + (first ? corr[N + i] : 0.0);
+      double acc = f[(N + i) * F_CSTRIDE] + (first ? corr[N + i] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         acc = fma(sc.PhiR[i * MAX_N + j], T[j], acc);
@@ -776,15 +778,30 @@ __device__ __forceinline__ void mf_iter(const double *kt, int kstride, bool colv
 
 // lane holds D[c = q + 4r][ch]: 16 consecutive channels per (block, c)
 __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, double *F, int64_t k,
-                                         int nc, int q, int64_t ch, int64_t n_ch) {
-  if (ch >= n_ch) return;
+                                         int nc, int q, int64_t ch, const BlockGeom &g) {
+  if (ch >= g.n_ch) return;
   const d4v acc = acc0 + acc1;
-  double *Fo = F + (k * nc) * n_ch + ch;
+  double *Fo = F + f_index(k, 0, ch, g.nb, nc);
 #pragma unroll
   for (int r = 0; r < 4; ++r)
-    if (q + 4 * r < nc) Fo[(int64_t)(q + 4 * r) * n_ch] = acc[r];
+    if (q + 4 * r < nc) Fo[(q + 4 * r) * F_CSTRIDE] = acc[r];
 }
 
+__device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
+
+// wave-uniform 64-bit value into SGPRs (VALU-computed values, e.g. 64-bit
+// divisions, otherwise make every dependent branch divergent)
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// MODE 0: production.  Diagnostic modes (timing experiments only, results
+// invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
+// ceiling of the x stream + F stores; 3 = no MFMA and no F stores = the
+// x-stream ceiling alone.
+template <int PF, int MODE>
 __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs) {
@@ -793,7 +810,8 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
   for (int i = 2 * threadIdx.x; i < tab * tg.nvar; i += 2 * blockDim.x)
     *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave-uniform (SGPR) unit arithmetic: the whole block/producer walk is scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t n_cg = (g.n_ch + 15) / 16;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_cg * n_runs) return;
@@ -816,8 +834,8 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
   // path; the rest run the pipelined loop with plain 16-B loads
   int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;                        // s_k >= 0
   int64_t kb = n_t - tg.Lp - s0 >= 0 ? (n_t - tg.Lp - s0) / L + 1 : 0;  // s_k + Lp <= n_t
-  ka = ka < k0 ? k0 : (ka > k1 ? k1 : ka);
-  kb = kb > k1 ? k1 : (kb < ka ? ka : kb);
+  ka = uniform64(ka < k0 ? k0 : (ka > k1 ? k1 : ka));
+  kb = uniform64(kb > k1 ? k1 : (kb < ka ? ka : kb));
   for (int64_t k = k0; k < k1; ++k) {
     if (k == ka) k = kb;  // skip the interior
     if (k >= k1) break;
@@ -832,45 +850,73 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
       for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
       mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
-    mf_store(acc0, acc1, F, k, tg.nc, q, ch, g.n_ch);
+    mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
   }
   if (ka >= kb) return;
 
-  // interior: flattened (block, iteration) loop, next iteration's loads in flight
+  // interior: flattened (block, iteration) stream; the loads of the next PF
+  // iterations are in flight behind the current iteration's MFMAs
   const float *xl = xr + 4 * q;
-  int64_t k = ka;
-  int64_t s = s0 + ka * L;
-  const float *p = xl + (s & ~(int64_t)3);
-  const double *kt = table(s);
+  auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
+  int64_t k = ka, s = s0 + ka * L;  // consumer position
   int it = 0;
-  f4v cur[4], nxt[4];
+  int64_t kp = ka, sp = s;          // producer position
+  int itp = 0;
+  // producer: loads are unconditional (the waitcnt pass then counts exactly
+  // PF iterations of loads in flight); past the unit's last iteration it
+  // re-loads that iteration (cache hits)
+  const float *pp = addr(sp, itp);
+  auto produce = [&]() {
+    if (kp == kb - 1 && itp == nit - 1) return;
+    if (++itp == nit) {
+      itp = 0;
+      ++kp;
+      sp += L;
+    }
+    pp = addr(sp, itp);
+  };
+  f4v buf[PF + 1][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) cur[j] = *reinterpret_cast<const f4v *>(p + 16 * j);
+  for (int d = 0; d < PF; ++d) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) buf[d][j] = ldx4(pp + 16 * j);
+    produce();
+  }
+  const double *kt = table(s);
   d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-  while (true) {
-    const bool last_it = it == nit - 1;
-    const bool more = !(last_it && k + 1 >= kb);
-    const float *pn = last_it ? xl + ((s + L) & ~(int64_t)3) : p + 64;
-    if (more) {
+  // the ring is unrolled PF+1 times so buffer indices are static: moving
+  // prefetched registers would wait for every load in flight
+  bool fin = false;
+  while (!fin) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) nxt[j] = *reinterpret_cast<const f4v *>(pn + 16 * j);
-    }
-    mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
-    if (last_it) {
-      mf_store(acc0, acc1, F, k, tg.nc, q, ch, g.n_ch);
-      acc0 = d4v{0.0, 0.0, 0.0, 0.0};
-      acc1 = d4v{0.0, 0.0, 0.0, 0.0};
-      ++k;
-      s += L;
-      kt = table(s);
-      it = 0;
-    } else {
-      ++it;
-    }
-    if (!more) break;
+    for (int u = 0; u <= PF; ++u) {
+      constexpr int NB = PF + 1;
+      const int lb = (u + PF) % NB;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-    p = pn;
+      for (int j = 0; j < 4; ++j) buf[lb][j] = ldx4(pp + 16 * j);
+      produce();
+      if (MODE == 1 || MODE == 3) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
+      } else {
+        mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+      }
+      if (++it == nit) {
+        if (MODE != 3) mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
+        else if (acc0[0] == 1234.5) F[0] = acc0[1];
+        acc0 = d4v{0.0, 0.0, 0.0, 0.0};
+        acc1 = d4v{0.0, 0.0, 0.0, 0.0};
+        it = 0;
+        ++k;
+        s += L;
+        if (k >= kb) {
+          fin = true;
+          break;
+        }
+        kt = table(s);
+      }
+    }
   }
 }
 
@@ -926,17 +972,39 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_functionals_mfma),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
-    if (e != hipSuccess) return e;
+    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<1, 0>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>)}) {
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         TAP_LDS_MAX);
+      if (e != hipSuccess) return e;
+    }
     attr = true;
   }
   // 16 waves per CU whatever the table size: 4 x 256, 2 x 512 or 1 x 1024 threads
-  const int threads = lds <= 40 * 1024 ? 256 : (lds <= 80 * 1024 ? 512 : 1024);
+  // share one LDS tap table each
+  int threads = lds <= 40 * 1024 ? 256 : (lds <= 80 * 1024 ? 512 : 1024);
+  if (const char *v = std::getenv("LFD_MF_THREADS")) threads = std::max(threads, std::atoi(v));
+  threads = std::min(threads, 1024);
+  int pf = 2, mode = 0;
+  if (const char *v = std::getenv("LFD_MF_PF")) pf = std::atoi(v);
+  if (const char *v = std::getenv("LFD_MF_MODE")) mode = std::atoi(v);
   const int64_t n_runs = (g.nb + MF_RUN - 1) / MF_RUN;
   const int64_t units = ((g.n_ch + 15) / 16) * n_runs;
-  k_block_functionals_mfma<<<nblk(units, threads / 64), threads, lds, st>>>(x, s_ch, n_t, g, taps,
-                                                                            tg, F, n_runs);
+  const unsigned grid = nblk(units, threads / 64);
+#define LFD_MF(PF_, MODE_)                                                                      \
+  k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
+                                                                   n_runs)
+  if (mode == 1)
+    LFD_MF(2, 1);
+  else if (mode == 3)
+    LFD_MF(2, 3);
+  else if (pf == 1)
+    LFD_MF(1, 0);
+  else
+    LFD_MF(2, 0);
+#undef LFD_MF
   return hipGetLastError();
 }
 

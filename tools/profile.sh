@@ -1,8 +1,10 @@
 #!/bin/bash
-# Collect the rocprofv3 evidence for bench.py's dominant kernel on the GPU box.
+# rocprofv3 evidence for bench.py's dominant kernel (run on the GPU box).
 #   tools/profile.sh <tag> [bench args...]
-# 1) kernel trace + stats of the full bench config (timing agrees with bench.py)
-# 2) PMC passes (separate runs, no tracing domains besides kernel-trace)
+# 1) kernel trace + stats of the bench config (durations agree with bench.py)
+# 2) PMC passes, each its own run with --kernel-trace only:
+#    FETCH_SIZE / WRITE_SIZE of the full-size K1, and the same counters on
+#    tools/ubench_hbm_pattern (known byte counts) to calibrate their units
 set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -11,14 +13,14 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu --no-rolling "$@" > $OUT/bench_traced.log 2>&1
-SMALL="--channels 2000 --steps 2 --warmup 0 --no-cpu --no-rolling"
-timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_sq -o sq \
-    --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU \
-    -- python3 bench.py $SMALL > $OUT/pmc_sq.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch --pmc FETCH_SIZE \
-    -- python3 bench.py $SMALL > $OUT/pmc_fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_write -o write --pmc WRITE_SIZE \
-    -- python3 bench.py $SMALL > $OUT/pmc_write.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_tcc -o tcc --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE \
-    -- python3 bench.py $SMALL > $OUT/pmc_tcc.log 2>&1 || true
+FULL="--steps 2 --warmup 0 --no-cpu --no-rolling"
+timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch --pmc FETCH_SIZE \
+    --kernel-include-regex block_functionals -- python3 bench.py $FULL "$@" > $OUT/pmc_fetch.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_write -o write --pmc WRITE_SIZE \
+    --kernel-include-regex block_functionals -- python3 bench.py $FULL "$@" > $OUT/pmc_write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/calib_fetch -o cf --pmc FETCH_SIZE \
+    -- ./tools/ubench_hbm_pattern > $OUT/calib_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/calib_write -o cw --pmc WRITE_SIZE \
+    -- ./tools/ubench_hbm_pattern > $OUT/calib_write.log 2>&1
+python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
 echo done

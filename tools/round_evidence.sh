@@ -1,0 +1,10 @@
+# Round-end evidence on the GPU box: parity tests, the default bench line
+# (CPU baseline + rolling mean included), rocprofv3 trace + PMC passes.
+set -e -o pipefail
+TAG=${1:-r01}
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu_$TAG.log
+timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+tail -1 gpurun_out/bench_$TAG.json
+bash tools/profile.sh $TAG

@@ -1,0 +1,44 @@
+"""profiles/pmc_traffic.json from a tools/profile.sh output directory.
+
+FETCH_SIZE / WRITE_SIZE units are calibrated on tools/ubench_hbm_pattern's
+known byte counts (same run): k_pattern<16> reads n_ch*n*4 bytes with the K1
+access shape (16 rows x 64 B per wave-instruction); k_store8 writes 2.88 GB.
+Usage: python tools/traffic_json.py gpurun_out/prof_<tag> profiles/pmc_traffic.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+vals = collections.defaultdict(list)
+for f in glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
+    part = os.path.basename(os.path.dirname(f))
+    for r in csv.DictReader(open(f)):
+        vals[(part, r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+
+
+def mean(part, kern_sub, counter):
+    v = [x for (p, k, c), xs in vals.items() if p == part and kern_sub in k and c == counter for x in xs]
+    return sum(v) / len(v)
+
+
+read_bytes = 10000 * (1800000 // 16000 * 16000) * 4.0  # k_pattern<16>, span 16000
+fetch_unit = read_bytes / mean("calib_fetch", "k_pattern<16>", "FETCH_SIZE")
+write_unit = 2.88e9 / mean("calib_write", "k_store8", "WRITE_SIZE")
+fetch = mean("pmc_fetch", "block_functionals", "FETCH_SIZE")
+write = mean("pmc_write", "block_functionals", "WRITE_SIZE")
+out = {
+    "kernel": "k_block_functionals_mfma", "channels": 10000, "samples": 1800000,
+    "fetch_size_mean": fetch, "write_size_mean": write,
+    "fetch_bytes_per_unit": fetch_unit, "write_bytes_per_unit": write_unit,
+    "hbm_read_bytes_per_launch": fetch * fetch_unit,
+    "hbm_write_bytes_per_launch": write * write_unit,
+    "hbm_bytes_per_launch": fetch * fetch_unit + write * write_unit,
+    "algorithmic_bytes_per_launch": 10000 * 1800000 * (4.0 + 4.0 / 500),
+    "source": src,
+}
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out, indent=1))
