@@ -224,8 +224,8 @@ def main():
                        "parallelism": f"channel-shard x{ws}", "io_dtype": "f32"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("k_block_functionals_mfma" if plan.last_kernel() == "mfma"
-                                    else "k_block_functionals_lds"), "kernel_ms": k1,
+                         "kernel": {"mfma_runs": "k_block_runs_mfma", "mfma": "k_block_functionals_mfma"}
+                                   .get(plan.last_kernel(), "k_block_functionals_lds"), "kernel_ms": k1,
                          "scan_kernel_ms": float(np.mean(scan_ms))},
             "cpu_baseline": cpu,
             "secondary": secondary,

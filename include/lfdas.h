@@ -100,6 +100,7 @@ int lfd_set_timing(int enable);
  * strides, or cascades above 6th order); 0 before the first execute. */
 #define LFD_K1_RECURRENCE 1
 #define LFD_K1_MFMA 2
+#define LFD_K1_MFMA_RUNS 3 /* MFMA + in-register run folding (4th-order cascades) */
 int lfd_lowpass_last_kernel(const lfd_lowpass_plan *plan);
 /* Testing hook: the plan's block taps Kx[n_comp][row_len] in natural layout,
  * F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p] (row_len = L + J).  With
@@ -107,6 +108,11 @@ int lfd_lowpass_last_kernel(const lfd_lowpass_plan *plan);
  * runs the recurrence kernel only. */
 int lfd_debug_block_taps(const lfd_lowpass_plan *plan, double *taps, size_t n_taps,
                          int *n_comp, int64_t *row_len);
+/* Testing hook: the run table (first block, length of every run) and the
+ * run-mode constants (lfd::RunConst of csrc/lfd_internal.h).  NULL arrays
+ * are skipped.  LFD_EUNSUPPORTED when the plan has no run mode. */
+int lfd_debug_runs(const lfd_lowpass_plan *plan, int64_t *run_ks, int *run_len,
+                   int64_t max_runs, int64_t *n_runs, void *run_const, size_t rc_bytes);
 /* Testing hook (not a stable interface): copies the plan's kernel constants
  * (lfd::BlockConst, lfd::ScanConst, lfd::ChunkGeom[n_chunks] of
  * csrc/lfd_internal.h) so CPU tests can check the host math without a GPU.

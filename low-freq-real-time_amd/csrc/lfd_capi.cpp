@@ -396,6 +396,85 @@ int block_taps(const Cascade &cs, int L, std::vector<long double> &Kx, int &nc, 
   return LFD_OK;
 }
 
+// Run-mode constants from the scan matrices (row-major 4x4, extended precision).
+void run_constants(const lfd::ScanConst &sc, lfd::RunConst &rc) {
+  typedef R M4[4][4];
+  auto ld = [](const double *src, int stride, M4 &m) {
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) m[i][j] = src[i * stride + j];
+  };
+  auto mul = [](const M4 &a, const M4 &b, M4 &o) {
+    M4 t;
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        R acc = 0;
+        for (int k = 0; k < 4; ++k) acc += a[i][k] * b[k][j];
+        t[i][j] = acc;
+      }
+    std::memcpy(o, t, sizeof(M4));
+  };
+  auto st = [](const M4 &m, double *dst) {
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) dst[i * 4 + j] = (double)m[i][j];
+  };
+  constexpr int RR = lfd::RUN_R;
+  M4 PF, PR, Mm;
+  ld(sc.PhiF, MAX_N, PF);
+  ld(sc.PhiR, MAX_N, PR);
+  ld(sc.M, MAX_N, Mm);
+  R G0[4], H0[4];
+  for (int j = 0; j < 4; ++j) {
+    G0[j] = sc.G0[j];
+    H0[j] = sc.H0[j];
+  }
+  std::vector<M4> Fp(RR + 1), Rp(RR + 1), Q(RR);  // PhiF^j, PhiR^j, M PhiF^m
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) Fp[0][i][j] = Rp[0][i][j] = (i == j);
+  for (int j = 1; j <= RR; ++j) {
+    mul(PF, Fp[j - 1], Fp[j]);
+    mul(PR, Rp[j - 1], Rp[j]);
+  }
+  for (int m = 0; m < RR; ++m) mul(Mm, Fp[m], Q[m]);
+  std::memset(&rc, 0, sizeof(rc));
+  for (int j = 0; j <= RR; ++j) {
+    st(Fp[j], rc.PhiFp[j]);
+    st(Rp[j], rc.PhiRp[j]);
+    M4 C = {};
+    for (int m = 0; m < j; ++m) {  // C[j] = sum_{m<j} PhiR^m M PhiF^m
+      M4 t;
+      mul(Rp[m], Q[m], t);
+      for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) C[a][b] += t[a][b];
+    }
+    st(C, rc.C[j]);
+  }
+  for (int d = 0; d < RR; ++d)
+    for (int j = 0; j < 4; ++j) {
+      R acc = 0;
+      for (int i = 0; i < 4; ++i) acc += H0[i] * Rp[d][i][j];
+      rc.B[d][j] = (double)acc;
+    }
+  for (int len = 1; len <= RR; ++len)
+    for (int p = 0; p < len; ++p)
+      for (int j = 0; j < 4; ++j) {
+        R acc = 0;
+        for (int i = 0; i < 4; ++i) acc += G0[i] * Fp[p][i][j];
+        for (int m = p + 1; m < len; ++m) {
+          M4 t;
+          mul(Rp[m - p - 1], Q[m], t);
+          for (int i = 0; i < 4; ++i) acc += H0[i] * t[i][j];
+        }
+        rc.A[len][p][j] = (double)acc;
+      }
+  st(PF, rc.PhiF);
+  st(Mm, rc.M);
+  st(PR, rc.PhiR);
+  for (int j = 0; j < 4; ++j) {
+    rc.G0[j] = sc.G0[j];
+    rc.H0[j] = sc.H0[j];
+  }
+}
+
 inline int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b;
   if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
@@ -420,6 +499,16 @@ struct lfd_lowpass_plan {
   std::vector<double> taps;      // natural layout [nc][L+J]
   lfd::TapGeom tg{};
   double *d_taps = nullptr;      // device layout (lfd_internal.h TapGeom)
+  // run mode (lfd_internal.h RunConst): run table, K1 units, constants
+  bool run_ok = false;
+  std::vector<int64_t> run_ks;
+  std::vector<int> run_len, group_r0;
+  lfd::RunConst rc{};
+  int64_t n_sr = 0;
+  int64_t *d_run_ks = nullptr;
+  int *d_run_len = nullptr, *d_group_r0 = nullptr;
+  lfd::RunConst *d_rc = nullptr;
+  size_t off_Y0 = 0, off_AG = 0, off_SR = 0;
   int64_t sf_blocks = 0, tp_len = 0;
   size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -565,12 +654,61 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     }
   }
   p->bg.n_sf = p->sf_blocks;
+  // run mode: 4th-order cascade, MFMA taps, LDS for taps + 16 run buffers
+  if (n_sec == 2 && !p->taps.empty() &&
+      sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 16 * lfd::RUN_R * 5 * 16) <=
+          (size_t)lfd::TAP_LDS_MAX) {
+    std::vector<int64_t> cuts = {0, p->bg.nb};
+    for (const auto &G : p->chunks) {
+      cuts.push_back(G.kb);
+      if (G.kb + 1 < G.ke) cuts.push_back(G.kb + 1);
+      cuts.push_back(G.ke);
+    }
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    for (size_t i = 0; i + 1 < cuts.size(); ++i)
+      for (int64_t a = cuts[i]; a < cuts[i + 1]; a += lfd::RUN_R) {
+        p->run_ks.push_back(a);
+        p->run_len.push_back((int)std::min<int64_t>(lfd::RUN_R, cuts[i + 1] - a));
+      }
+    const int64_t n_runs = (int64_t)p->run_ks.size();
+    // K1 units: consecutive runs up to 32 blocks
+    int acc = 0;
+    for (int64_t r = 0; r < n_runs; ++r) {
+      if (r == 0 || acc + p->run_len[r] > 32) {
+        p->group_r0.push_back((int)r);
+        acc = 0;
+      }
+      acc += p->run_len[r];
+    }
+    p->group_r0.push_back((int)n_runs);
+    auto run_at = [&](int64_t k) {
+      return (int64_t)(std::lower_bound(p->run_ks.begin(), p->run_ks.end(), k) - p->run_ks.begin());
+    };
+    int64_t sr = 0;
+    for (auto &G : p->chunks) {
+      G.r0 = run_at(G.kb);
+      G.r1 = run_at(G.ke);
+      G.sr_off = sr;
+      sr += G.r1 - G.r0;
+    }
+    p->n_sr = sr;
+    run_constants(p->sc, p->rc);
+    p->run_ok = true;
+  }
   // channel-group-major layouts (lfd_internal.h f_index / sf_index): channels
   // padded to 16 (F) and 64 (SF)
   const size_t ch16 = (size_t)((n_ch + 15) / 16) * 16, ch64 = (size_t)((n_ch + 63) / 64) * 64;
   p->off_F = 0;
   p->off_SF = align256(p->off_F + sizeof(double) * (size_t)p->bg.nF * p->bg.nb * ch16);
-  p->off_TP = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * ch64);
+  size_t end_F = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * ch64);
+  if (p->run_ok) {  // run-mode buffers alias the F / SF region (one mode per execute)
+    p->off_Y0 = 0;
+    p->off_AG = align256(sizeof(double) * (size_t)p->bg.nb * ch16);
+    p->off_SR = align256(p->off_AG + sizeof(double) * (size_t)p->run_ks.size() * 8 * ch16);
+    end_F = std::max(end_F, align256(p->off_SR + sizeof(double) * (size_t)p->n_sr * 4 * ch64));
+  }
+  p->off_TP = end_F;
   p->ws_bytes = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);
   // Device state.  Without a visible device the plan stays host-only (its
   // geometry and constants can still be inspected); execute then fails.
@@ -607,6 +745,19 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     e = hipMalloc(&p->d_taps, dev.size() * sizeof(double));
     if (e == hipSuccess)
       e = hipMemcpy(p->d_taps, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess && p->run_ok) {
+    e = hipMalloc(&p->d_run_ks, sizeof(int64_t) * p->run_ks.size());
+    if (e == hipSuccess) e = hipMalloc(&p->d_run_len, sizeof(int) * p->run_len.size());
+    if (e == hipSuccess) e = hipMalloc(&p->d_group_r0, sizeof(int) * p->group_r0.size());
+    if (e == hipSuccess) e = hipMalloc(&p->d_rc, sizeof(lfd::RunConst));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_run_ks, p->run_ks.data(), sizeof(int64_t) * p->run_ks.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_run_len, p->run_len.data(), sizeof(int) * p->run_len.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_group_r0, p->group_r0.data(), sizeof(int) * p->group_r0.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_rc, &p->rc, sizeof(lfd::RunConst), hipMemcpyHostToDevice);
   }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
   if (e != hipSuccess) {
@@ -646,7 +797,21 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
   const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !env_flag("LFD_K1_REC");
-  p->last_k1 = mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE;
+  const bool runs = mfma && p->run_ok && !env_flag("LFD_NO_RUNS");
+  p->last_k1 = runs ? LFD_K1_MFMA_RUNS : (mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE);
+  if (runs) {
+    const lfd::RunGeom rg{(int64_t)p->run_ks.size(), (int64_t)p->group_r0.size() - 1, p->n_sr,
+                          p->d_run_ks, p->d_run_len, p->d_group_r0, p->d_rc};
+    double *Y0 = reinterpret_cast<double *>(ws + p->off_Y0);
+    double *AG = reinterpret_cast<double *>(ws + p->off_AG);
+    double *SR = reinterpret_cast<double *>(ws + p->off_SR);
+    LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
+    if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
+    LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks,
+                                        p->n_chunks, Y0, AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st));
+    if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
+    return LFD_OK;
+  }
   if (mfma)
     LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, F, st));
   else
@@ -700,6 +865,25 @@ int lfd_debug_block_taps(const lfd_lowpass_plan *p, double *taps, size_t n_taps,
   return LFD_OK;
 }
 
+int lfd_debug_runs(const lfd_lowpass_plan *p, int64_t *run_ks, int *run_len, int64_t max_runs,
+                   int64_t *n_runs, void *run_const, size_t rc_bytes) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (!p->run_ok) return fail(LFD_EUNSUPPORTED, "plan has no run mode");
+  const int64_t nr = (int64_t)p->run_ks.size();
+  if (n_runs) *n_runs = nr;
+  if (run_ks || run_len) {
+    if (max_runs < nr) return fail(LFD_EINVAL, "run arrays too small");
+    if (run_ks) std::memcpy(run_ks, p->run_ks.data(), sizeof(int64_t) * nr);
+    if (run_len) std::memcpy(run_len, p->run_len.data(), sizeof(int) * nr);
+  }
+  if (run_const) {
+    if (rc_bytes != sizeof(lfd::RunConst))
+      return fail(LFD_EINVAL, "RunConst is " + std::to_string(sizeof(lfd::RunConst)) + " bytes");
+    std::memcpy(run_const, &p->rc, rc_bytes);
+  }
+  return LFD_OK;
+}
+
 int lfd_lowpass_last_kernel(const lfd_lowpass_plan *p) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
   return p->last_k1;
@@ -709,6 +893,8 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   if (!p) return;
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);
+  for (void *d : {(void *)p->d_run_ks, (void *)p->d_run_len, (void *)p->d_group_r0, (void *)p->d_rc})
+    if (d) (void)hipFree(d);
   for (auto &e : p->ev)
     if (e) (void)hipEventDestroy(e);
   delete p;

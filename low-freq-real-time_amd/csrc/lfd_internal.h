@@ -74,6 +74,8 @@ struct ChunkGeom {
   int64_t jout0;         // grid index of block kout0's output
   int64_t sf_off;        // offset (in blocks) of this chunk in the s_f scratch
   int64_t tail_out_pos, tail_out_j;  // output inside the tail (j < 0: none)
+  int64_t r0, r1;        // run-mode: runs [r0, r1) tile blocks [kb, ke) (run r0 = [kb])
+  int64_t sr_off;        // run-mode: offset (in runs) of this chunk in the S_in scratch
 };
 
 struct BlockGeom {
@@ -113,11 +115,47 @@ struct TapGeom {
 };
 constexpr int TAP_LDS_MAX = 160 * 1024;  // taps must fit one workgroup's LDS
 
+// Run mode (4th-order cascades, n = 4): K1 folds consecutive blocks into runs
+// of <= RUN_R blocks that never straddle a chunk start, chunk start + 1 or
+// chunk end, and writes per block only the zero-boundary output y0(k) and per
+// run the aggregates E_f = S0(run end), E_r = T0(run start) (zero states at
+// both run ends).  With S_in entering the run and T_in entering from its right:
+//   y(ks + p)  = y0(ks + p) + A[len][p] . S_in + B[len-1-p] . T_in
+//   S_out      = PhiF^len S_in + E_f
+//   T(ks)      = PhiR^len T_in + E_r + C[len] S_in
+// Layouts (channel-group major): Y0 [ch/16][block][ch%16], AG [ch/16][run][8][ch%16].
+constexpr int RUN_R = 8;
+constexpr int RUN_N = 4;  // state dimension of run mode
+struct RunConst {
+  double PhiFp[RUN_R + 1][16];      // PhiF^j
+  double PhiRp[RUN_R + 1][16];      // PhiR^j
+  double C[RUN_R + 1][16];          // sum_{m<len} PhiR^m M PhiF^m
+  double A[RUN_R + 1][RUN_R][4];    // G0 PhiF^p + H0 sum_{m=p+1}^{len-1} PhiR^{m-p-1} M PhiF^m
+  double B[RUN_R][4];               // H0 PhiR^d
+  // K1 epilogue: PhiF, M, PhiR (row-major 4x4), G0, H0
+  double PhiF[16], M[16], PhiR[16], G0[4], H0[4];
+};
+struct RunGeom {
+  int64_t n_runs, n_groups, n_sr;
+  const int64_t *run_ks;    // first block of run r
+  const int *run_len;       // blocks in run r (<= RUN_R)
+  const int *group_r0;      // K1 unit g = runs [group_r0[g], group_r0[g+1])
+  const RunConst *rc;
+};
+
 // Launchers (lfd_kernels.hip).  All return hipError_t of the launch.
 // MFMA block functionals: s_t == 1, s_ch % 4 == 0, 16-B aligned x.
 hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n_t,
                                          const BlockGeom &g, const double *taps,
                                          const TapGeom &tg, double *F, hipStream_t st);
+hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+                                  const double *taps, const TapGeom &tg, const RunGeom &rg,
+                                  double *Y0, double *AG, hipStream_t st);
+hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
+                                  int padlen, const ScanConst &sc, const RunGeom &rg,
+                                  const ChunkGeom *cg_dev, int64_t n_chunks, const double *Y0,
+                                  const double *AG, double *SR, double *TP, int64_t tp_len,
+                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st);
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g,
                                     const BlockConst &kc, double *F,

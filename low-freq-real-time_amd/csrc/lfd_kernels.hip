@@ -450,12 +450,15 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
   }
 };
 
-template <int NS>
+// RUNS: the scans walk runs (lfd_internal.h RunConst) over K1's y0 / run
+// aggregates instead of blocks over F (requires NS == 2).
+template <int NS, bool RUNS>
 __global__ __launch_bounds__(256) void k_chunk_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
     const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
     const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
-    int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+    int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
+    const double *__restrict__ Y0) {
   constexpr int N = 2 * NS;
   constexpr int J = 2 * NS;
   constexpr int NF = 2 * N + 1;
@@ -509,9 +512,30 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     }
   }
 
-  // ---- forward scan over the full blocks
+  // ---- forward scan over the full blocks (run mode: over runs; SF holds S_in
+  // per run, F holds the run aggregates)
   const int64_t nF = NF;
-  for (int64_t k = G.kb; k < G.ke; ++k) {
+  if constexpr (RUNS) {
+    static_assert(N == RUN_N, "run mode is 4th order");
+    const RunConst &rc = *rg.rc;
+    for (int64_t r = G.r0; r < G.r1; ++r) {
+      double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
+      const double *ag = F + (((ch >> 4) * rg.n_runs + r) * 8) * 16 + (ch & 15);
+      const double *P = rc.PhiFp[rg.run_len[r]];
+      double ns[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        sr[i * SF_ISTRIDE] = S[i];
+        double acc = ag[i * 16] + (r == G.r0 ? corr[i] : 0.0);
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
+        ns[i] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) S[i] = ns[i];
+    }
+  }
+  for (int64_t k = G.kb; !RUNS && k < G.ke; ++k) {
     double *sf = SF + sf_index(G.sf_off + (k - G.kb), 0, ch, g.n_sf, N);
     const double *f = F + f_index(k, 0, ch, g.nb, nF);
     double ns[N];
@@ -567,6 +591,47 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   }
 
   // ---- backward scan, outputs at block starts
+  if constexpr (RUNS) {
+    const RunConst &rc = *rg.rc;
+    for (int64_t r = G.r1 - 1; r >= G.r0; --r) {
+      const double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
+      const double *ag = F + (((ch >> 4) * rg.n_runs + r) * 8) * 16 + (ch & 15);
+      const int len = rg.run_len[r];
+      const int64_t ks = rg.run_ks[r];
+      double sin[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) sin[i] = sr[i * SF_ISTRIDE];
+      const double *y0p = Y0 + ((ch >> 4) * g.nb + ks) * 16 + (ch & 15);
+      for (int pp = 0; pp < len; ++pp) {
+        const int64_t k = ks + pp;
+        if (k < G.kout0 || k >= G.kout1) continue;
+        double acc = y0p[pp * 16] + (k == G.kb ? corr[2 * N] : 0.0);
+        const double *A = rc.A[len][pp];
+        const double *B = rc.B[len - 1 - pp];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          acc = fma(A[j], sin[j], acc);
+          acc = fma(B[j], T[j], acc);
+        }
+        y[ch * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t] = (float)acc;
+      }
+      const double *PR = rc.PhiRp[len], *CC = rc.C[len];
+      double nr[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double acc = ag[(4 + i) * 16] + (r == G.r0 ? corr[N + i] : 0.0);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          acc = fma(PR[i * 4 + j], T[j], acc);
+          acc = fma(CC[i * 4 + j], sin[j], acc);
+        }
+        nr[i] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) T[i] = nr[i];
+    }
+    return;
+  }
   for (int64_t k = G.ke - 1; k >= G.kb; --k) {
     const double *sf = SF + sf_index(G.sf_off + (k - G.kb), 0, ch, g.n_sf, N);
     const double *f = F + f_index(k, 0, ch, g.nb, nF);
@@ -903,7 +968,13 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
         mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
       }
       if (++it == nit) {
-        if (MODE != 3) mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
+        if (MODE == 6) {  // diagnostic: same stores into a 64 KB L2-resident window
+          BlockGeom gh = g;
+          gh.nb = 1;
+          mf_store(acc0, acc1, F + ((k & 7) * 16 + (ch >> 4) % 32) * 16 * 9, 0, tg.nc, q, ch & 15, gh);
+        } else if (MODE != 3) {
+          mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
+        }
         else if (acc0[0] == 1234.5) F[0] = acc0[1];
         acc0 = d4v{0.0, 0.0, 0.0, 0.0};
         acc1 = d4v{0.0, 0.0, 0.0, 0.0};
@@ -918,6 +989,182 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_block_runs_mfma — K1 in run mode (lfd_internal.h RunConst): the same fp64
+// MFMA block functionals, folded in-register into runs so that only
+// y0(k) (8 B per block per channel) and the run aggregates E_f, E_r (64 B per
+// run per channel) reach HBM instead of 72 B of functionals per block.
+// Lane (q, col) holds component q of channel col: the run's forward prefix
+// S0 (one state per lane), the per-block reverse inputs v = e_r0 + M S0 and
+// pg = p0 + G0.S0 go to a wave-private LDS buffer [p][pg, v0..v3][16 ch]; at
+// the run's last block a backward sweep over it gives y0 and E_r = T0(ks).
+// One 1024-thread workgroup per CU (taps + constants + 16 run buffers).
+// ---------------------------------------------------------------------------
+constexpr int RUN_WB = RUN_R * 5 * 16;  // doubles per wave run buffer
+constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
+
+template <int PF>
+__global__ __launch_bounds__(1024) void k_block_runs_mfma(
+    const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
+    const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
+    double *__restrict__ AG) {
+  extern __shared__ double Ks[];
+  const int tab = tg.Lp * tg.nc;
+  const int ntab = tab * tg.nvar;
+  for (int i = 2 * threadIdx.x; i < ntab; i += 2 * blockDim.x)
+    *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
+  double *cst = Ks + ntab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4]
+  for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  double *wb = Ks + ntab + RUN_CST + wave * RUN_WB;
+  const int64_t n_cg = (g.n_ch + 15) / 16;
+  const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (unit >= n_cg * rg.n_groups) return;
+  const int64_t cg = unit % n_cg, grp = unit / n_cg;
+  int r = __builtin_amdgcn_readfirstlane(rg.group_r0[grp]);
+  const int r_end = __builtin_amdgcn_readfirstlane(rg.group_r0[grp + 1]);
+  const int64_t k0 = uniform64(rg.run_ks[r]);
+  const int64_t k1 = uniform64(rg.run_ks[r_end - 1] + rg.run_len[r_end - 1]);
+  const int col = lane & 15, q = lane >> 4;
+  const int64_t ch = cg * 16 + col;  // stores land in the 16-channel padding past n_ch
+  const float *xr = x + (ch < g.n_ch ? ch : g.n_ch - 1) * s_ch;
+  const bool colv = col < tg.nc;
+  const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
+  const int nit = tg.Lp / 64;
+  const int kstride = 16 * tg.nc;
+  const int64_t s0 = g.base - tg.J;
+  const int L = g.L;
+  auto table = [&](int64_t s) { return tg.nvar == 1 ? kl : kl + (int)(s & 3) * tab; };
+  const double *PhiF = cst, *Mm = cst + 16, *PhiR = cst + 32, *G0 = cst + 48, *H0 = cst + 52;
+
+  int64_t rks = k0;
+  int rlen = __builtin_amdgcn_readfirstlane(rg.run_len[r]);
+  double S0 = 0.0;  // run prefix state, component q of channel col
+  auto block_done = [&](const d4v &acc0, const d4v &acc1, int64_t k) {
+    const d4v a = acc0 + acc1;  // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
+    const int p = (int)(k - rks);
+    double sv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sv[j] = __shfl(S0, col + 16 * j, 64);
+    double v = a[1], pg = a[2], sn = a[0];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v = fma(Mm[q * 4 + j], sv[j], v);
+      pg = fma(G0[j], sv[j], pg);
+      sn = fma(PhiF[q * 4 + j], sv[j], sn);
+    }
+    S0 = sn;
+    wb[(p * 5 + 1 + q) * 16 + col] = v;
+    if (q == 0) wb[(p * 5) * 16 + col] = pg;
+    if (p + 1 == rlen) {
+      __builtin_amdgcn_wave_barrier();
+      double T[4] = {0.0, 0.0, 0.0, 0.0};
+      double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
+      for (int pp = rlen - 1; pp >= 0; --pp) {
+        double y0 = wb[(pp * 5) * 16 + col];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y0 = fma(H0[j], T[j], y0);
+        if ((pp & 3) == q) y0o[pp * 16] = y0;
+        double nt[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double acc = wb[(pp * 5 + 1 + i) * 16 + col];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc = fma(PhiR[i * 4 + j], T[j], acc);
+          nt[i] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T[i] = nt[i];
+      }
+      double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + col;
+      ag[q * 16] = S0;
+      ag[(4 + q) * 16] = q == 0 ? T[0] : (q == 1 ? T[1] : (q == 2 ? T[2] : T[3]));
+      __builtin_amdgcn_wave_barrier();
+      S0 = 0.0;
+      ++r;
+      if (r < r_end) {
+        rks = uniform64(rg.run_ks[r]);
+        rlen = __builtin_amdgcn_readfirstlane(rg.run_len[r]);
+      }
+    }
+  };
+  // one block through the guarded (edge) path
+  auto guarded_block = [&](int64_t k) {
+    const int64_t s = s0 + k * L;
+    const int v = (int)(((s % 4) + 4) % 4);
+    const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
+    const int64_t a = s - v + 4 * q;
+    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int it = 0; it < nit; ++it) {
+      f4v cur[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+      mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+    }
+    block_done(acc0, acc1, k);
+  };
+
+  int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
+  int64_t kb = n_t - tg.Lp - s0 >= 0 ? (n_t - tg.Lp - s0) / L + 1 : 0;
+  ka = uniform64(ka < k0 ? k0 : (ka > k1 ? k1 : ka));
+  kb = uniform64(kb > k1 ? k1 : (kb < ka ? ka : kb));
+  for (int64_t k = k0; k < ka; ++k) guarded_block(k);
+  if (ka < kb) {
+    const float *xl = xr + 4 * q;
+    auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
+    int64_t k = ka, s = s0 + ka * L;
+    int it = 0;
+    int64_t kp = ka, sp = s;
+    int itp = 0;
+    const float *pp = addr(sp, itp);
+    auto produce = [&]() {
+      if (kp == kb - 1 && itp == nit - 1) return;
+      if (++itp == nit) {
+        itp = 0;
+        ++kp;
+        sp += L;
+      }
+      pp = addr(sp, itp);
+    };
+    f4v buf[PF + 1][4];
+#pragma unroll
+    for (int d = 0; d < PF; ++d) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) buf[d][j] = ldx4(pp + 16 * j);
+      produce();
+    }
+    const double *kt = table(s);
+    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    bool fin = false;
+    while (!fin) {
+#pragma unroll
+      for (int u = 0; u <= PF; ++u) {
+        constexpr int NB = PF + 1;
+        const int lb = (u + PF) % NB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) buf[lb][j] = ldx4(pp + 16 * j);
+        produce();
+        mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+        if (++it == nit) {
+          block_done(acc0, acc1, k);
+          acc0 = d4v{0.0, 0.0, 0.0, 0.0};
+          acc1 = d4v{0.0, 0.0, 0.0, 0.0};
+          it = 0;
+          ++k;
+          s += L;
+          if (k >= kb) {
+            fin = true;
+            break;
+          }
+          kt = table(s);
+        }
+      }
+    }
+  }
+  for (int64_t k = kb; k < k1; ++k) guarded_block(k);
 }
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
@@ -975,7 +1222,8 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
     for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<1, 0>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>)}) {
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6>)}) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          TAP_LDS_MAX);
       if (e != hipSuccess) return e;
@@ -1000,11 +1248,42 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
     LFD_MF(2, 1);
   else if (mode == 3)
     LFD_MF(2, 3);
+  else if (mode == 6)
+    LFD_MF(2, 6);
   else if (pf == 1)
     LFD_MF(1, 0);
   else
     LFD_MF(2, 0);
 #undef LFD_MF
+  return hipGetLastError();
+}
+
+hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+                                  const double *taps, const TapGeom &tg, const RunGeom &rg,
+                                  double *Y0, double *AG, hipStream_t st) {
+  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + 16 * RUN_WB);
+  if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<1>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
+  k_block_runs_mfma<1><<<nblk(units, 16), 1024, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
+  return hipGetLastError();
+}
+
+hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
+                                  int padlen, const ScanConst &sc, const RunGeom &rg,
+                                  const ChunkGeom *cg, int64_t n_chunks, const double *Y0,
+                                  const double *AG, double *SR, double *TP, int64_t tp_len,
+                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+  const unsigned nb = nblk(n_chunks * g.n_ch, 256);
+  k_chunk_scan<2, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
+                                            tp_len, y, ys_ch, ys_t, rg, Y0);
   return hipGetLastError();
 }
 
@@ -1015,9 +1294,9 @@ hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch
                              hipStream_t st) {
   (void)fir32;
   const unsigned nb = nblk(n_chunks * g.n_ch, 256);
-#define LFD_SCAN(NS)                                                                  \
-  k_chunk_scan<NS><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, F, SF, TP, \
-                                        tp_len, y, ys_ch, ys_t)
+#define LFD_SCAN(NS)                                                                         \
+  k_chunk_scan<NS, false><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, F, SF, \
+                                               TP, tp_len, y, ys_ch, ys_t, RunGeom{}, nullptr)
   switch (n_sec) {
     case 1: LFD_SCAN(1); break;
     case 2: LFD_SCAN(2); break;

@@ -38,7 +38,12 @@ SCAN_CONST_DTYPE = np.dtype([("r", _RCOEF), ("PhiF", "f8", (MAX_N, MAX_N)),
                              ("Kc", "f8", (2 * MAX_N + 1, MAX_J))], align=True)
 CHUNK_GEOM_DTYPE = np.dtype([(n, "i8") for n in (
     "s0", "s1", "kb", "ke", "head_end", "tail_begin", "kout0", "kout1", "jout0",
-    "sf_off", "tail_out_pos", "tail_out_j")])
+    "sf_off", "tail_out_pos", "tail_out_j", "r0", "r1", "sr_off")])
+RUN_R = 8  # lfd::RUN_R
+RUN_CONST_DTYPE = np.dtype([("PhiFp", "f8", (RUN_R + 1, 16)), ("PhiRp", "f8", (RUN_R + 1, 16)),
+                            ("C", "f8", (RUN_R + 1, 16)), ("A", "f8", (RUN_R + 1, RUN_R, 4)),
+                            ("B", "f8", (RUN_R, 4)), ("PhiF", "f8", 16), ("M", "f8", 16),
+                            ("PhiR", "f8", 16), ("G0", "f8", 4), ("H0", "f8", 4)])
 
 
 class LFDLibraryError(RuntimeError):
@@ -95,6 +100,7 @@ def load():
         "lfd_debug_plan_constants": ([vp, vp, sz, vp, sz, vp, sz], i32),
         "lfd_debug_block_taps": ([vp, vp, sz, P(i32), P(i64)], i32),
         "lfd_lowpass_last_kernel": ([vp], i32),
+        "lfd_debug_runs": ([vp, vp, vp, i64, P(i64), vp, sz], i32),
         "lfd_sos_filtfilt_resample_f32": ([vp, i64, i64, i64, i64, vp, i32, i32,
                                            vp, vp, i64, vp, i64, i64, vp], i32),
         "lfd_sosfiltfilt_workspace_bytes": ([i64, i64, i32, i32], sz),
@@ -117,7 +123,7 @@ EXPORTED = (
     "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing",
     "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute",
     "lfd_lowpass_last_timing", "lfd_lowpass_plan_destroy",
-    "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel",
+    "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_debug_runs",
     "lfd_sos_filtfilt_resample_f32",
     "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32",
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32",

@@ -113,9 +113,24 @@ class LowpassPlan:
         return float(a.value), float(b.value)
 
     def last_kernel(self) -> str:
-        """Block-functional kernel of the last execute: "mfma" or "recurrence"."""
+        """Block-functional kernel of the last execute: "mfma_runs" (MFMA +
+        run folding), "mfma" or "recurrence"."""
         k = self._lib.lfd_lowpass_last_kernel(self._h)
-        return {1: "recurrence", 2: "mfma"}.get(k, "none")
+        return {1: "recurrence", 2: "mfma", 3: "mfma_runs"}.get(k, "none")
+
+    def runs(self):
+        """(run_ks, run_len, RunConst record) or None without run mode — testing hook."""
+        n = ctypes.c_int64()
+        rc = self._lib.lfd_debug_runs(self._h, None, None, 0, ctypes.byref(n), None, 0)
+        if rc == _lib.LFD_EUNSUPPORTED:
+            return None
+        check(rc)
+        ks = np.zeros(n.value, np.int64)
+        ln = np.zeros(n.value, np.int32)
+        cst = np.zeros(1, _lib.RUN_CONST_DTYPE)
+        check(self._lib.lfd_debug_runs(self._h, ks.ctypes.data, ln.ctypes.data, n.value, None,
+                                       cst.ctypes.data, cst.nbytes))
+        return ks, ln, cst[0]
 
     def block_taps(self):
         """Kx[n_comp, L + J] (F_c(k) = sum_p Kx[c, p] x[base + k L - J + p]) or

@@ -73,9 +73,28 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
     ef = S
     er0 = np.einsum("ij,jab->iab", bc["T"][:n, :n], u)
     p0 = np.einsum("j,jab->ab", bc["cp"][:n], u) + np.einsum("m,mab->ab", bc["dp"][:J], y0)
-    if k1 == "taps":
+    if k1 in ("taps", "runs"):
         F = block_functionals_taps(plan, x)
         ef, er0, p0 = F[:n], F[n:2 * n], F[2 * n]
+    if k1 == "runs":  # model of k_block_runs_mfma: fold blocks into runs
+        run_ks, run_len, rc = plan.runs()
+        rPhiF, rM, rPhiR = (rc[k].reshape(4, 4) for k in ("PhiF", "M", "PhiR"))
+        rG0, rH0 = rc["G0"], rc["H0"]
+        Y0 = np.zeros((n_ch, nb))
+        AG = np.zeros((len(run_ks), 8, n_ch))
+        for ri, (ks, ln) in enumerate(zip(run_ks, run_len)):
+            S0 = np.zeros((4, n_ch))
+            pg, vv = [], []
+            for p in range(ln):
+                k = ks + p
+                pg.append(p0[:, k] + rG0 @ S0)
+                vv.append(er0[:, :, k] + rM @ S0)
+                S0 = rPhiF @ S0 + ef[:, :, k]
+            T0 = np.zeros((4, n_ch))
+            for p in range(ln - 1, -1, -1):
+                Y0[:, ks + p] = pg[p] + rH0 @ T0
+                T0 = rPhiR @ T0 + vv[p]
+            AG[ri, :4], AG[ri, 4:] = S0, T0
     # ---------------- K2
     PhiF, PhiR, M = sc["PhiF"][:n, :n], sc["PhiR"][:n, :n], sc["M"][:n, :n]
     G0, H0, Kc = sc["G0"][:n], sc["H0"][:n], sc["Kc"][: 2 * n + 1, :J]
@@ -129,7 +148,13 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
         dw = np.stack([sum(c64[jj] * dh[jj - m - 1] for jj in range(m + 1, J + 1)) for m in range(J)], 0)
         corr = Kc @ dw
         SFs = {}
-        for k in range(kb, ke):
+        if k1 == "runs":
+            r0, r1 = int(Gc["r0"]), int(Gc["r1"])
+            assert run_ks[r0] == kb and run_len[r0] == 1 and (r1 == len(run_ks) or run_ks[r1] == ke)
+            for ri in range(r0, r1):
+                SFs[ri] = Sf.copy()
+                Sf = rc["PhiFp"][run_len[ri]].reshape(4, 4) @ Sf + AG[ri, :4] + (corr[:n] if ri == r0 else 0)
+        for k in range(kb, ke if k1 != "runs" else kb):
             SFs[k] = Sf.copy()
             Sf = PhiF @ Sf + ef[:, :, k] + (corr[:n] if k == kb else 0)
         tb = int(Gc["tail_begin"])
@@ -145,6 +170,18 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
             if Gc["tail_out_j"] >= 0 and tb + i == Gc["tail_out_pos"]:
                 y[:, Gc["tail_out_j"]] = G * (q + sum(c64[j] * qw[j - 1] for j in range(1, J + 1)))
             qw = [q] + qw[:-1]
+        if k1 == "runs":
+            for ri in range(r1 - 1, r0 - 1, -1):
+                sin, ks, ln = SFs[ri], int(run_ks[ri]), int(run_len[ri])
+                for p in range(ln):
+                    k = ks + p
+                    if Gc["kout0"] <= k < Gc["kout1"]:
+                        yk = Y0[:, k] + (corr[2 * n] if k == kb else 0)
+                        yk = yk + rc["A"][ln][p] @ sin + rc["B"][ln - 1 - p] @ T
+                        y[:, Gc["jout0"] + k - Gc["kout0"]] = yk
+                T = (rc["PhiRp"][ln].reshape(4, 4) @ T + AG[ri, 4:] + (corr[n:2 * n] if ri == r0 else 0)
+                     + rc["C"][ln].reshape(4, 4) @ sin)
+            continue
         for k in range(ke - 1, kb - 1, -1):
             sf = SFs[k]
             if Gc["kout0"] <= k < Gc["kout1"]:

@@ -67,7 +67,10 @@ def test_lfproc_parity(cfg, dc, layout):
     assert (num / den) ** 0.5 < 1e-4
     assert np.all(np.isnan(y[:, ~produced]))  # trimmed edges untouched
     # contiguous rows run the fp64-MFMA block taps; strided rows the recurrence
-    assert _run.last_kernel == ("mfma" if layout == "tc" else "recurrence")
+    if layout == "tc":  # run folding wherever its LDS fits (not at L = 2000)
+        assert _run.last_kernel == ("mfma" if fs * dt_out == 2000 else "mfma_runs")
+    else:
+        assert _run.last_kernel == "recurrence"
 
 
 def _plan_cfg(fs, dt_out, P, B, n_ch, n):
@@ -98,7 +101,9 @@ def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
     xd = torch.from_numpy(x).cuda()
     ws = plan.alloc_workspace()
     out = {}
-    for mode in ("default", "rec"):
+    for mode in ("default", "noruns", "rec"):
+        if mode == "noruns":
+            monkeypatch.setenv("LFD_NO_RUNS", "1")
         if mode == "rec":
             monkeypatch.setenv("LFD_K1_REC", "1")
         yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
@@ -106,12 +111,16 @@ def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
     aligned = n % 4 == 0
-    assert out["default"][1] == ("mfma" if aligned else "recurrence")
+    L = int(fs * dt_out)
+    assert out["default"][1] == (("mfma_runs" if L != 2000 else "mfma") if aligned else "recurrence")
+    assert out["noruns"][1] == ("mfma" if aligned else "recurrence")
     assert out["rec"][1] == "recurrence"
-    a, b = out["default"][0], out["rec"][0]
+    b = out["rec"][0]
     m = ~np.isnan(b)
-    assert np.array_equal(np.isnan(a), ~m)
-    assert _relrms(a[m], b[m]) < 1e-6
+    for mode in ("default", "noruns"):
+        a = out[mode][0]
+        assert np.array_equal(np.isnan(a), ~m)
+        assert _relrms(a[m], b[m]) < 1e-6
 
 
 def test_k1_unaligned_base_pointer():
@@ -132,7 +141,7 @@ def test_k1_unaligned_base_pointer():
     xa = torch.from_numpy(np.ascontiguousarray(x[:, 1:n + 1])).cuda()
     yd2 = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
     plan.execute(xa, yd2, plan.alloc_workspace())
-    assert plan.last_kernel() == "mfma"
+    assert plan.last_kernel() == "mfma_runs"
     y2 = yd2.cpu().numpy()
     m = ~np.isnan(y2)
     assert _relrms(y_ok[m], y2[m]) < 1e-6

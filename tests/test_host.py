@@ -137,11 +137,15 @@ def test_block_taps_reproduce_golden(name):
     plan, sched, tg = _plan_for(fs, dt_out, P, B, x.shape[0], x.shape[1])
     Kx = plan.block_taps()
     assert Kx.shape == (4 * plan.n_sec + 1, plan.block_len + 2 * plan.n_sec)
-    y = emulate(plan, x, 15, k1="taps")
     m = ~np.isnan(ref)
-    assert np.array_equal(np.isnan(y), ~m)
-    rel = np.sqrt(np.sum((y[m] - ref[m]) ** 2) / np.sum(ref[m] ** 2))
-    assert rel < 1e-6
+    for k1 in ("taps", "runs"):
+        if k1 == "runs" and plan.runs() is None:
+            assert plan.block_len == 2000  # cfg5: 147 KB of taps leave no LDS for run buffers
+            continue
+        y = emulate(plan, x, 15, k1=k1)
+        assert np.array_equal(np.isnan(y), ~m)
+        rel = np.sqrt(np.sum((y[m] - ref[m]) ** 2) / np.sum(ref[m] ** 2))
+        assert rel < 1e-6, (k1, rel)
 
 
 def test_host_only_plan_cannot_execute():
