@@ -15,9 +15,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace
     python3 bench.py --steps 5 --warmup 1 --no-cpu --no-rolling "$@" > $OUT/bench_traced.log 2>&1
 FULL="--steps 2 --warmup 0 --no-cpu --no-rolling"
 timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch --pmc FETCH_SIZE \
-    --kernel-include-regex block_functionals -- python3 bench.py $FULL "$@" > $OUT/pmc_fetch.log 2>&1
+    --kernel-include-regex k_block_ -- python3 bench.py $FULL "$@" > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_write -o write --pmc WRITE_SIZE \
-    --kernel-include-regex block_functionals -- python3 bench.py $FULL "$@" > $OUT/pmc_write.log 2>&1
+    --kernel-include-regex k_block_ -- python3 bench.py $FULL "$@" > $OUT/pmc_write.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/calib_fetch -o cf --pmc FETCH_SIZE \
     -- ./tools/ubench_hbm_pattern > $OUT/calib_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/calib_write -o cw --pmc WRITE_SIZE \

@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
@@ -28,10 +29,12 @@ def mean(part, kern_sub, counter):
 read_bytes = 10000 * (1800000 // 16000 * 16000) * 4.0  # k_pattern<16>, span 16000
 fetch_unit = read_bytes / mean("calib_fetch", "k_pattern<16>", "FETCH_SIZE")
 write_unit = 2.88e9 / mean("calib_write", "k_store8", "WRITE_SIZE")
-fetch = mean("pmc_fetch", "block_functionals", "FETCH_SIZE")
-write = mean("pmc_write", "block_functionals", "WRITE_SIZE")
+fetch = mean("pmc_fetch", "k_block_", "FETCH_SIZE")
+write = mean("pmc_write", "k_block_", "WRITE_SIZE")
+kname = sorted({k for (p, k, c) in vals if p == "pmc_fetch" and "k_block_" in k})
+kname = re.search(r"k_block_\w+", kname[0]).group(0) if kname else "k_block_functionals_mfma"
 out = {
-    "kernel": "k_block_functionals_mfma", "channels": 10000, "samples": 1800000,
+    "kernel": kname, "channels": 10000, "samples": 1800000,
     "fetch_size_mean": fetch, "write_size_mean": write,
     "fetch_bytes_per_unit": fetch_unit, "write_bytes_per_unit": write_unit,
     "hbm_read_bytes_per_launch": fetch * fetch_unit,
