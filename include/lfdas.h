@@ -161,6 +161,115 @@ int lfd_rolling_mean_f32(const float *x, int64_t n_ch, int64_t n_t,
                          int64_t step, float *y, int64_t ys_ch, int64_t ys_t,
                          void *stream);
 
+/* ------------------------------------------------------------------------
+ * LFProc chunk schedule (host arithmetic, no device): the index loop of
+ *   lf_das.py:258-290.  rows[4*i..4*i+3] = (read_first, read_last, out_begin,
+ *   out_end) grid indices of chunk i: it selects time_grid[read_first] ..
+ *   time_grid[read_last] (inclusive) and writes time_grid[out_begin:out_end].
+ *   LFD_EINVAL when the loop cannot progress (process_patch_size <=
+ *   2*edge_buff_size; the reference loops forever there) or n_grid < 2.
+ * ------------------------------------------------------------------------ */
+int lfd_lfproc_schedule(int64_t n_grid, int64_t patch_size, int64_t buff_size,
+                        int64_t *rows, int64_t max_rows, int64_t *n_rows);
+
+/* ------------------------------------------------------------------------
+ * Streaming low-pass + decimate with a device-resident sample arena.
+ *   replaces the real-time loop of low_pass_dascore_edge.ipynb cell 11
+ *   (:199-235): every new file triggers a fresh LFProc.process_time_range
+ *   (t_1, t_2) (lf_das.py:219-290) with t_2 = newest time_max and
+ *   t_1 = get_last_processed_time() (lf_das.py:214-217) - buffer, re-reading
+ *   the 2*edge overlap from the archive.  Here the overlap never leaves HBM:
+ *   pushes append to a per-channel arena (ping-pong compaction keeps only
+ *   what a later run reads), host->HBM copies run on their own HIP stream
+ *   (direct DMA from pinned memory, double-buffered pinned staging
+ *   otherwise), and each run is one lfd_lowpass_plan execute over all of its
+ *   chunks (plans cached by geometry).
+ *
+ * Modes
+ *   LFD_STREAM_EDGE        each push runs process_time_range(t_1, t_hi):
+ *                          t_hi = time of the newest sample; t_1 =
+ *                          t_start_ns on the first run, afterwards
+ *                          last output time - resume_back_ns (the notebook's
+ *                          buffer = int((ceil(edge/dt)-1)*dt) s).  Results are
+ *                          those of the notebook loop with one file per push.
+ *   LFD_STREAM_CONTINUOUS  one process_time_range(t_start_ns, t_end_ns) over
+ *                          a spool too large for HBM (out-of-core): chunk i
+ *                          runs as soon as time_grid[read_last] has arrived;
+ *                          lfd_stream_flush runs what remains.
+ * A run that cannot produce an output (time grid of <= 2*B+1 points) is
+ * deferred to the next push (the reference indexes out of range there).
+ * Pushes must be contiguous in time (next t0 = previous t0 + n_t*sample_ns);
+ * otherwise the push fails with "patch merge failed! Gap in data exists"
+ * (_check_merge, lf_das.py:16-20).
+ * ------------------------------------------------------------------------ */
+#define LFD_STREAM_EDGE 0
+#define LFD_STREAM_CONTINUOUS 1
+#define LFD_STREAM_DRY_RUN 1 /* flags: host bookkeeping only (no device, x may be NULL) */
+
+typedef struct lfd_stream_config {
+  int64_t n_ch;                   /* channels of every push                      */
+  int64_t sample_ns;              /* input sampling interval, ns                 */
+  double output_sample_interval;  /* dt, s; grid step int(dt*1000) ms (lf_das.py:255) */
+  int64_t process_patch_size;     /* P (lf_das.py:199)                          */
+  int64_t edge_buff_size;         /* B (lf_das.py:200)                          */
+  int mode;                       /* LFD_STREAM_EDGE | LFD_STREAM_CONTINUOUS    */
+  int flags;                      /* LFD_STREAM_DRY_RUN                         */
+  int64_t t_start_ns;             /* edge: first run's t_1; continuous: bgtime  */
+  int64_t t_end_ns;               /* continuous: edtime (exclusive)             */
+  int64_t resume_back_ns;         /* edge: t_1 = last output - resume_back_ns   */
+  int64_t capacity;               /* arena samples per channel (0: automatic)   */
+} lfd_stream_config;
+
+typedef struct lfd_stream lfd_stream;
+
+/* Device streams, events and the arena live on the current device. */
+int lfd_stream_open(lfd_stream **s, const lfd_stream_config *cfg, const double *sos,
+                    int n_sec, int padlen);
+/* Append n_t samples of every channel starting at time t0_ns.  x is a HOST
+ * array addressed by element strides (s_t == 1: (channel, time) rows;
+ * s_ch == 1: (time, channel) rows, transposed on device).  Pinned x
+ * (hipHostMalloc / hipHostRegister / lfd_host_alloc) is copied by DMA
+ * directly and asynchronously: keep it unchanged until lfd_stream_fetch or
+ * lfd_stream_synchronize returns.  Pageable x is staged through two pinned
+ * buffers and may be reused on return.  Returns once the copy and the run
+ * are enqueued. */
+int lfd_stream_push(lfd_stream *s, const float *x, int64_t n_t, int64_t s_ch, int64_t s_t,
+                    int64_t t0_ns);
+/* Continuous mode: run the chunks still pending (the schedule's tail) on
+ * the data received so far.  No-op in edge mode. */
+int lfd_stream_flush(lfd_stream *s);
+
+typedef struct lfd_stream_output {
+  int64_t n_out;        /* output samples per channel produced by the last push/flush */
+  int64_t t_first_ns;   /* time of the first output sample                           */
+  int64_t t_step_ns;    /* spacing (int(dt*1000) ms)                                 */
+  int64_t n_chunks;     /* LFProc chunks (reference output files) completed          */
+  int64_t n_runs;       /* process_time_range runs executed so far                   */
+  const float *y;       /* device (n_ch, n_out), row stride ys_ch; valid until the
+                           second-next push                                          */
+  int64_t ys_ch;
+} lfd_stream_output;
+int lfd_stream_last_output(const lfd_stream *s, lfd_stream_output *out);
+/* Per-chunk output counts of the last push (chunk i holds counts[i] samples). */
+int lfd_stream_last_chunks(const lfd_stream *s, int64_t *counts, int64_t max_chunks,
+                           int64_t *n_chunks);
+/* Wait for the last push (its host->HBM copy and its outputs) and copy the
+ * outputs to host y[ch*ys_ch + j*ys_t] (nothing to copy when n_out == 0). */
+int lfd_stream_fetch(lfd_stream *s, float *y, int64_t ys_ch, int64_t ys_t);
+/* Wait for all enqueued work of the stream. */
+int lfd_stream_synchronize(lfd_stream *s);
+/* Device time of the last push (ms; needs lfd_set_timing(1)): host->HBM copy
+ * (+ transpose) and the low-pass run. */
+int lfd_stream_last_timing(const lfd_stream *s, float *ms_copy, float *ms_run);
+/* Arena geometry: capacity (samples per channel) and valid columns. */
+int lfd_stream_info(const lfd_stream *s, int64_t *capacity, int64_t *held_samples,
+                    int64_t *t_first_held_ns);
+void lfd_stream_close(lfd_stream *s);
+
+/* Pinned host memory for pushes (hipHostMalloc). */
+int lfd_host_alloc(void **p, size_t bytes);
+void lfd_host_free(void *p);
+
 #ifdef __cplusplus
 }
 #endif

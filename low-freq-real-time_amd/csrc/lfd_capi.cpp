@@ -23,14 +23,22 @@ using lfd::MAX_N;
 using lfd::MAX_SEC;
 
 namespace {
-
 thread_local std::string g_err;
-std::atomic<int> g_timing{0};
+}  // namespace
 
-int fail(int code, const std::string &m) {
+int lfd::fail(int code, const std::string &m) {
   g_err = m;
   return code;
 }
+
+namespace {
+using lfd::fail;
+std::atomic<int> g_timing{0};
+}  // namespace
+
+bool lfd::timing_enabled() { return g_timing.load() != 0; }
+
+namespace {
 
 #define LFD_HIP(call)                                                      \
   do {                                                                     \

@@ -4,8 +4,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 
 namespace lfd {
+
+// Sets the calling thread's lfd_last_error() message; returns `code`.
+int fail(int code, const std::string &m);
+// lfd_set_timing() state (HIP-event timing of executes / pushes).
+bool timing_enabled();
 
 constexpr int MAX_SEC = 4;            // up to 8th-order cascades
 constexpr int MAX_N = 2 * MAX_SEC;    // state dimension (TDF-II, 2 per section)
@@ -179,5 +185,8 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                int64_t s_ch, int64_t s_t, int64_t W, int64_t S,
                                float *y, int64_t ys_ch, int64_t ys_t,
                                hipStream_t st);
+// dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.
+hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
+                            int64_t dp, hipStream_t st);
 
 }  // namespace lfd

@@ -1356,4 +1356,38 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
   return hipGetLastError();
 }
 
+// Time-major -> channel-major transpose for the stream arena
+// (host (time, distance) rows, as real DAS files store them,
+// low_pass_dascore.ipynb:222 data[:, ch]).  64x64 tiles through LDS (one
+// padding column against bank conflicts); both sides coalesced.
+__global__ __launch_bounds__(256) void k_transpose_tc(const float *__restrict__ src, int64_t n_rows,
+                                                      int64_t n_cols, int64_t sp,
+                                                      float *__restrict__ dst, int64_t dp) {
+  __shared__ float tile[64][65];
+  const int64_t c0 = (int64_t)blockIdx.x * 64, r0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    if (r < n_rows && c < n_cols) tile[i][tx] = src[r * sp + c];
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (r < n_rows && c < n_cols) dst[c * dp + r] = tile[tx][i];
+  }
+}
+
+hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
+                            int64_t dp, hipStream_t st) {
+  const int64_t slab = (int64_t)65535 * 64;  // grid.y limit
+  for (int64_t r = 0; r < n_rows; r += slab) {
+    const int64_t nr = n_rows - r < slab ? n_rows - r : slab;
+    dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((nr + 63) / 64));
+    k_transpose_tc<<<grid, 256, 0, st>>>(src + r * sp, nr, n_cols, sp, dst + r, dp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 }  // namespace lfd

@@ -63,6 +63,28 @@ class LFDUnsupported(LFDError):
     pass
 
 
+class lfd_stream_config(ctypes.Structure):
+    """include/lfdas.h lfd_stream_config."""
+    _fields_ = [("n_ch", ctypes.c_int64), ("sample_ns", ctypes.c_int64),
+                ("output_sample_interval", ctypes.c_double),
+                ("process_patch_size", ctypes.c_int64), ("edge_buff_size", ctypes.c_int64),
+                ("mode", ctypes.c_int), ("flags", ctypes.c_int),
+                ("t_start_ns", ctypes.c_int64), ("t_end_ns", ctypes.c_int64),
+                ("resume_back_ns", ctypes.c_int64), ("capacity", ctypes.c_int64)]
+
+
+class lfd_stream_output(ctypes.Structure):
+    """include/lfdas.h lfd_stream_output."""
+    _fields_ = [("n_out", ctypes.c_int64), ("t_first_ns", ctypes.c_int64),
+                ("t_step_ns", ctypes.c_int64), ("n_chunks", ctypes.c_int64),
+                ("n_runs", ctypes.c_int64), ("y", ctypes.c_void_p), ("ys_ch", ctypes.c_int64)]
+
+
+LFD_STREAM_EDGE = 0
+LFD_STREAM_CONTINUOUS = 1
+LFD_STREAM_DRY_RUN = 1
+
+
 class lfd_chunk(ctypes.Structure):
     _fields_ = [("s0", ctypes.c_int64), ("s1", ctypes.c_int64),
                 ("g0", ctypes.c_int64), ("g1", ctypes.c_int64)]
@@ -110,6 +132,19 @@ def load():
                                    i64, vp], i32),
         "lfd_rolling_mean_f32": ([vp, i64, i64, i64, i64, i64, i64, vp, i64, i64,
                                   vp], i32),
+        "lfd_lfproc_schedule": ([i64, i64, i64, vp, i64, P(i64)], i32),
+        "lfd_stream_open": ([P(vp), vp, vp, i32, i32], i32),
+        "lfd_stream_push": ([vp, vp, i64, i64, i64, i64], i32),
+        "lfd_stream_flush": ([vp], i32),
+        "lfd_stream_last_output": ([vp, vp], i32),
+        "lfd_stream_last_chunks": ([vp, vp, i64, P(i64)], i32),
+        "lfd_stream_fetch": ([vp, vp, i64, i64], i32),
+        "lfd_stream_synchronize": ([vp], i32),
+        "lfd_stream_last_timing": ([vp, P(ctypes.c_float), P(ctypes.c_float)], i32),
+        "lfd_stream_info": ([vp, P(i64), P(i64), P(i64)], i32),
+        "lfd_stream_close": ([vp], None),
+        "lfd_host_alloc": ([P(vp), sz], i32),
+        "lfd_host_free": ([vp], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -127,6 +162,10 @@ EXPORTED = (
     "lfd_sos_filtfilt_resample_f32",
     "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32",
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32",
+    "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_push", "lfd_stream_flush",
+    "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
+    "lfd_stream_synchronize", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
+    "lfd_host_alloc", "lfd_host_free",
 )
 
 

@@ -21,7 +21,7 @@ __all__ = [
     "pass_filter", "interpolate", "rolling_mean", "rolling_out_times",
     "get_patch_time", "lfproc_time_grid", "lfproc_schedule", "lfproc_process",
     "down_sample_processing", "get_edge_effect_time", "have_c_oracle",
-    "sosfiltfilt_rows_c",
+    "sosfiltfilt_rows_c", "edge_loop",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -540,3 +540,35 @@ def get_edge_effect_time(sampling_interval, total_T, tol=1e-6, freq=5, nqfreq_ra
     if int(math.ceil(edge_t * freq)) * 2 >= int(total_T * freq):
         raise ValueError(f"edge_t value ({edge_t} sec) is too close to half of the processing chunk size ({total_T} sec).")
     return edge_t
+
+
+def edge_loop(data, t0_ns: int, dt_ns: int, push_len: int, t_start_ns: int, dt_out: float,
+              patch_size: int, buff_size: int, resume_back_ns: int, corners: int = 4):
+    """The real-time loop of low_pass_dascore_edge.ipynb cell 11 (:199-235)
+    with one new file of ``push_len`` samples per iteration: run k sees the
+    data of files 0..k and calls ``process_time_range(t_1, t_2)`` with
+    ``t_2`` = newest sample time (``sub_sp[-1].attrs['time_max']``) and
+    ``t_1`` = ``t_start`` on the first run, else ``get_last_processed_time()``
+    (lf_das.py:214-217: the last output time) minus ``resume_back_ns``
+    (``int((ceil(edge/d_t)-1)*d_t)`` s).  A run whose time grid holds
+    ``<= 2*buff_size + 1`` points cannot produce an output (the reference
+    indexes out of range there) and is skipped until more data arrives.
+    Returns, per push, the list of ``(out_times_ns, out_data)`` chunks."""
+    data = np.asarray(data)
+    n = data.shape[-1]
+    res = []
+    last_out = None
+    for end in range(push_len, n + 1, push_len):
+        t2 = t0_ns + (end - 1) * dt_ns
+        t1 = t_start_ns if last_out is None else last_out - resume_back_ns
+        tg = lfproc_time_grid(t1, t2, dt_out)
+        if len(tg) < 2 or len(tg) <= 2 * buff_size + 1:
+            res.append([])
+            continue
+        out = lfproc_process(data[..., :end], t0_ns, dt_ns, t1, t2, dt_out, patch_size,
+                             buff_size, corners)
+        out = [(t, y) for t, y in out if len(t)]
+        if out:
+            last_out = int(out[-1][0][-1])
+        res.append(out)
+    return res
