@@ -44,6 +44,7 @@ def _args():
                    help="channels of the bounded CPU-baseline sample (full hour each)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-rolling", action="store_true")
+    p.add_argument("--no-stream", action="store_true", help="skip the cfg4 / cfg5 streaming lines")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 PMC traffic summary (tools/pmc_summary.py) for roofline.traffic")
     return p.parse_args()
@@ -110,6 +111,99 @@ def cpu_baseline(args, sos, sched, t0, dt_ns, tg):
                       f"chunks, oracle C sosfiltfilt + interp1d, 1 thread, {el:.1f} s"}
 
 
+def _pinned_blocks(dev, n_blocks, shape, fs, seed):
+    """Pinned host blocks of synthetic samples (generated on the device, copied
+    down once): the host side of a stream, outside the timed region."""
+    import torch
+    out = []
+    for i in range(n_blocks):
+        d = torch.empty(shape, dtype=torch.float32, device=dev)
+        synth_fill(d, fs, seed + i)
+        h = torch.empty(shape, dtype=torch.float32).pin_memory()
+        h.copy_(d)
+        out.append(h)
+        del d
+    torch.cuda.synchronize(dev)
+    return out
+
+
+def bench_edge_cfg4(dev, n_push=12, warm=2, time_major=False):
+    """cfg4: real-time edge mode, 2,000 ch @ 2 kHz in 30 s files
+    (low_pass_dascore_edge.ipynb cell 11 with one file per run), dt = 1 s,
+    P = 125 (the notebook's 125 s cadence), B = 7 (planner edge ~6 s).
+    Latency = push of a pinned 30 s file -> decimated outputs on the host."""
+    import torch
+    from lfdas.plan import set_timing
+    from lfdas.stream import LowpassStream
+    n_ch, fs, push_s = 2000, 2000.0, 30.0
+    push = int(push_s * fs)
+    dt_ns = int(1e9 / fs)
+    t0 = 1_679_464_800_000_000_000  # 2023-03-22T06:00:00 (the notebook's start)
+    shape = (push, n_ch) if time_major else (n_ch, push)
+    blocks = _pinned_blocks(dev, 2, shape, fs, 4321)
+    st = LowpassStream(n_ch, dt_ns, 1.0, 125, 7, mode="edge", t_start=t0)
+    lat, cp, run, n_out = [], [], [], []
+    set_timing(True)
+    for k in range(n_push + warm):
+        blk = blocks[k % 2]
+        ta = time.perf_counter()
+        o = st.push(blk, t0 + k * push * dt_ns, time_axis=0 if time_major else 1)
+        st.fetch()
+        tb = time.perf_counter()
+        if k >= warm:
+            lat.append((tb - ta) * 1e3)
+            a, b = st.last_timing_ms()
+            cp.append(a)
+            run.append(b)
+            n_out.append(o.n_out)
+    set_timing(False)
+    st.close()
+    lat = np.array(lat)
+    return {"p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+            "max_ms": float(lat.max()), "chunk_ms": push_s * 1e3,
+            "latency_frac_of_chunk": float(np.percentile(lat, 99) / (push_s * 1e3)),
+            "h2d_ms": float(np.median(cp)), "run_ms": float(np.median(run)),
+            "h2d_GBps": n_ch * push * 4 / (np.median(cp) * 1e-3) / 1e9,
+            "outputs_per_push": int(np.median(n_out)), "pushes": n_push,
+            "config": f"2,000 ch @ 2 kHz, 30 s pinned pushes ({'time, distance' if time_major else 'distance, time'} "
+                      "layout), dt = 1 s, P = 125, B = 7, resume buffer (B-1) s; latency = push -> host outputs"}
+
+
+def bench_ooc_cfg5(dev, n_ch=50_000, seconds=3600.0, push_s=60.0):
+    """cfg5 (bounded sample): out-of-core process_time_range over a 50,000-ch
+    @ 200 Hz spool streamed from a pinned host ring, dt = 10 s (fc = 0.045 Hz),
+    P = 120 (1,200 s chunks), B = 6 (planner edge 60 s).  Bound: PCIe."""
+    import torch
+    from lfdas.stream import LowpassStream
+    fs = 200.0
+    push = int(push_s * fs)
+    n = int(seconds * fs)
+    dt_ns = int(1e9 / fs)
+    t0 = 1_679_464_800_000_000_000
+    blocks = _pinned_blocks(dev, 2, (n_ch, push), fs, 777)
+    st = LowpassStream(n_ch, dt_ns, 10.0, 120, 6, mode="continuous", t_start=t0,
+                       t_end=t0 + (n - 1) * dt_ns, capacity=int(1300 * fs) + 2 * push)
+    n_out = 0
+    torch.cuda.synchronize(dev)
+    ta = time.perf_counter()
+    for k in range(n // push):
+        o = st.push(blocks[k % 2], t0 + k * push * dt_ns)
+        n_out += o.n_out
+        st.wait_copy()  # ring buffer (k+1) % 2 is free again
+    o = st.flush()
+    n_out += o.n_out
+    st.synchronize()
+    el = time.perf_counter() - ta
+    st.close()
+    del blocks
+    samples = n_ch * (n // push) * push
+    return {"value": samples / el, "unit": "channel-samples/s", "seconds_streamed": seconds,
+            "wall_s": el, "h2d_GBps": samples * 4 / el / 1e9, "pcie_peak_GBps": 63.0,
+            "pcie_frac": samples * 4 / el / 1e9 / 63.0, "outputs_per_channel": n_out,
+            "config": f"{n_ch:,} ch @ 200 Hz, {seconds:.0f} s of the 24 h spool in {push_s:.0f} s pinned "
+                      "pushes, dt = 10 s, P = 120, B = 6, 1 GPU"}
+
+
 def main():
     args = _args()
     import torch
@@ -152,6 +246,7 @@ def main():
     barrier()
     el = time.perf_counter() - t_a
     set_timing(False)
+    k1_kernel = plan.last_kernel()
     if ws > 1:
         tt = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -173,10 +268,12 @@ def main():
         pass
 
     secondary = {}
-    if not args.no_rolling and rank == 0:
-        from lfdas.plan import rolling_mean_device
-        del x
+    if ws == 1:
+        del x, y, wsb
+        plan.close()
         torch.cuda.empty_cache()
+    if not args.no_rolling and ws == 1:
+        from lfdas.plan import rolling_mean_device
         xr = torch.empty((5000, 600_000), dtype=torch.float32, device=dev)
         synth_fill(xr, 1000.0, 99)
         for _ in range(2):
@@ -198,9 +295,16 @@ def main():
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS}}
         del xr
+        torch.cuda.empty_cache()
+    if not args.no_stream and ws == 1:
+        secondary["edge_latency_cfg4"] = bench_edge_cfg4(dev)
+        secondary["edge_latency_cfg4_time_major"] = bench_edge_cfg4(dev, time_major=True)
+        torch.cuda.empty_cache()
+        secondary["out_of_core_cfg5"] = bench_ooc_cfg5(dev)
+        torch.cuda.empty_cache()
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if ws == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, sos, sched, t0, dt_ns, tg)
 
     if rank == 0:
@@ -225,7 +329,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": {"mfma_runs": "k_block_runs_mfma", "mfma": "k_block_functionals_mfma"}
-                                   .get(plan.last_kernel(), "k_block_functionals_lds"), "kernel_ms": k1,
+                                   .get(k1_kernel, "k_block_functionals_lds"), "kernel_ms": k1,
                          "scan_kernel_ms": float(np.mean(scan_ms))},
             "cpu_baseline": cpu,
             "secondary": secondary,

@@ -256,6 +256,10 @@ int lfd_stream_last_chunks(const lfd_stream *s, int64_t *counts, int64_t max_chu
 /* Wait for the last push (its host->HBM copy and its outputs) and copy the
  * outputs to host y[ch*ys_ch + j*ys_t] (nothing to copy when n_out == 0). */
 int lfd_stream_fetch(lfd_stream *s, float *y, int64_t ys_ch, int64_t ys_t);
+/* Wait until the last push's host buffer has been read (its host->HBM copy
+ * is done; the run may still be executing).  A pinned ring of host buffers is
+ * refilled after this returns. */
+int lfd_stream_wait_copy(lfd_stream *s);
 /* Wait for all enqueued work of the stream. */
 int lfd_stream_synchronize(lfd_stream *s);
 /* Device time of the last push (ms; needs lfd_set_timing(1)): host->HBM copy

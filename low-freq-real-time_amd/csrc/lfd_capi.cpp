@@ -680,10 +680,13 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
         p->run_len.push_back((int)std::min<int64_t>(lfd::RUN_R, cuts[i + 1] - a));
       }
     const int64_t n_runs = (int64_t)p->run_ks.size();
-    // K1 units: consecutive runs up to 32 blocks
+    // K1 units: consecutive runs up to 32 blocks (fewer for narrow arrays, so
+    // that >= ~4,096 wave units cover the chip)
+    const int64_t unit_blocks =
+        std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(32, ((n_ch + 15) / 16) * p->bg.nb / 4096));
     int acc = 0;
     for (int64_t r = 0; r < n_runs; ++r) {
-      if (r == 0 || acc + p->run_len[r] > 32) {
+      if (r == 0 || acc + p->run_len[r] > unit_blocks) {
         p->group_r0.push_back((int)r);
         acc = 0;
       }

@@ -797,7 +797,8 @@ __global__ __launch_bounds__(256) void k_rolling_generic(
 // k_block_functionals_mfma — the block functionals as a skinny GEMM on the
 // fp64 matrix cores (lfd_internal.h TapGeom):
 //   F[k][c][ch] = sum_p Kx[c][p] x[ch][base + k*L + row_off + p].
-// A wave owns 16 channels x MF_RUN consecutive blocks.  One
+// A wave owns 16 channels x bpw consecutive blocks (bpw <= MF_RUN, fewer for
+// narrow arrays so the grid still fills the chip).  One
 // v_mfma_f64_16x16x4_f64 multiplies taps (A: 16 functionals x 4 samples; rows
 // >= nc are zero) by samples (B: 4 samples x 16 channels): lane l supplies
 // A[c = l&15][k = l>>4] from the LDS tap table and B[k = l>>4][ch = l&15] from
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(256) void k_rolling_generic(
 // the current iteration's 16 MFMAs; the VALU only converts f32 -> f64.
 // ---------------------------------------------------------------------------
 typedef double d4v __attribute__((ext_vector_type(4)));
-constexpr int MF_RUN = 32;  // blocks per wave
+constexpr int MF_RUN = 32;  // max blocks per wave
 
 // guarded 4-sample load (edge blocks only): FIR history is 0 before the
 // channel start; the zero-tap padding after the block may run past n_t
@@ -869,7 +870,8 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 template <int PF, int MODE>
 __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
-    const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs) {
+    const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs,
+    int bpw) {
   extern __shared__ double Ks[];
   const int tab = tg.Lp * tg.nc;  // doubles per shift table (even)
   for (int i = 2 * threadIdx.x; i < tab * tg.nvar; i += 2 * blockDim.x)
@@ -881,8 +883,8 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_cg * n_runs) return;
   const int64_t cg = unit % n_cg, run = unit / n_cg;
-  const int64_t k0 = run * MF_RUN;
-  const int64_t k1 = k0 + MF_RUN < g.nb ? k0 + MF_RUN : g.nb;
+  const int64_t k0 = run * bpw;
+  const int64_t k1 = k0 + bpw < g.nb ? k0 + bpw : g.nb;
   const int col = lane & 15, q = lane >> 4;
   const int64_t ch = cg * 16 + col;
   const float *xr = x + (ch < g.n_ch ? ch : g.n_ch - 1) * s_ch;  // channel row
@@ -1238,12 +1240,18 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   int pf = 2, mode = 0;
   if (const char *v = std::getenv("LFD_MF_PF")) pf = std::atoi(v);
   if (const char *v = std::getenv("LFD_MF_MODE")) mode = std::atoi(v);
-  const int64_t n_runs = (g.nb + MF_RUN - 1) / MF_RUN;
-  const int64_t units = ((g.n_ch + 15) / 16) * n_runs;
+  // blocks per wave: MF_RUN when the array is wide; narrow arrays (the
+  // real-time edge runs: 2,000 channels, 44 blocks of 2,000 samples) get
+  // fewer so that >= ~4,096 waves (16 per CU) cover the chip
+  const int64_t n_cg = (g.n_ch + 15) / 16;
+  int bpw = (int)std::max<int64_t>(1, std::min<int64_t>(MF_RUN, n_cg * g.nb / 4096));
+  if (const char *v = std::getenv("LFD_MF_BPW")) bpw = std::max(1, std::min(MF_RUN, std::atoi(v)));
+  const int64_t n_runs = (g.nb + bpw - 1) / bpw;
+  const int64_t units = n_cg * n_runs;
   const unsigned grid = nblk(units, threads / 64);
 #define LFD_MF(PF_, MODE_)                                                                      \
   k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
-                                                                   n_runs)
+                                                                   n_runs, bpw)
   if (mode == 1)
     LFD_MF(2, 1);
   else if (mode == 3)

@@ -140,6 +140,7 @@ def load():
         "lfd_stream_last_chunks": ([vp, vp, i64, P(i64)], i32),
         "lfd_stream_fetch": ([vp, vp, i64, i64], i32),
         "lfd_stream_synchronize": ([vp], i32),
+        "lfd_stream_wait_copy": ([vp], i32),
         "lfd_stream_last_timing": ([vp, P(ctypes.c_float), P(ctypes.c_float)], i32),
         "lfd_stream_info": ([vp, P(i64), P(i64), P(i64)], i32),
         "lfd_stream_close": ([vp], None),
@@ -164,7 +165,7 @@ EXPORTED = (
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32",
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
-    "lfd_stream_synchronize", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
+    "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
     "lfd_host_alloc", "lfd_host_free",
 )
 

@@ -180,6 +180,11 @@ class LowpassStream:
         self._keep.clear()
         return out
 
+    def wait_copy(self):
+        """Block until the last push's host buffer has been copied to HBM."""
+        check(self._lib.lfd_stream_wait_copy(self._h))
+        self._keep.clear()
+
     def synchronize(self):
         check(self._lib.lfd_stream_synchronize(self._h))
         self._keep.clear()
