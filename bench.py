@@ -142,6 +142,7 @@ def bench_edge_cfg4(dev, n_push=12, warm=2, time_major=False):
     shape = (push, n_ch) if time_major else (n_ch, push)
     blocks = _pinned_blocks(dev, 2, shape, fs, 4321)
     st = LowpassStream(n_ch, dt_ns, 1.0, 125, 7, mode="edge", t_start=t0)
+    st.reserve(push)
     lat, cp, run, n_out = [], [], [], []
     set_timing(True)
     for k in range(n_push + warm):
@@ -183,13 +184,19 @@ def bench_ooc_cfg5(dev, n_ch=50_000, seconds=3600.0, push_s=60.0):
     blocks = _pinned_blocks(dev, 2, (n_ch, push), fs, 777)
     st = LowpassStream(n_ch, dt_ns, 10.0, 120, 6, mode="continuous", t_start=t0,
                        t_end=t0 + (n - 1) * dt_ns, capacity=int(1300 * fs) + 2 * push)
+    from lfdas.plan import set_timing
+    st.reserve(push)
     n_out = 0
+    cp = []
     torch.cuda.synchronize(dev)
+    set_timing(True)
     ta = time.perf_counter()
     for k in range(n // push):
         o = st.push(blocks[k % 2], t0 + k * push * dt_ns)
         n_out += o.n_out
         st.wait_copy()  # ring buffer (k+1) % 2 is free again
+        cp.append(st.last_timing_ms()[0])
+    set_timing(False)
     o = st.flush()
     n_out += o.n_out
     st.synchronize()
@@ -200,8 +207,71 @@ def bench_ooc_cfg5(dev, n_ch=50_000, seconds=3600.0, push_s=60.0):
     return {"value": samples / el, "unit": "channel-samples/s", "seconds_streamed": seconds,
             "wall_s": el, "h2d_GBps": samples * 4 / el / 1e9, "pcie_peak_GBps": 63.0,
             "pcie_frac": samples * 4 / el / 1e9 / 63.0, "outputs_per_channel": n_out,
+            "copy_ms_p50": float(np.median(cp)), "copy_ms_max": float(np.max(cp)),
             "config": f"{n_ch:,} ch @ 200 Hz, {seconds:.0f} s of the 24 h spool in {push_s:.0f} s pinned "
                       "pushes, dt = 10 s, P = 120, B = 6, 1 GPU"}
+
+
+def _cpu_worker(a, barrier=None, q=None):
+    """One CPU-baseline process: the LFProc chunks of ``n_c`` channels x the
+    full hour through the oracle C sosfiltfilt + interp1d (own data, made
+    before the start barrier)."""
+    fs, seconds, n_c, seed, sos, sched, t0, dt_ns, tg = a
+    sys.path.insert(0, ROOT)
+    import oracle
+    from lfdas import schedule as S
+    n = int(seconds * fs)
+    rng = np.random.default_rng(seed)
+    t = np.arange(n, dtype=np.float64) * (2 * np.pi * 0.05 / fs)
+    x = (rng.standard_normal((n_c, n)) + 0.5 + np.sin(t)[None, :]).astype(np.float32)
+    if barrier is not None:
+        barrier.wait()
+    ta = time.perf_counter()
+    for a_, b_, oa, ob in sched:
+        s0, s1 = S.select_range(t0, dt_ns, n, tg[a_], tg[b_])
+        y = oracle.sosfiltfilt_rows_c(sos, x[:, s0:s1 + 1])
+        tt = (np.arange(s0, s1 + 1, dtype=np.int64) * dt_ns).astype(np.float64)
+        oracle.interp1d_linear(tt, y, (tg[oa:ob] - t0).astype(np.float64))
+    el = time.perf_counter() - ta
+    if q is not None:
+        q.put(el)
+    return el
+
+
+def cpu_workers() -> int:
+    """The host cores this job may use: the box's CPU share (OMP_NUM_THREADS,
+    16 per GPU on the pool) bounded by the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(aff, cap, 16))
+
+
+def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48):
+    """SURVEY §8(d) figure 2: one worker PROCESS per core over channel blocks
+    (SciPy's _sosfilt does not scale with threads).  Forked before the GPU is
+    initialised.  Channel-sample rate of the whole pool (wall clock)."""
+    import multiprocessing as mp
+    nw = cpu_workers()
+    ctx = mp.get_context("fork")
+    barrier = ctx.Barrier(nw + 1)
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=((args.fs, args.seconds, n_c_per, 100 + i, sos, sched,
+                                                     t0, dt_ns, tg), barrier, q)) for i in range(nw)]
+    for p in procs:
+        p.start()
+    barrier.wait()  # every worker holds its data
+    ta = time.perf_counter()
+    per = [q.get(timeout=600) for _ in procs]
+    wall = time.perf_counter() - ta
+    for p in procs:
+        p.join()
+    n = int(args.seconds * args.fs)
+    return {"value": nw * n_c_per * n / wall, "cores": nw, "wall_s": wall,
+            "sample": f"{nw} processes x {n_c_per} ch x {n} samples, same LFProc chunks, oracle C "
+                      f"sosfiltfilt + interp1d; per-process {min(per):.1f}-{max(per):.1f} s"}
 
 
 def main():
@@ -218,6 +288,24 @@ def main():
     from lfdas.plan import set_timing
     n_ch = args.channels
     n = int(args.seconds * args.fs)
+    cpu = None
+    if ws == 1 and not args.no_cpu:
+        # host-only plan geometry (the library's schedule), then the CPU legs
+        # before the GPU is initialised (the parallel leg forks)
+        from lfdas import schedule as S
+        from lfdas.design import lowpass_sos
+        c_dt_ns = int(round(1e9 / args.fs))
+        c_t0 = 1_505_692_800_000_000_000
+        c_tg = S.time_grid(c_t0, c_t0 + n * c_dt_ns, args.dt_out)
+        c_sched = S.lfproc_chunks(len(c_tg), args.patch_size, args.edge_buff)
+        c_sos = lowpass_sos(args.fs, 1 / args.dt_out / 2 * 0.9, 4)
+        one = cpu_baseline(args, c_sos, c_sched, c_t0, c_dt_ns, c_tg)
+        par = cpu_baseline_parallel(args, c_sos, c_sched, c_t0, c_dt_ns, c_tg)
+        cpu = {"value": par["value"], "unit": "channel-samples/s", "cores": par["cores"], "kind": "port",
+               "extrapolated": True,
+               "sample": par["sample"] + "; rate extrapolated linearly to the full 10,000-channel step",
+               "single_process": {"value": one["value"], "cores": 1, "sample": one["sample"]},
+               "workers": "processes (fork) over channel blocks"}
     plan, sched, sos, t0, dt_ns, tg = build_plan(n_ch, n, args.fs, args.dt_out, args.patch_size,
                                                  args.edge_buff)
     x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
@@ -303,9 +391,6 @@ def main():
         secondary["out_of_core_cfg5"] = bench_ooc_cfg5(dev)
         torch.cuda.empty_cache()
 
-    cpu = None
-    if ws == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, sos, sched, t0, dt_ns, tg)
 
     if rank == 0:
         out = {

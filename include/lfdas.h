@@ -225,6 +225,10 @@ typedef struct lfd_stream lfd_stream;
 /* Device streams, events and the arena live on the current device. */
 int lfd_stream_open(lfd_stream **s, const lfd_stream_config *cfg, const double *sos,
                     int n_sec, int padlen);
+/* Allocate the arena (capacity max(cfg capacity, 4*max_push)) and the
+ * staging buffer for pushes of up to max_push samples now, so that no push
+ * allocates (device allocation after large frees can take seconds). */
+int lfd_stream_reserve(lfd_stream *s, int64_t max_push);
 /* Append n_t samples of every channel starting at time t0_ns.  x is a HOST
  * array addressed by element strides (s_t == 1: (channel, time) rows;
  * s_ch == 1: (time, channel) rows, transposed on device).  Pinned x

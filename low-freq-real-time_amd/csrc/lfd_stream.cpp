@@ -503,6 +503,16 @@ int lfd_stream_open(lfd_stream **out, const lfd_stream_config *cfg, const double
   return LFD_OK;
 }
 
+int lfd_stream_reserve(lfd_stream *s, int64_t max_push) {
+  if (!s) return fail(LFD_EINVAL, "stream is NULL");
+  if (max_push < 1) return fail(LFD_EINVAL, "max_push must be >= 1");
+  DeviceGuard g(s->device);
+  const int64_t want = round_up(std::max<int64_t>(s->cfg.capacity, 4 * max_push), 64);
+  if (want > s->cap) LFD_TRY(alloc_arena(s, want));
+  if (!s->dry) LFD_TRY(ensure_stage(s, sizeof(float) * (size_t)max_push * (size_t)s->cfg.n_ch));
+  return LFD_OK;
+}
+
 int lfd_stream_push(lfd_stream *s, const float *x, int64_t n_t, int64_t s_ch, int64_t s_t, int64_t t0_ns) {
   if (!s) return fail(LFD_EINVAL, "stream is NULL");
   if (n_t < 1) return fail(LFD_EINVAL, "push needs n_t >= 1");

@@ -135,6 +135,7 @@ def load():
         "lfd_lfproc_schedule": ([i64, i64, i64, vp, i64, P(i64)], i32),
         "lfd_stream_open": ([P(vp), vp, vp, i32, i32], i32),
         "lfd_stream_push": ([vp, vp, i64, i64, i64, i64], i32),
+        "lfd_stream_reserve": ([vp, i64], i32),
         "lfd_stream_flush": ([vp], i32),
         "lfd_stream_last_output": ([vp, vp], i32),
         "lfd_stream_last_chunks": ([vp, vp, i64, P(i64)], i32),
@@ -163,7 +164,7 @@ EXPORTED = (
     "lfd_sos_filtfilt_resample_f32",
     "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32",
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32",
-    "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_push", "lfd_stream_flush",
+    "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
     "lfd_host_alloc", "lfd_host_free",

@@ -110,6 +110,11 @@ class LowpassStream:
         self._keep = []  # host buffers of pushes whose DMA may still be in flight
 
     # -- pushing -------------------------------------------------------
+    def reserve(self, max_push: int):
+        """Allocate the arena and staging for pushes of up to ``max_push``
+        samples now (keeps allocation out of the first pushes)."""
+        check(self._lib.lfd_stream_reserve(self._h, int(max_push)))
+
     def push(self, x, t0, time_axis: int = 1) -> StreamOutput:
         """Append host samples ``x`` (2-D, channels x time for ``time_axis=1``,
         time x channels for ``time_axis=0``; float32 numpy array or CPU torch

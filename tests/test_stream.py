@@ -103,6 +103,8 @@ def test_continuous_dry_run_matches_process_time_range(push_s):
 
 def test_stream_gap_and_config_errors():
     s = ST.LowpassStream(2, 4_000_000, 1.0, 40, 6, dry_run=True, t_start=T0)
+    s.reserve(100)
+    assert s.info()[0] >= 400
     s.push(np.zeros((2, 100), np.float32), T0)
     with pytest.raises(ValueError, match="patch merge failed! Gap in data exists"):
         s.push(np.zeros((2, 100), np.float32), T0 + 101 * 4_000_000)

@@ -12,8 +12,8 @@ TAG=${1:-r01}; shift || true
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu --no-rolling "$@" > $OUT/bench_traced.log 2>&1
-FULL="--steps 2 --warmup 0 --no-cpu --no-rolling"
+    python3 bench.py --steps 5 --warmup 1 --no-cpu --no-rolling --no-stream "$@" > $OUT/bench_traced.log 2>&1
+FULL="--steps 2 --warmup 0 --no-cpu --no-rolling --no-stream"
 timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch --pmc FETCH_SIZE \
     --kernel-include-regex k_block_ -- python3 bench.py $FULL "$@" > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_write -o write --pmc WRITE_SIZE \
