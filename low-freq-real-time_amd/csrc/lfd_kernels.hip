@@ -464,6 +464,15 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   constexpr int NF = 2 * N + 1;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n_thr = n_chunks * g.n_ch;
+  // run mode: the run-algebra constants live in LDS (read every run step;
+  // from global they put two dependent load latencies on each step)
+  __shared__ RunConst rcs[1];
+  if constexpr (RUNS) {
+    const double *src = &rg.rc->PhiFp[0][0];
+    double *dst = &rcs[0].PhiFp[0][0];
+    for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
   if (tid >= n_thr) return;
   const int64_t ch = tid % g.n_ch;
   const int64_t c = tid / g.n_ch;
@@ -517,16 +526,34 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   const int64_t nF = NF;
   if constexpr (RUNS) {
     static_assert(N == RUN_N, "run mode is 4th order");
-    const RunConst &rc = *rg.rc;
+    const RunConst &rc = rcs[0];
+    // software-pipelined: run r+1's aggregates and length load while run r
+    // is applied
+    const double *agb = F + (((ch >> 4) * rg.n_runs) * 8) * 16 + (ch & 15);
+    double agn[N];
+    int lenn = 0;
+    if (G.r0 < G.r1) {
+      lenn = rg.run_len[G.r0];
+#pragma unroll
+      for (int i = 0; i < N; ++i) agn[i] = agb[(G.r0 * 8 + i) * 16];
+    }
     for (int64_t r = G.r0; r < G.r1; ++r) {
+      double agc[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) agc[i] = agn[i];
+      const int len = lenn;
+      if (r + 1 < G.r1) {
+        lenn = rg.run_len[r + 1];
+#pragma unroll
+        for (int i = 0; i < N; ++i) agn[i] = agb[((r + 1) * 8 + i) * 16];
+      }
       double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
-      const double *ag = F + (((ch >> 4) * rg.n_runs + r) * 8) * 16 + (ch & 15);
-      const double *P = rc.PhiFp[rg.run_len[r]];
+      const double *P = rc.PhiFp[len];
       double ns[N];
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         sr[i * SF_ISTRIDE] = S[i];
-        double acc = ag[i * 16] + (r == G.r0 ? corr[i] : 0.0);
+        double acc = agc[i] + (r == G.r0 ? corr[i] : 0.0);
 #pragma unroll
         for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
         ns[i] = acc;
@@ -592,20 +619,40 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 
   // ---- backward scan, outputs at block starts
   if constexpr (RUNS) {
-    const RunConst &rc = *rg.rc;
-    for (int64_t r = G.r1 - 1; r >= G.r0; --r) {
+    const RunConst &rc = rcs[0];
+    // software-pipelined like the forward scan: run r-1's inputs (S_in,
+    // E_r, y0 of its blocks, length, first block) load while run r is applied
+    struct RunIn {
+      double sin[N], er[N], y0[RUN_R];
+      int len;
+      int64_t ks;
+    };
+    const double *agb = F + (((ch >> 4) * rg.n_runs) * 8) * 16 + (ch & 15);
+    const double *y0b = Y0 + ((ch >> 4) * g.nb) * 16 + (ch & 15);
+    auto load_run = [&](int64_t r, RunIn &o) {
+      o.len = rg.run_len[r];
+      o.ks = rg.run_ks[r];
       const double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
-      const double *ag = F + (((ch >> 4) * rg.n_runs + r) * 8) * 16 + (ch & 15);
-      const int len = rg.run_len[r];
-      const int64_t ks = rg.run_ks[r];
-      double sin[N];
 #pragma unroll
-      for (int i = 0; i < N; ++i) sin[i] = sr[i * SF_ISTRIDE];
-      const double *y0p = Y0 + ((ch >> 4) * g.nb + ks) * 16 + (ch & 15);
-      for (int pp = 0; pp < len; ++pp) {
+      for (int i = 0; i < N; ++i) {
+        o.sin[i] = sr[i * SF_ISTRIDE];
+        o.er[i] = agb[(r * 8 + 4 + i) * 16];
+      }
+#pragma unroll
+      for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = pp < o.len ? y0b[(o.ks + pp) * 16] : 0.0;
+    };
+    RunIn cur, nxt;
+    if (G.r0 < G.r1) load_run(G.r1 - 1, cur);
+    for (int64_t r = G.r1 - 1; r >= G.r0; --r) {
+      if (r - 1 >= G.r0) load_run(r - 1, nxt);
+      const int len = cur.len;
+      const int64_t ks = cur.ks;
+      const double *sin = cur.sin;
+#pragma unroll
+      for (int pp = 0; pp < RUN_R; ++pp) {
         const int64_t k = ks + pp;
-        if (k < G.kout0 || k >= G.kout1) continue;
-        double acc = y0p[pp * 16] + (k == G.kb ? corr[2 * N] : 0.0);
+        if (pp >= len || k < G.kout0 || k >= G.kout1) continue;
+        double acc = cur.y0[pp] + (k == G.kb ? corr[2 * N] : 0.0);
         const double *A = rc.A[len][pp];
         const double *B = rc.B[len - 1 - pp];
 #pragma unroll
@@ -619,7 +666,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       double nr[N];
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        double acc = ag[(4 + i) * 16] + (r == G.r0 ? corr[N + i] : 0.0);
+        double acc = cur.er[i] + (r == G.r0 ? corr[N + i] : 0.0);
 #pragma unroll
         for (int j = 0; j < N; ++j) {
           acc = fma(PR[i * 4 + j], T[j], acc);
@@ -629,6 +676,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) T[i] = nr[i];
+      cur = nxt;
     }
     return;
   }
