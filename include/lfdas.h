@@ -278,6 +278,22 @@ void lfd_stream_close(lfd_stream *s);
 int lfd_host_alloc(void **p, size_t bytes);
 void lfd_host_free(void *p);
 
+/* ------------------------------------------------------------------------
+ * Post-processing of the decimated output (low_pass_dascore.ipynb cells
+ * 14-22, notebook numpy/scipy code run on device):
+ *   lfd_demean_scale_f64: y[r, c] = (x[r, c] - mean(x[r, c0:c1])) * scale per
+ *     time row r ((time, distance) rows: the notebook's
+ *     (filtered - mean(filtered[:, c0:c1], axis=1)) * scale_iDAS).
+ *   lfd_median_filter_f64: scipy.ndimage.median_filter(x, size=(k0, k1)) with
+ *     mode 'reflect', origin 0, rank = k0*k1 // 2 (bit-exact: the output is an
+ *     input value; NaN-free input).  1-D traces: n0 = 1, k0 = 1.
+ * ------------------------------------------------------------------------ */
+int lfd_demean_scale_f64(const double *x, int64_t n_rows, int64_t n_cols, int64_t s_r, int64_t s_c,
+                         int64_t c0, int64_t c1, double scale, double *y, int64_t ys_r, int64_t ys_c,
+                         void *stream);
+int lfd_median_filter_f64(const double *x, int64_t n0, int64_t n1, int64_t s0, int64_t s1, int k0, int k1,
+                          double *y, int64_t ys0, int64_t ys1, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1019,4 +1019,29 @@ int lfd_rolling_mean_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch
   return LFD_OK;
 }
 
+int lfd_demean_scale_f64(const double *x, int64_t n_rows, int64_t n_cols, int64_t s_r, int64_t s_c,
+                         int64_t c0, int64_t c1, double scale, double *y, int64_t ys_r, int64_t ys_c,
+                         void *stream) {
+  if (n_rows < 0 || n_cols < 0) return fail(LFD_EINVAL, "negative size");
+  if (c0 < 0 || c1 > n_cols || c1 <= c0) return fail(LFD_EINVAL, "demean channel range must be inside [0, n_cols) and non-empty");
+  if (n_rows == 0) return LFD_OK;
+  if (!x || !y) return fail(LFD_EINVAL, "x and y must be device pointers");
+  LFD_HIP(lfd::launch_demean_scale(x, n_rows, n_cols, s_r, s_c, c0, c1, scale, y, ys_r, ys_c,
+                                   reinterpret_cast<hipStream_t>(stream)));
+  return LFD_OK;
+}
+
+int lfd_median_filter_f64(const double *x, int64_t n0, int64_t n1, int64_t s0, int64_t s1, int k0, int k1,
+                          double *y, int64_t ys0, int64_t ys1, void *stream) {
+  if (n0 < 0 || n1 < 0) return fail(LFD_EINVAL, "negative size");
+  if (k0 < 1 || k1 < 1) return fail(LFD_EINVAL, "median window sizes must be >= 1");
+  if ((size_t)(16 + k0 - 1) * (size_t)(16 + k1 - 1) * sizeof(double) > 64 * 1024)
+    return fail(LFD_EUNSUPPORTED, "median window too large for one LDS tile");
+  if (n0 == 0 || n1 == 0) return LFD_OK;
+  if (!x || !y) return fail(LFD_EINVAL, "x and y must be device pointers");
+  if (x == y) return fail(LFD_EINVAL, "median filter cannot run in place");
+  LFD_HIP(lfd::launch_median2d(x, n0, n1, s0, s1, k0, k1, y, ys0, ys1, reinterpret_cast<hipStream_t>(stream)));
+  return LFD_OK;
+}
+
 }  // extern "C"

@@ -188,5 +188,12 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
 // dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.
 hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
                             int64_t dp, hipStream_t st);
+// Notebook post-processing (low_pass_dascore.ipynb cells 14-22).
+hipError_t launch_demean_scale(const double *x, int64_t n_rows, int64_t n_cols, int64_t s_r, int64_t s_c,
+                               int64_t c0, int64_t c1, double scale, double *y, int64_t ys_r, int64_t ys_c,
+                               hipStream_t st);
+// scipy.ndimage.median_filter(x, size=(k0, k1), mode='reflect'); LDS tile <= 64 KB.
+hipError_t launch_median2d(const double *x, int64_t n0, int64_t n1, int64_t s0, int64_t s1, int k0, int k1,
+                           double *y, int64_t ys0, int64_t ys1, hipStream_t st);
 
 }  // namespace lfd

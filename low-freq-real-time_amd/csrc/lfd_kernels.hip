@@ -1446,4 +1446,94 @@ hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, in
   return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// Notebook post-processing of the decimated output (low_pass_dascore.ipynb
+// cells 14-22): demean over a channel range + strain-rate scale, and
+// scipy.ndimage.median_filter (mode 'reflect', origin 0, rank = n // 2).
+// ---------------------------------------------------------------------------
+
+// One wave per time row: mean over channels [c0, c1) (float64 sum, lane
+// strided then a wave reduction), then y = (x - mean) * scale over the row.
+__global__ __launch_bounds__(256) void k_demean_scale(const double *__restrict__ x, int64_t n_rows,
+                                                      int64_t n_cols, int64_t s_r, int64_t s_c, int64_t c0,
+                                                      int64_t c1, double scale, double *__restrict__ y,
+                                                      int64_t ys_r, int64_t ys_c) {
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n_rows) return;
+  const double *xr = x + row * s_r;
+  double acc = 0.0;
+  for (int64_t c = c0 + lane; c < c1; c += 64) acc += xr[c * s_c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  const double mean = acc / (double)(c1 - c0);
+  double *yr = y + row * ys_r;
+  for (int64_t c = lane; c < n_cols; c += 64) yr[c * ys_c] = (xr[c * s_c] - mean) * scale;
+}
+
+__device__ __forceinline__ int64_t reflect_idx(int64_t i, int64_t n) {
+  // scipy.ndimage 'reflect' (half-sample symmetric, period 2n): d c b a | a b c d | d c b a
+  if (n == 1) return 0;
+  const int64_t p = 2 * n;
+  i %= p;
+  if (i < 0) i += p;
+  return i < n ? i : p - 1 - i;
+}
+
+constexpr int MED_T = 16;  // output tile edge
+
+// 16x16 outputs per workgroup; the (16+k0-1) x (16+k1-1) input tile (reflect
+// padded) is staged in LDS; each output selects the rank-th smallest of its
+// k0*k1 window by counting (exact: the result is one of the inputs).
+__global__ __launch_bounds__(256) void k_median2d(const double *__restrict__ x, int64_t n0, int64_t n1,
+                                                  int64_t s0, int64_t s1, int k0, int k1,
+                                                  double *__restrict__ y, int64_t ys0, int64_t ys1) {
+  extern __shared__ double tile[];
+  const int T1 = MED_T + k1 - 1, T0 = MED_T + k0 - 1;
+  const int64_t b0 = (int64_t)blockIdx.y * MED_T - k0 / 2, b1 = (int64_t)blockIdx.x * MED_T - k1 / 2;
+  for (int idx = threadIdx.x; idx < T0 * T1; idx += blockDim.x) {
+    const int r = idx / T1, c = idx % T1;
+    tile[idx] = x[reflect_idx(b0 + r, n0) * s0 + reflect_idx(b1 + c, n1) * s1];
+  }
+  __syncthreads();
+  const int tx = threadIdx.x % MED_T, ty = threadIdx.x / MED_T;
+  const int64_t i = (int64_t)blockIdx.y * MED_T + ty, j = (int64_t)blockIdx.x * MED_T + tx;
+  if (i >= n0 || j >= n1) return;
+  const int n = k0 * k1, rank = n / 2;
+  const double *w = tile + ty * T1 + tx;
+  double res = w[0];
+  for (int a = 0; a < n; ++a) {
+    const double v = w[(a / k1) * T1 + a % k1];
+    int lt = 0, eq = 0;
+    for (int b = 0; b < n; ++b) {
+      const double u = w[(b / k1) * T1 + b % k1];
+      lt += u < v;
+      eq += u == v;
+    }
+    if (lt <= rank && rank < lt + eq) {
+      res = v;
+      break;
+    }
+  }
+  y[i * ys0 + j * ys1] = res;
+}
+
+hipError_t launch_demean_scale(const double *x, int64_t n_rows, int64_t n_cols, int64_t s_r, int64_t s_c,
+                               int64_t c0, int64_t c1, double scale, double *y, int64_t ys_r, int64_t ys_c,
+                               hipStream_t st) {
+  if (n_rows <= 0) return hipSuccess;
+  k_demean_scale<<<nblk(n_rows, 4), 256, 0, st>>>(x, n_rows, n_cols, s_r, s_c, c0, c1, scale, y, ys_r, ys_c);
+  return hipGetLastError();
+}
+
+hipError_t launch_median2d(const double *x, int64_t n0, int64_t n1, int64_t s0, int64_t s1, int k0, int k1,
+                           double *y, int64_t ys0, int64_t ys1, hipStream_t st) {
+  if (n0 <= 0 || n1 <= 0) return hipSuccess;
+  const size_t lds = sizeof(double) * (size_t)(MED_T + k0 - 1) * (size_t)(MED_T + k1 - 1);
+  if (lds > 64 * 1024 || (n0 + MED_T - 1) / MED_T > 65535) return hipErrorInvalidValue;
+  dim3 grid((unsigned)((n1 + MED_T - 1) / MED_T), (unsigned)((n0 + MED_T - 1) / MED_T));
+  k_median2d<<<grid, 256, lds, st>>>(x, n0, n1, s0, s1, k0, k1, y, ys0, ys1);
+  return hipGetLastError();
+}
+
 }  // namespace lfd

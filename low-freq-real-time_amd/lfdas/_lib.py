@@ -133,6 +133,8 @@ def load():
         "lfd_rolling_mean_f32": ([vp, i64, i64, i64, i64, i64, i64, vp, i64, i64,
                                   vp], i32),
         "lfd_lfproc_schedule": ([i64, i64, i64, vp, i64, P(i64)], i32),
+        "lfd_demean_scale_f64": ([vp, i64, i64, i64, i64, i64, i64, ctypes.c_double, vp, i64, i64, vp], i32),
+        "lfd_median_filter_f64": ([vp, i64, i64, i64, i64, i32, i32, vp, i64, i64, vp], i32),
         "lfd_stream_open": ([P(vp), vp, vp, i32, i32], i32),
         "lfd_stream_push": ([vp, vp, i64, i64, i64, i64], i32),
         "lfd_stream_reserve": ([vp, i64], i32),
@@ -167,7 +169,7 @@ EXPORTED = (
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
-    "lfd_host_alloc", "lfd_host_free",
+    "lfd_host_alloc", "lfd_host_free", "lfd_demean_scale_f64", "lfd_median_filter_f64",
 )
 
 

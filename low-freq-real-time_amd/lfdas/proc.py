@@ -135,18 +135,46 @@ def interpolate(patch: Patch, kind="linear", **kwargs):
 
 
 def decimate(patch: Patch, filter_type=None, **kwargs):
-    if filter_type not in (None, False):
-        raise NotImplementedError("decimate with an anti-alias filter is a next-row item; "
-                                  "use pass_filter(...).interpolate(...) (the LFProc path)")
+    """``Patch.decimate(time=q, filter_type=None | 'iir')``.  ``None``: every
+    q-th sample.  ``'iir'``: restated as ``scipy.signal.decimate(x, q,
+    ftype='iir', axis=time, zero_phase=True)`` — 8th-order Chebyshev I at
+    0.8/q (designed on the host), zero-phase ``sosfiltfilt`` and the q-th
+    sample pick fused in one device pass (``lfd_sos_filtfilt_resample_f32``,
+    grid = every q-th sample).  *(DASCore, external: the wrapper is unpinned;
+    ``'fir'`` (resample_poly) is not on the device path.)*"""
+    if len(kwargs) != 1:
+        raise ValueError("decimate takes exactly one dimension keyword, e.g. time=5")
     (dim, q), = kwargs.items()
     q = int(q)
+    if q < 1:
+        raise ValueError("decimation factor must be >= 1")
     ax = patch.dims.index(dim)
-    idx = [slice(None)] * len(patch.dims)
-    idx[ax] = slice(None, None, q)
     coords = dict(patch.coords.coord_map)
     coords[dim] = coords[dim][::q]
-    return Patch(data=patch.device_data()[tuple(idx)], coords=coords, dims=patch.dims,
-                 attrs=patch._attrs_wo_coords())
+    if filter_type in (None, False):
+        idx = [slice(None)] * len(patch.dims)
+        idx[ax] = slice(None, None, q)
+        return Patch(data=patch.device_data()[tuple(idx)], coords=coords, dims=patch.dims,
+                     attrs=patch._attrs_wo_coords())
+    if str(filter_type).lower() != "iir":
+        raise NotImplementedError(f"decimate filter_type={filter_type!r} is not on the device path "
+                                  "(supported: None, 'iir')")
+    if dim != "time":
+        raise NotImplementedError("only time-axis decimation is on the device path")
+    import scipy.signal as _sig
+
+    from .plan import filtfilt_resample_device
+    sos = np.ascontiguousarray(_sig.cheby1(8, 0.05, 0.8 / q, output="sos"), dtype=np.float64)
+    padlen = default_padlen(sos)
+    n_t = patch.shape[ax]
+    if n_t <= padlen:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {padlen}.")
+    lo = np.arange(0, n_t, q, dtype=np.int64)
+    w = np.zeros(len(lo))
+    x = to_device_ct(patch)
+    y = filtfilt_resample_device(x, sos, lo, w, padlen)
+    data = _from_ct(y, patch.dims).astype(np.float64)
+    return Patch(data=data, coords=coords, dims=patch.dims, attrs=patch._attrs_wo_coords())
 
 
 def _to_samples(patch: Patch, v) -> int:

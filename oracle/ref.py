@@ -21,7 +21,8 @@ __all__ = [
     "pass_filter", "interpolate", "rolling_mean", "rolling_out_times",
     "get_patch_time", "lfproc_time_grid", "lfproc_schedule", "lfproc_process",
     "down_sample_processing", "get_edge_effect_time", "have_c_oracle",
-    "sosfiltfilt_rows_c", "edge_loop",
+    "sosfiltfilt_rows_c", "edge_loop", "lp2bp_zpk", "cheb1ap", "cheby1_sos", "decimate_iir",
+    "median_filter", "demean_scale",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -112,6 +113,84 @@ def bilinear_zpk(z, p, k, fs):
     return z_z, p_z, k_z
 
 
+def lp2bp_zpk(z, p, k, wo=1.0, bw=1.0):
+    """scipy/signal/_filter_design.py lp2bp_zpk: low-pass prototype → band-pass
+    centred on ``wo`` with bandwidth ``bw``."""
+    z = np.atleast_1d(z)
+    p = np.atleast_1d(p)
+    wo = float(wo)
+    bw = float(bw)
+    degree = _relative_degree(z, p)
+    z_lp = (z * bw / 2).astype(complex)
+    p_lp = (p * bw / 2).astype(complex)
+    z_bp = np.concatenate((z_lp + np.sqrt(z_lp ** 2 - wo ** 2), z_lp - np.sqrt(z_lp ** 2 - wo ** 2)))
+    p_bp = np.concatenate((p_lp + np.sqrt(p_lp ** 2 - wo ** 2), p_lp - np.sqrt(p_lp ** 2 - wo ** 2)))
+    z_bp = np.append(z_bp, np.zeros(degree))
+    return z_bp, p_bp, k * bw ** degree
+
+
+def cheb1ap(N: int, rp: float):
+    """scipy/signal/_filter_design.py cheb1ap: analog Chebyshev type I
+    prototype (``rp`` dB ripple)."""
+    if N == 0:
+        return np.array([]), np.array([]), 10 ** (-rp / 20)
+    z = np.array([])
+    eps = np.sqrt(10 ** (0.1 * rp) - 1.0)
+    mu = 1.0 / N * np.arcsinh(1 / eps)
+    m = np.arange(-N + 1, N, 2)
+    theta = np.pi * m / (2 * N)
+    p = -np.sinh(mu + 1j * theta)
+    k = np.prod(-p, axis=0).real
+    if N % 2 == 0:
+        k = k / np.sqrt(1 + eps * eps)
+    return z, p, k
+
+
+def cheby1_sos(N: int, rp: float, Wn: float):
+    """``scipy.signal.cheby1(N, rp, Wn, output='sos')`` (digital low-pass):
+    iirfilter's digital branch (fs = 2, prewarp) → lp2lp → bilinear → zpk2sos."""
+    z, p, k = cheb1ap(N, rp)
+    fs = 2.0
+    warped = 2 * fs * np.tan(np.pi * float(Wn) / fs)
+    z, p, k = lp2lp_zpk(z, p, k, wo=warped)
+    z, p, k = bilinear_zpk(z, p, k, fs=fs)
+    return zpk2sos(z, p, k)
+
+
+def decimate_iir(x, q: int, axis: int = -1):
+    """``scipy.signal.decimate(x, q, ftype='iir', axis=axis, zero_phase=True)``
+    (scipy/signal/_signaltools.py decimate): 8th-order Chebyshev I at
+    ``0.8/q``, ``sosfiltfilt``, then every q-th sample.  (DASCore's
+    ``Patch.decimate(filter_type='iir')`` is restated as this call; the
+    wrapper itself is external and unpinned.)  float64 data."""
+    sos = cheby1_sos(8, 0.05, 0.8 / q)
+    y = sosfiltfilt(sos, np.asarray(x, dtype=np.float64), axis=axis)
+    sl = [slice(None)] * y.ndim
+    sl[axis] = slice(None, None, q)
+    return y[tuple(sl)]
+
+
+def median_filter(a, size):
+    """``scipy.ndimage.median_filter(a, size=size)`` (mode 'reflect' =
+    half-sample symmetric, origin 0, rank = window // 2) —
+    scipy/ndimage/_filters.py median_filter → _rank_filter."""
+    a = np.asarray(a)
+    k = (int(size),) * a.ndim if np.ndim(size) == 0 else tuple(int(v) for v in size)
+    pad = [(kk // 2, kk - 1 - kk // 2) for kk in k]
+    padded = np.pad(a, pad, mode="symmetric")
+    win = np.lib.stride_tricks.sliding_window_view(padded, k)
+    flat = win.reshape(a.shape + (-1,))
+    n = flat.shape[-1]
+    return np.partition(flat, n // 2, axis=-1)[..., n // 2]
+
+
+def demean_scale(data, ch_start: int, ch_end: int, scale: float):
+    """low_pass_dascore.ipynb cells 14/18/22 on (time, distance) data:
+    ``(data - mean(data[:, c0:c1], axis=1).reshape(-1, 1)) * scale_iDAS``."""
+    data = np.asarray(data, dtype=np.float64)
+    return (data - np.mean(data[:, ch_start:ch_end], axis=1).reshape(-1, 1)) * scale
+
+
 def iirfilter_butter_zpk(N: int, Wn: float, btype: str = "lowpass"):
     """Digital Butterworth zpk, as scipy.signal.iirfilter(N, Wn, btype=...,
     ftype='butter', output='zpk') — scipy/signal/_filter_design.py:2443-2680
@@ -123,6 +202,10 @@ def iirfilter_butter_zpk(N: int, Wn: float, btype: str = "lowpass"):
         z, p, k = lp2lp_zpk(z, p, k, wo=float(warped))
     elif btype in ("highpass", "high"):
         z, p, k = lp2hp_zpk(z, p, k, wo=float(warped))
+    elif btype in ("bandpass", "band"):
+        bw = warped[1] - warped[0]
+        wo = np.sqrt(warped[0] * warped[1])
+        z, p, k = lp2bp_zpk(z, p, k, wo=wo, bw=bw)
     else:
         raise NotImplementedError(btype)
     return bilinear_zpk(z, p, k, fs=fs)
@@ -396,7 +479,7 @@ def dascore_pass_filter_sos(fs: float, lo, hi, corners: int = 4):
         return butter_sos(corners, hi / nyquist, "lowpass")
     if hi is None and lo is not None:
         return butter_sos(corners, lo / nyquist, "highpass")
-    raise NotImplementedError("band-pass not restated")
+    return butter_sos(corners, [lo / nyquist, hi / nyquist], "bandpass")
 
 
 def pass_filter(data, axis: int, fs: float, lo, hi, corners: int = 4):

@@ -119,5 +119,39 @@ def main():
     print("golden vectors written to", HERE)
 
 
+def main_next_rows():
+    """band-pass design, decimate(ftype='iir'), and the
+    notebook post-processing (scipy.ndimage.median_filter, demean + scale)."""
+    import scipy.ndimage as nd
+    band = {}
+    for i, (N, W) in enumerate([(4, (0.01, 0.1)), (2, (0.2, 0.4)), (4, (4.5e-4, 0.02))]):
+        z, p, k = ss.iirfilter(N, list(W), btype="bandpass", ftype="butter", output="zpk")
+        band[f"sos_{i}"] = ss.zpk2sos(z, p, k)
+        band[f"case_{i}"] = np.array([N, W[0], W[1]])
+    x = synth.noise_sine(3, 4000, 250.0, seed=21, dc=2.0).astype(np.float64)
+    band["x"] = x
+    band["y_bp0"] = ss.sosfiltfilt(band["sos_0"], x, axis=-1)
+    for q in (2, 5, 10, 50):
+        band[f"cheby_{q}"] = ss.cheby1(8, 0.05, 0.8 / q, output="sos")
+        band[f"dec_{q}"] = ss.decimate(x, q, ftype="iir", axis=-1)
+    np.savez_compressed(os.path.join(HERE, "band_decimate.npz"), **band)
+    rng = np.random.default_rng(77)
+    post = {"x2": rng.standard_normal((40, 23)), "x1": rng.standard_normal(200)}
+    for k in (5, (3, 7), 4, (9, 3), 11):
+        tag = "x".join(str(v) for v in np.atleast_1d(k))
+        post[f"med2_{tag}"] = nd.median_filter(post["x2"], size=k)
+    for k in (9, 5, 4):
+        post[f"med1_{k}"] = nd.median_filter(post["x1"], size=k)
+    d = rng.standard_normal((50, 30)) * 1e-3 + 5.0
+    post["d"] = d
+    post["demean"] = (d - np.mean(d[:, 5:17], axis=1).reshape(-1, 1)) * float((116 * 500.0 / 10.0) / 1e9)
+    np.savez_compressed(os.path.join(HERE, "post.npz"), **post)
+    print("next-row golden vectors written to", HERE)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "next":
+        main_next_rows()
+    else:
+        main()
+        main_next_rows()

@@ -1,0 +1,138 @@
+"""SURVEY §8(f) rows beside the hot path, each to the same bar:
+band-/high-pass ``pass_filter`` through the same device kernels, DASCore
+``decimate(filter_type='iir')`` (restated as scipy.signal.decimate), and the
+notebook post-processing (demean + strain-rate scale, scipy.ndimage
+median_filter) on device.
+
+CPU: the oracle restatements against the SciPy goldens (tests/golden/
+make_golden.py main_next_rows).  GPU: device results against the oracle —
+median filter bit-exact (the output is an input value), demean/scale and
+filters within relRMS 1e-9 / 1e-4 (float64 / float32-sample paths)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T0 = np.datetime64("2023-03-22T03:00:00", "ns")
+
+
+def _g(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.sum((a - b) ** 2) / np.sum(b ** 2)))
+
+
+# ---------------------------------------------------------------- CPU ---
+def test_bandpass_design_matches_golden():
+    g = _g("band_decimate.npz")
+    for i in range(3):
+        N, w0, w1 = g[f"case_{i}"]
+        np.testing.assert_allclose(oracle.butter_sos(int(N), [w0, w1], "bandpass"), g[f"sos_{i}"],
+                                   rtol=0, atol=1e-15)
+    assert _rel(oracle.sosfiltfilt(g["sos_0"], g["x"]), g["y_bp0"]) < 1e-13
+
+
+@pytest.mark.parametrize("q", [2, 5, 10, 50])
+def test_decimate_iir_matches_golden(q):
+    g = _g("band_decimate.npz")
+    np.testing.assert_allclose(oracle.cheby1_sos(8, 0.05, 0.8 / q), g[f"cheby_{q}"], rtol=0, atol=1e-15)
+    assert _rel(oracle.decimate_iir(g["x"], q), g[f"dec_{q}"]) < 1e-13
+
+
+def test_median_and_demean_match_golden():
+    g = _g("post.npz")
+    for k in (5, (3, 7), 4, (9, 3), 11):
+        tag = "x".join(str(v) for v in np.atleast_1d(k))
+        np.testing.assert_array_equal(oracle.median_filter(g["x2"], k), g[f"med2_{tag}"])
+    for k in (9, 5, 4):
+        np.testing.assert_array_equal(oracle.median_filter(g["x1"], k), g[f"med1_{k}"])
+    np.testing.assert_allclose(oracle.demean_scale(g["d"], 5, 17, (116 * 500.0 / 10.0) / 1e9), g["demean"],
+                               rtol=1e-12, atol=0)
+
+
+def test_scale_iDAS():
+    from lfdas.post import scale_iDAS
+    assert scale_iDAS(500.0, 10.0) == float((116 * 500.0 / 10.0) / 1e9)
+
+
+# ---------------------------------------------------------------- GPU ---
+def _patch(x, fs):
+    import lfdas.dc as dc
+    t = T0 + np.arange(x.shape[1]) * np.timedelta64(int(round(1e9 / fs)), "ns")
+    return dc.Patch(data=x, coords={"distance": np.arange(float(x.shape[0])), "time": t},
+                    dims=("distance", "time"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["row", "col"])
+def test_median_filter_device_bit_exact(layout):
+    from lfdas.post import median_filter
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((137, 61))
+    if layout == "col":
+        x = np.asfortranarray(x)
+    for k in (5, (3, 7), 4, (9, 3), 11, 1, (1, 9)):
+        np.testing.assert_array_equal(median_filter(x, k), oracle.median_filter(x, k))
+    tr = rng.standard_normal(300)
+    for k in (9, 5, 4):
+        np.testing.assert_array_equal(median_filter(tr, k), oracle.median_filter(tr, k))
+    # the notebook's 2-D use on a (time, distance) low-passed result (cell 20)
+    big = rng.standard_normal((1400, 96))
+    np.testing.assert_array_equal(median_filter(big, 5), oracle.median_filter(big, 5))
+
+
+@pytest.mark.gpu
+def test_demean_scale_device():
+    from lfdas.post import demean_scale, scale_iDAS
+    g = _g("post.npz")
+    s = scale_iDAS(500.0, 10.0)
+    y = demean_scale(g["d"], 5, 17, s)
+    assert _rel(y, g["demean"]) < 1e-12
+    x = np.random.default_rng(6).standard_normal((3000, 955)) * 1e-6 + 1e-4
+    assert _rel(demean_scale(x, 0, 200, s), oracle.demean_scale(x, 0, 200, s)) < 1e-12
+    with pytest.raises(ValueError):
+        demean_scale(x, 10, 10, s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("band", [(1.0, 10.0), (None, 10.0), (2.0, None), (0.2, 30.0)])
+def test_pass_filter_band_and_high_full_rate(band):
+    fs = 250.0
+    x = np.random.default_rng(8).standard_normal((7, 5000)).astype(np.float32) + 3.0
+    y = _patch(x, fs).pass_filter(time=band).data
+    ref = oracle.sosfiltfilt(oracle.dascore_pass_filter_sos(fs, band[0], band[1]), x)
+    assert y.dtype == np.float64 and _rel(y, ref) < 1e-9
+
+
+@pytest.mark.gpu
+def test_bandpass_interpolate_uses_block_path():
+    fs = 250.0
+    x = np.random.default_rng(9).standard_normal((9, 6000)).astype(np.float32)
+    p = _patch(x, fs)
+    grid = p.coords["time"][::25][1:-2]
+    out = p.pass_filter(time=(0.5, 4.0)).interpolate(time=grid)
+    ref = oracle.sosfiltfilt(oracle.dascore_pass_filter_sos(fs, 0.5, 4.0), x)[:, 25::25][:, :len(grid)]
+    assert _rel(out.data, ref) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [2, 5, 10, 50])
+def test_decimate_iir_device(q):
+    g = _g("band_decimate.npz")
+    x = g["x"]
+    p = _patch(x, 250.0)
+    out = p.decimate(time=q, filter_type="iir")
+    ref = oracle.decimate_iir(x.astype(np.float32).astype(np.float64), q)
+    assert out.data.shape == ref.shape
+    np.testing.assert_array_equal(out.coords["time"], p.coords["time"][::q])
+    assert _rel(out.data, ref) < 1e-4
+    assert _rel(out.data, g[f"dec_{q}"]) < 1e-4  # SciPy on the float64 data
+    with pytest.raises(NotImplementedError):
+        p.decimate(time=q, filter_type="fir")
