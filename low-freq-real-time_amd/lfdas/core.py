@@ -190,6 +190,9 @@ class Patch:
     def data(self):
         """Host (numpy) view of the data; lazy device results materialise here."""
         if self._lazy is not None:
+            if getattr(self._lazy, "transient", False):
+                # file-backed samples of an archive index: read on use, not kept
+                return self._lazy.materialize(self)
             self._data = self._lazy.materialize(self)
             self._lazy = None
         if _is_torch(self._data):

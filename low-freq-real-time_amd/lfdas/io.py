@@ -70,14 +70,73 @@ def read_patch(path: str) -> Patch:
                      attrs=_attrs_from_json(json.loads(str(z["attrs"]))))
 
 
-def read_directory(folder: str):
+class _FileData:
+    """Lazy data of a patch file: the spool index holds coordinates and
+    attributes only; the samples are read when the patch's data is used
+    (out-of-core archives: one file in host memory at a time)."""
+
+    transient = True  # Patch.data reads the file on every use and keeps nothing
+
+    def __init__(self, path: str, shape):
+        self.path = path
+        self.shape = tuple(shape)
+
+    def materialize(self, patch: Patch):
+        with np.load(self.path, allow_pickle=False) as z:
+            return z["data"]
+
+
+def _data_shape(z) -> tuple:
+    """Shape of the ``data`` member from its .npy header (no sample read)."""
+    with z.zip.open("data.npy") as fh:
+        version = np.lib.format.read_magic(fh)
+        shape, _, _ = np.lib.format._read_array_header(fh, version)
+    return tuple(shape)
+
+
+def index_patch(path: str) -> Patch:
+    """Header-only read of a patch file (coordinates, dims, attributes)."""
+    with np.load(path, allow_pickle=False) as z:
+        if "magic" not in z.files or str(z["magic"]) != _MAGIC:
+            raise ValueError(f"{path} is not an lfdas patch file")
+        coords = {}
+        for f in z.files:
+            if f.startswith("coord_ns__"):
+                coords[f[len("coord_ns__"):]] = z[f].astype("datetime64[ns]")
+            elif f.startswith("coord__"):
+                coords[f[len("coord__"):]] = z[f]
+        shape = _data_shape(z)
+        p = Patch(data=None, coords=coords, dims=tuple(str(d) for d in z["dims"]),
+                  attrs=_attrs_from_json(json.loads(str(z["attrs"]))), _lazy=_FileData(path, shape))
+    p.source_path = path
+    return p
+
+
+# header index of a directory, reused by Spool.update(): path -> (mtime, size, patch)
+_INDEX: dict = {}
+
+
+def read_directory(folder: str, lazy: bool = True):
+    """Every patch file of ``folder`` (the ``dc.spool(path).update()`` index).
+    ``lazy``: read headers only and load samples on use; files already indexed
+    and unchanged (mtime, size) are not re-read."""
     out = []
     for name in sorted(os.listdir(folder)):
         p = os.path.join(folder, name)
         if not os.path.isfile(p):
             continue
         try:
-            out.append(read_patch(p))
+            if not lazy:
+                out.append(read_patch(p))
+                continue
+            st = os.stat(p)
+            hit = _INDEX.get(p)
+            if hit is not None and hit[0] == st.st_mtime_ns and hit[1] == st.st_size:
+                out.append(hit[2])
+                continue
+            patch = index_patch(p)
+            _INDEX[p] = (st.st_mtime_ns, st.st_size, patch)
+            out.append(patch)
         except Exception:
             continue
     return out

@@ -126,7 +126,7 @@ class LFProc:
     ``self.outputs`` (and written to the output folder like the reference).
     """
 
-    def __init__(self, sp=None, device=None, verbose=True):
+    def __init__(self, sp=None, device=None, verbose=True, max_resident_bytes=None):
         self._spool = sp
         self._para = self._default_process_parameters()
         self._output_folder = None
@@ -134,6 +134,11 @@ class LFProc:
         self.verbose = verbose
         self.outputs = []
         self.write_files = True
+        # time ranges whose samples exceed this many bytes stream through the
+        # device arena (out-of-core); default: env LFDAS_MAX_RESIDENT_BYTES,
+        # else half of the free HBM
+        self.max_resident_bytes = max_resident_bytes
+        self.last_mode = None
 
     def set_output_folder(self, folder, delete_existing=False):
         """lf_das.py:188-195."""
@@ -183,6 +188,10 @@ class LFProc:
         tg = S.time_grid(bgtime, edtime, dt)
         sched, self._kinds = S.lfproc_chunks(len(tg), patch_size, buff_size, with_kind=True)
         self.outputs = []
+        if self._resident_bytes(tg, sched) > self._budget():
+            self.last_mode = "stream"
+            return self._process_streaming(bgtime, edtime, tg, sched, dt, patch_size, buff_size)
+        self.last_mode = "resident"
 
         # merged, gap-checked data of every chunk (lf_das.py:236-240, 264-266)
         n_ok, merged = self._merged_span(tg, sched)
@@ -192,6 +201,101 @@ class LFProc:
             if self.verbose:
                 print("Processing patch ", str(n_ok + 1))
             raise Exception("patch merge failed! Gap in data exists")
+
+    # -- out-of-core: stream the spool's files through the device arena ----
+    def _budget(self) -> int:
+        if self.max_resident_bytes is not None:
+            return int(self.max_resident_bytes)
+        env = os.environ.get("LFDAS_MAX_RESIDENT_BYTES")
+        if env:
+            return int(float(env))
+        import torch
+        if not torch.cuda.is_available():
+            return 1 << 62
+        free, _ = torch.cuda.mem_get_info(self._device)
+        return free // 2
+
+    def _span_patches(self, tg, sched):
+        t_lo = np.datetime64(int(tg[sched[0][0]]), "ns")
+        t_hi = np.datetime64(int(tg[max(b for _, b, _, _ in sched)]), "ns")
+        pats = [p for p in self._spool
+                if not (p.coords["time"][-1] < t_lo or p.coords["time"][0] > t_hi)]
+        return sorted(pats, key=lambda p: p.coords["time"][0]), t_lo, t_hi
+
+    def _resident_bytes(self, tg, sched) -> int:
+        pats, t_lo, t_hi = self._span_patches(tg, sched)
+        if not pats:
+            return 0
+        p = pats[0]
+        n_ch = int(np.prod([n for d, n in zip(p.dims, p.shape) if d != "time"]))
+        n_t = int((t_hi - t_lo).astype("timedelta64[ns]").astype(np.int64) // p.sampling_interval_ns()) + 1
+        return 4 * n_ch * n_t
+
+    def _process_streaming(self, bgtime, edtime, tg, sched, dt, patch_size, buff_size):
+        """The same chunks as the resident path, produced by a continuous
+        ``LowpassStream`` (lfd_stream_*): files are loaded one at a time,
+        pushed to HBM, and each chunk runs as soon as its selection has
+        arrived; its output file is written then (lp_process, lf_das.py:221-232)."""
+        from .stream import LowpassStream
+        pats, t_lo, t_hi = self._span_patches(tg, sched)
+        if not pats:
+            raise IndexError("list index out of range")  # _check_merge(plist) on an empty spool
+        p0 = pats[0]
+        tdim = p0.dims.index("time")
+        dt_ns = p0.sampling_interval_ns()
+        n_ch = p0.shape[1 - tdim]
+        st = LowpassStream(n_ch, dt_ns, dt, patch_size, buff_size, mode="continuous",
+                           t_start=S.to_ns(bgtime), t_end=S.to_ns(edtime), device=self._device)
+        coords0 = dict(p0.coords.coord_map)
+        attrs0 = p0._attrs_wo_coords()
+        done = 0
+
+        def emit(o):
+            nonlocal done
+            if o.n_out == 0 and not o.chunk_counts:
+                return
+            y = st.fetch() if o.n_out else np.zeros((n_ch, 0), np.float32)
+            t = o.times_ns
+            j = 0
+            for cnt in o.chunk_counts:
+                done += 1
+                if self.verbose:
+                    if self._kinds[done - 1] == "tail":
+                        print(f"Processing patch {done} (Last portion of data)")
+                    else:
+                        print("Processing patch ", str(done))
+                seg = y[:, j:j + cnt].astype(np.float64)
+                coords = dict(coords0)
+                coords["time"] = t[j:j + cnt].astype("datetime64[ns]")
+                out = Patch(data=seg.T.copy() if tdim == 0 else seg, coords=coords, dims=p0.dims,
+                            attrs=attrs0).update_attrs(d_time=dt)
+                self.outputs.append(out)
+                if self.write_files:
+                    fn = _get_filename(out.attrs["time_min"], out.attrs["time_max"])
+                    out.io.write(self._output_folder + "/" + fn, "dasdae")
+                j += cnt
+
+        expected = None
+        try:
+            for p in pats:
+                sel = p.select(time=(t_lo, t_hi))
+                t_ns = sel.sample_times_ns()
+                if expected is not None and len(t_ns) and t_ns[0] < expected:
+                    sel = sel.select(time=(np.datetime64(int(expected), "ns"), None))  # duplicated boundary
+                    t_ns = sel.sample_times_ns()
+                if not len(t_ns):
+                    continue
+                data = np.asarray(sel.data, dtype=np.float32)
+                try:
+                    emit(st.push(data, int(t_ns[0]), time_axis=tdim))
+                except ValueError as e:
+                    if "Gap in data" in str(e):
+                        raise Exception("patch merge failed! Gap in data exists") from None
+                    raise
+                expected = int(t_ns[-1]) + dt_ns
+            emit(st.flush())
+        finally:
+            st.close()
 
     def _merged_span(self, tg, sched):
         """Largest chunk prefix whose selections are each gap-free; returns
