@@ -664,7 +664,7 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   p->bg.n_sf = p->sf_blocks;
   // run mode: 4th-order cascade, MFMA taps, LDS for taps + 16 run buffers
   if (n_sec == 2 && !p->taps.empty() &&
-      sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 16 * lfd::RUN_R * 5 * 16) <=
+      sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 8 * lfd::RUN_R * 5 * 16) <=
           (size_t)lfd::TAP_LDS_MAX) {
     std::vector<int64_t> cuts = {0, p->bg.nb};
     for (const auto &G : p->chunks) {
@@ -682,8 +682,10 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     const int64_t n_runs = (int64_t)p->run_ks.size();
     // K1 units: consecutive runs up to 32 blocks (fewer for narrow arrays, so
     // that >= ~4,096 wave units cover the chip)
+    int64_t unit_cap = 32;
+    if (const char *v = std::getenv("LFD_RUN_UNIT")) unit_cap = std::max(lfd::RUN_R, std::atoi(v));
     const int64_t unit_blocks =
-        std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(32, ((n_ch + 15) / 16) * p->bg.nb / 4096));
+        std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(unit_cap, ((n_ch + 15) / 16) * p->bg.nb / 4096));
     int acc = 0;
     for (int64_t r = 0; r < n_runs; ++r) {
       if (r == 0 || acc + p->run_len[r] > unit_blocks) {

@@ -874,15 +874,19 @@ __device__ __forceinline__ f4v mf_load_guarded(const float *__restrict__ xr, int
   return v;
 }
 
-// 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur
+// 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur.
+// Lanes of A rows c >= nc read a copy of row nc-1 instead of zeros: MFMA rows
+// are independent (D[c][:] depends on A[c][:] only) and rows >= nc of D are
+// never read, so no per-MFMA select is needed.
 __device__ __forceinline__ void mf_iter(const double *kt, int kstride, bool colv,
                                         const f4v (&cur)[4], d4v &acc0, d4v &acc1) {
+  (void)colv;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const double2 b01 = *reinterpret_cast<const double2 *>(kt + j * kstride);
     const double2 b23 = *reinterpret_cast<const double2 *>(kt + j * kstride + 2);
-    const double a0 = colv ? b01.x : 0.0, a1 = colv ? b01.y : 0.0;
-    const double a2 = colv ? b23.x : 0.0, a3 = colv ? b23.y : 0.0;
+    const double a0 = b01.x, a1 = b01.y;
+    const double a2 = b23.x, a3 = b23.y;
     acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, (double)cur[j].x, acc0, 0, 0, 0);
     acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, (double)cur[j].y, acc1, 0, 0, 0);
     acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, (double)cur[j].z, acc0, 0, 0, 0);
@@ -1055,8 +1059,11 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
 constexpr int RUN_WB = RUN_R * 5 * 16;  // doubles per wave run buffer
 constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 
-template <int PF>
-__global__ __launch_bounds__(1024) void k_block_runs_mfma(
+// MODE 0: production.  Diagnostics (timing only, results invalid;
+// LFD_RUN_MODE): 1 = VALU sum instead of the MFMAs, 4 = MFMAs but the run
+// epilogue reduced to one store per block.
+template <int PF, int MODE = 0, int NT = 1024>
+__global__ __launch_bounds__(NT) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
     double *__restrict__ AG) {
@@ -1088,7 +1095,15 @@ __global__ __launch_bounds__(1024) void k_block_runs_mfma(
   const int64_t s0 = g.base - tg.J;
   const int L = g.L;
   auto table = [&](int64_t s) { return tg.nvar == 1 ? kl : kl + (int)(s & 3) * tab; };
+#ifdef LFD_RUN_CONST_SMEM
+  // epilogue constants straight from global memory: uniform addresses, so
+  // they are scalar loads into SGPRs (operands of the fp64 FMAs) instead of
+  // LDS reads into VGPRs
+  const double *__restrict__ rcg = &rg.rc->PhiF[0];
+  const double *PhiF = rcg, *Mm = rcg + 16, *PhiR = rcg + 32, *G0 = rcg + 48, *H0 = rcg + 52;
+#else
   const double *PhiF = cst, *Mm = cst + 16, *PhiR = cst + 32, *G0 = cst + 48, *H0 = cst + 52;
+#endif
 
   int64_t rks = k0;
   int rlen = __builtin_amdgcn_readfirstlane(rg.run_len[r]);
@@ -1197,9 +1212,20 @@ __global__ __launch_bounds__(1024) void k_block_runs_mfma(
 #pragma unroll
         for (int j = 0; j < 4; ++j) buf[lb][j] = ldx4(pp + 16 * j);
         produce();
-        mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+        if (MODE == 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
+        } else {
+          mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+        }
         if (++it == nit) {
-          block_done(acc0, acc1, k);
+          if (MODE == 4) {
+            const d4v a = acc0 + acc1;
+            Y0[(cg * g.nb + k) * 16 + col] = a[q & 3];
+          } else {
+            block_done(acc0, acc1, k);
+          }
           acc0 = d4v{0.0, 0.0, 0.0, 0.0};
           acc1 = d4v{0.0, 0.0, 0.0, 0.0};
           it = 0;
@@ -1314,22 +1340,42 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   return hipGetLastError();
 }
 
-hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
-                                  const double *taps, const TapGeom &tg, const RunGeom &rg,
-                                  double *Y0, double *AG, hipStream_t st) {
-  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
-  const size_t lds = sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + 16 * RUN_WB);
+template <int PF, int MODE, int NT>
+hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
+                  const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
+  constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
+  const size_t lds = sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + W * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<1>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
-  k_block_runs_mfma<1><<<nblk(units, 16), 1024, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
+  k_block_runs_mfma<PF, MODE, NT><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
   return hipGetLastError();
+}
+
+hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+                                  const double *taps, const TapGeom &tg, const RunGeom &rg,
+                                  double *Y0, double *AG, hipStream_t st) {
+  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
+  const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
+  // 512-thread workgroups (2 per CU: 16 waves, 2 x 77 KB LDS at cfg3) retire
+  // independently, unlike one 1024-thread group per CU: 12.3-12.7 ms vs
+  // 12.65-13.0 on cfg3 (A/B, tools/ab_env.sh)
+  int mode = 0, pf = 1, nt = 512;
+  if (const char *v = std::getenv("LFD_RUN_MODE")) mode = std::atoi(v);
+  if (const char *v = std::getenv("LFD_RUN_PF")) pf = std::atoi(v);
+  if (const char *v = std::getenv("LFD_RUN_NT")) nt = std::atoi(v);
+  if (mode == 1) return run_k1<1, 1, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (mode == 4) return run_k1<1, 4, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 2 && nt == 768) return run_k1<2, 0, 768>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 2 && nt == 384) return run_k1<2, 0, 384>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 2 && nt == 512) return run_k1<2, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 1 && nt == 1024) return run_k1<1, 0, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  return run_k1<1, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 }
 
 hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
