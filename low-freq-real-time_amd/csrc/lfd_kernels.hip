@@ -905,6 +905,9 @@ __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, doubl
     if (q + 4 * r < nc) Fo[(q + 4 * r) * F_CSTRIDE] = acc[r];
 }
 
+// (non-temporal loads of the sample stream were measured 40 % slower on cfg3:
+// 18.5 vs 13.1 ms — the 64-B row pieces of consecutive iterations no longer
+// meet in L2)
 __device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
 
 // wave-uniform 64-bit value into SGPRs (VALU-computed values, e.g. 64-bit
@@ -1080,11 +1083,24 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
   const int64_t n_cg = (g.n_ch + 15) / 16;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_cg * rg.n_groups) return;
+  // channel-group-major unit order (time-major measured 2 % slower on cfg3)
   const int64_t cg = unit % n_cg, grp = unit / n_cg;
   int r = __builtin_amdgcn_readfirstlane(rg.group_r0[grp]);
   const int r_end = __builtin_amdgcn_readfirstlane(rg.group_r0[grp + 1]);
-  const int64_t k0 = uniform64(rg.run_ks[r]);
-  const int64_t k1 = uniform64(rg.run_ks[r_end - 1] + rg.run_len[r_end - 1]);
+  // the unit's run table (<= 32 runs) is held one run per lane and read with
+  // v_readlane at run ends: a vector load there would wait (vmcnt(0)) for
+  // every sample load in flight
+  const int ru0 = r;
+  const int my_len = lane < r_end - ru0 ? rg.run_len[ru0 + lane] : 0;
+  const int64_t my_ks = lane < r_end - ru0 ? rg.run_ks[ru0 + lane] : 0;
+  auto run_len_of = [&](int rr) { return __builtin_amdgcn_readlane(my_len, rr - ru0); };
+  auto run_ks_of = [&](int rr) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_ks, rr - ru0);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)my_ks >> 32), rr - ru0);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  const int64_t k0 = run_ks_of(r);
+  const int64_t k1 = run_ks_of(r_end - 1) + run_len_of(r_end - 1);
   const int col = lane & 15, q = lane >> 4;
   const int64_t ch = cg * 16 + col;  // stores land in the 16-channel padding past n_ch
   const float *xr = x + (ch < g.n_ch ? ch : g.n_ch - 1) * s_ch;
@@ -1095,18 +1111,10 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
   const int64_t s0 = g.base - tg.J;
   const int L = g.L;
   auto table = [&](int64_t s) { return tg.nvar == 1 ? kl : kl + (int)(s & 3) * tab; };
-#ifdef LFD_RUN_CONST_SMEM
-  // epilogue constants straight from global memory: uniform addresses, so
-  // they are scalar loads into SGPRs (operands of the fp64 FMAs) instead of
-  // LDS reads into VGPRs
-  const double *__restrict__ rcg = &rg.rc->PhiF[0];
-  const double *PhiF = rcg, *Mm = rcg + 16, *PhiR = rcg + 32, *G0 = rcg + 48, *H0 = rcg + 52;
-#else
   const double *PhiF = cst, *Mm = cst + 16, *PhiR = cst + 32, *G0 = cst + 48, *H0 = cst + 52;
-#endif
 
   int64_t rks = k0;
-  int rlen = __builtin_amdgcn_readfirstlane(rg.run_len[r]);
+  int rlen = run_len_of(r);
   double S0 = 0.0;  // run prefix state, component q of channel col
   auto block_done = [&](const d4v &acc0, const d4v &acc1, int64_t k) {
     const d4v a = acc0 + acc1;  // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
@@ -1151,8 +1159,8 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
       S0 = 0.0;
       ++r;
       if (r < r_end) {
-        rks = uniform64(rg.run_ks[r]);
-        rlen = __builtin_amdgcn_readfirstlane(rg.run_len[r]);
+        rks = run_ks_of(r);
+        rlen = run_len_of(r);
       }
     }
   };
