@@ -356,6 +356,29 @@ def main():
         pass
 
     secondary = {}
+    if ws > 1:
+        # the path's one collective, outside the timed step: RCCL all-gather of
+        # the decimated outputs (lfdas.shard.all_gather_channels), every rank
+        # ends with all n_ch * ws channels
+        from lfdas.shard import all_gather_channels
+        try:
+            g_ms = []
+            for i in range(4):
+                barrier()
+                t_g = time.perf_counter()
+                full = all_gather_channels(y, n_ch * ws)
+                torch.cuda.synchronize(dev)
+                if i:
+                    g_ms.append((time.perf_counter() - t_g) * 1e3)
+            del full
+            tt = torch.tensor([float(np.median(g_ms))], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            secondary["allgather_outputs"] = {
+                "ms": float(tt.item()), "bytes_per_rank": int(y.numel() * 4),
+                "frac_of_step": float(tt.item()) / (el / args.steps * 1e3),
+                "note": "RCCL all_gather of every rank's (n_ch, n_grid) float32 outputs; not in the timed step"}
+        except Exception as e:  # the optional gather never voids the bench line
+            secondary["allgather_outputs"] = {"error": repr(e)}
     if ws == 1:
         del x, y, wsb
         plan.close()
