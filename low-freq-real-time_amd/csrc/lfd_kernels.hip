@@ -778,6 +778,36 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // time-contiguous: one wave per output window, float4 loads on the aligned
 // interior of the window, fp64 accumulation, grid-stride over windows.
+// lane's share of sum(x[a:b]) (float64), float4 loads on the 16-B aligned
+// interior with up to 4 independent 1-KB wave loads in flight per step
+__device__ __forceinline__ double window_part(const float *__restrict__ x, int64_t a, int64_t b, int lane,
+                                              bool vec) {
+  double acc = 0.0;
+  const int64_t a4 = (a + 3) & ~(int64_t)3;
+  const int64_t b4 = b & ~(int64_t)3;
+  if (!vec || a4 >= b4) {
+    for (int64_t i = a + lane; i < b; i += 64) acc += (double)x[i];
+    return acc;
+  }
+  if (lane < a4 - a) acc += (double)x[a + lane];
+  if (lane < b - b4) acc += (double)x[b4 + lane];
+  const float4 *p4 = reinterpret_cast<const float4 *>(x + a4);
+  const int64_t n4 = (b4 - a4) >> 2;
+  for (int64_t q0 = lane; q0 < n4; q0 += 256) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = q0 + 64 * u;
+      v[u] = q < n4 ? p4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += ((double)v[u].x + (double)v[u].y) + ((double)v[u].z + (double)v[u].w);
+  }
+  return acc;
+}
+
+// One wave per output window (grid-stride).  Two windows per step: their
+// loads are issued together (8 KB per wave in flight at W = 1000).
 __global__ __launch_bounds__(256) void k_rolling_tc(
     const float *__restrict__ x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     int64_t W, int64_t S, float *__restrict__ y, int64_t ys_ch, int64_t ys_t,
@@ -788,33 +818,30 @@ __global__ __launch_bounds__(256) void k_rolling_tc(
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const float nanv = __builtin_nanf("");
-  for (int64_t wi = wave0; wi < n_win; wi += n_waves) {
-    const int64_t ch = wi / n_out, k = wi % n_out;
-    const int64_t e = k * S;  // inclusive window end
-    float *out = y + ch * ys_ch + k * ys_t;
-    if (e < W - 1) {
-      if (lane == 0) *out = nanv;
-      continue;
-    }
-    const int64_t a = ch * s_ch + e - W + 1;  // absolute element index
-    const int64_t b = a + W;                  // exclusive
-    int64_t a4 = (a + 3) & ~(int64_t)3;
-    int64_t b4 = b & ~(int64_t)3;
-    double acc = 0.0;
-    if (!vec || a4 >= b4) {
-      for (int64_t i = a + lane; i < b; i += 64) acc += (double)x[i];
-    } else {
-      if (lane < a4 - a) acc += (double)x[a + lane];
-      if (lane < b - b4) acc += (double)x[b4 + lane];
-      const float4 *p4 = reinterpret_cast<const float4 *>(x + a4);
-      const int64_t n4 = (b4 - a4) >> 2;
-      for (int64_t q = lane; q < n4; q += 64) {
-        const float4 v = p4[q];
-        acc += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+  for (int64_t w0 = wave0; w0 < n_win; w0 += 2 * n_waves) {
+    double acc[2] = {0.0, 0.0};
+    float *out[2] = {nullptr, nullptr};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t wi = w0 + h * n_waves;
+      if (wi >= n_win) continue;
+      const int64_t ch = wi / n_out, k = wi % n_out;
+      const int64_t e = k * S;  // inclusive window end
+      out[h] = y + ch * ys_ch + k * ys_t;
+      if (e < W - 1) {
+        if (lane == 0) *out[h] = nanv;
+        out[h] = nullptr;
+        continue;
       }
+      const int64_t a = ch * s_ch + e - W + 1;  // absolute element index
+      acc[h] = window_part(x, a, a + W, lane, vec);
     }
-    acc = wave_sum(acc);
-    if (lane == 0) *out = (float)(acc / (double)W);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!out[h]) continue;
+      const double t = wave_sum(acc[h]);
+      if (lane == 0) *out[h] = (float)(t / (double)W);
+    }
   }
 }
 
