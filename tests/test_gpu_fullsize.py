@@ -1,0 +1,148 @@
+"""Parity at BASELINE.json's full sizes.  The oracle cannot process 72 GB in
+seconds, so every check here is size-independent: a sample of channels of the
+full-size device result against the oracle (relRMS <= 1e-4, identical output
+times), and closed-form properties over every channel (a constant input comes
+back exactly; linearity of the filter across two inputs)."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_505_692_800_000_000_000
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.sqrt(np.sum((a - b) ** 2) / np.sum(b ** 2)))
+
+
+def _cfg3_plan(n_ch=10_000, n=1_800_000, fs=500.0, dt_out=1.0, P=600, B=7):
+    import bench
+    plan, sched, sos, t0, dt_ns, tg = bench.build_plan(n_ch, n, fs, dt_out, P, B)
+    return plan, sched, dt_ns, tg
+
+
+def test_cfg3_full_size_sampled_channels_and_dc():
+    import torch
+
+    import bench
+    n_ch, n = 10_000, 1_800_000
+    plan, sched, dt_ns, tg = _cfg3_plan(n_ch, n)
+    x = torch.empty((n_ch, n), dtype=torch.float32, device="cuda")
+    bench.synth_fill(x, 500.0, 2024)
+    y = torch.full((n_ch, plan.n_grid), float("nan"), dtype=torch.float32, device="cuda")
+    ws = plan.alloc_workspace()
+    plan.execute(x, y, ws)
+    torch.cuda.synchronize()
+    assert plan.last_kernel() == "mfma_runs"
+    rows = [0, 1, 15, 16, 4999, 9983, 9998, 9999]
+    xs = x[rows].cpu().numpy()
+    ys = y[rows].cpu().numpy()
+    ref = oracle.lfproc_process(xs, T0, dt_ns, tg[0], tg[-1] + 1, 1.0, 600, 7)
+    got = np.concatenate([ys[:, oa:ob] for _, _, oa, ob in sched], axis=1)
+    want = np.concatenate([r for _, r in ref], axis=1)
+    assert got.shape == want.shape == (len(rows), 3585)
+    assert _rel(got, want) < 1e-4
+    produced = np.zeros(plan.n_grid, bool)
+    for _, _, oa, ob in sched:
+        produced[oa:ob] = True
+    assert not torch.isnan(y[:, torch.as_tensor(produced, device="cuda")]).any()
+    # every channel: a constant comes back as itself (DC gain 1, odd padding
+    # of a constant is the constant, zi starts it steady)
+    x.fill_(0.0)
+    x += torch.arange(n_ch, device="cuda", dtype=torch.float32)[:, None] * 0.5 + 100.0
+    plan.execute(x, y, ws)
+    torch.cuda.synchronize()
+    yc = y[:, torch.as_tensor(produced, device="cuda")]
+    expect = (torch.arange(n_ch, device="cuda", dtype=torch.float32) * 0.5 + 100.0)[:, None]
+    assert float(((yc - expect).abs() / expect).max()) < 1e-6
+    del x, y, ws
+    torch.cuda.empty_cache()
+
+
+def test_cfg3_full_size_linearity():
+    """f(x1 + 3 x2) == f(x1) + 3 f(x2) over all 10,000 channels."""
+    import torch
+
+    import bench
+    n_ch, n = 10_000, 1_800_000
+    plan, sched, dt_ns, tg = _cfg3_plan(n_ch, n)
+    ws = plan.alloc_workspace()
+    x = torch.empty((n_ch, n), dtype=torch.float32, device="cuda")
+    outs = []
+    for seed in (1, 2):
+        bench.synth_fill(x, 500.0, seed)
+        y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device="cuda")
+        plan.execute(x, y, ws)
+        outs.append(y)
+    # x1 + 3 x2 regenerated in place (the generator is seeded)
+    bench.synth_fill(x, 500.0, 2)
+    x *= 3.0
+    g = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device="cuda")
+    # add x1 slice by slice to keep memory at 2 x 72 GB
+    x_full1 = torch.empty((n_ch, n), dtype=torch.float32, device="cuda")
+    bench.synth_fill(x_full1, 500.0, 1)
+    x += x_full1
+    del x_full1
+    plan.execute(x, g, ws)
+    torch.cuda.synchronize()
+    lhs = g[:, sched[0][2]:sched[-1][3]].double()
+    rhs = (outs[0] + 3.0 * outs[1])[:, sched[0][2]:sched[-1][3]].double()
+    rel = float(torch.sqrt(((lhs - rhs) ** 2).sum() / (rhs ** 2).sum()))
+    assert rel < 1e-6, rel
+    del x, g, outs, ws
+    torch.cuda.empty_cache()
+
+
+def test_cfg2_rolling_full_size_sampled_channels():
+    import torch
+
+    import bench
+    from lfdas.plan import rolling_mean_device
+    x = torch.empty((5000, 600_000), dtype=torch.float32, device="cuda")
+    bench.synth_fill(x, 1000.0, 99)
+    y = rolling_mean_device(x, 1000, 1000)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (5000, 600)
+    rows = [0, 17, 2500, 4999]
+    ref = oracle.rolling_mean(x[rows].cpu().numpy(), 1000, 1000)
+    got = y[rows].cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    m = ~np.isnan(ref)
+    assert _rel(got[m], ref[m]) < 1e-6
+    assert bool(torch.isnan(y[:, 0]).all()) and not bool(torch.isnan(y[:, 1:]).any())
+    del x, y
+    torch.cuda.empty_cache()
+
+
+def test_cfg4_edge_full_width_sampled_channels():
+    """cfg4 (2,000 ch @ 2 kHz, 30 s pushes) through the edge stream, a sample
+    of channels against the oracle's notebook loop."""
+    import torch
+
+    from lfdas.stream import LowpassStream
+    n_ch, fs, push = 2000, 2000.0, 60_000
+    dt_ns = 500_000
+    n_push = 4
+    rng = np.random.default_rng(4)
+    rows = [0, 777, 1999]
+    st = LowpassStream(n_ch, dt_ns, 1.0, 125, 7, mode="edge", t_start=T0)
+    st.reserve(push)
+    xs = np.empty((len(rows), push * n_push), np.float32)
+    got = []
+    for k in range(n_push):
+        blk = torch.empty((n_ch, push), dtype=torch.float32).pin_memory()
+        blk.copy_(torch.from_numpy((rng.standard_normal((n_ch, push)) + 2.0).astype(np.float32)))
+        xs[:, k * push:(k + 1) * push] = blk[rows].numpy()
+        st.push(blk, T0 + k * push * dt_ns)
+        got.append(st.fetch()[rows])
+    st.close()
+    ref = oracle.edge_loop(xs, T0, dt_ns, push, T0, 1.0, 125, 7, 6_000_000_000)
+    for g, r in zip(got, ref):
+        want = np.concatenate([d for _, d in r], axis=1) if r else np.zeros((len(rows), 0))
+        assert g.shape == want.shape
+        if want.size:
+            assert _rel(g, want) < 1e-4
