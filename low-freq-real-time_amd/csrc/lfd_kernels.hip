@@ -1379,7 +1379,9 @@ template <int PF, int MODE, int NT>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
-  const size_t lds = sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + W * RUN_WB);
+  // (MODE 4 diagnostic: no run buffers needed)
+  const size_t lds =
+      sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
@@ -1405,6 +1407,8 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   if (const char *v = std::getenv("LFD_RUN_PF")) pf = std::atoi(v);
   if (const char *v = std::getenv("LFD_RUN_NT")) nt = std::atoi(v);
   if (mode == 1) return run_k1<1, 1, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (mode == 4 && nt == 320) return run_k1<1, 4, 320>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (mode == 4 && nt == 512) return run_k1<1, 4, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (mode == 4) return run_k1<1, 4, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 2 && nt == 768) return run_k1<2, 0, 768>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 2 && nt == 384) return run_k1<2, 0, 384>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
