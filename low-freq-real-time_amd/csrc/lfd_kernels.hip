@@ -452,6 +452,17 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 
 // RUNS: the scans walk runs (lfd_internal.h RunConst) over K1's y0 / run
 // aggregates instead of blocks over F (requires NS == 2).
+#ifndef SCAN_DF
+#define SCAN_DF 4  // runs in flight in the forward scan
+#endif
+#ifndef SCAN_DB
+#define SCAN_DB 2  // runs in flight in the backward scan
+#endif
+// LFD_SCAN_DIAG (timing experiments only, results invalid): bit 1 skips the
+// left pad/head, 2 the forward run scan, 4 the right pad and its reverse,
+// 8 the backward run scan.
+__constant__ int g_scan_diag = 0;
+
 template <int NS, bool RUNS>
 __global__ __launch_bounds__(256) void k_chunk_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
@@ -467,12 +478,21 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // run mode: the run-algebra constants live in LDS (read every run step;
   // from global they put two dependent load latencies on each step)
   __shared__ RunConst rcs[1];
+  // run-mode output staging: a wave's 64 channels x one run's <= 8 outputs,
+  // written back as 8 rows x 8 consecutive samples per store instruction
+  // instead of 64 scattered 4-B stores (0.2 ms of the cfg3 scan)
+  __shared__ float outs[RUNS ? 4 : 1][64][RUN_R + 1];
   if constexpr (RUNS) {
     const double *src = &rg.rc->PhiFp[0][0];
     double *dst = &rcs[0].PhiFp[0][0];
     for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
     __syncthreads();
   }
+  // whole wave active and inside one chunk: outputs leave through LDS (above)
+  const int lane = threadIdx.x & 63;
+  const int64_t tid_w = tid - lane;
+  const bool coal = RUNS && tid_w + 63 < n_thr && tid_w / g.n_ch == (tid_w + 63) / g.n_ch;
+  const int64_t ch_w = tid_w % g.n_ch;
   if (tid >= n_thr) return;
   const int64_t ch = tid % g.n_ch;
   const int64_t c = tid / g.n_ch;
@@ -490,9 +510,9 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     R.steady(S, e0, true);
 #pragma unroll
     for (int j = 0; j < J; ++j) h[j] = e0;
-    for (int i = 0; i < E; ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
+    for (int i = 0; i < E && !(g_scan_diag & 1); ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
   }
-  for (int64_t t = G.s0; t < G.head_end; ++t) R.fwd(S, h, (double)xc[t * s_t]);
+  for (int64_t t = G.s0; t < G.head_end && !(g_scan_diag & 1); ++t) R.fwd(S, h, (double)xc[t * s_t]);
 
   // ---- FIR-history correction of block kb: K1 used the raw samples before
   // head_end (0 before the channel start); this chunk saw pad / head values.
@@ -527,39 +547,48 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   if constexpr (RUNS) {
     static_assert(N == RUN_N, "run mode is 4th order");
     const RunConst &rc = rcs[0];
-    // software-pipelined: run r+1's aggregates and length load while run r
-    // is applied
+    // software-pipelined through a ring of SCAN_DF runs: the aggregates and
+    // lengths of runs r+1 .. r+SCAN_DF are in flight while run r is applied
+    // (the step is ~150 cycles, a load ~1.5 us)
+    constexpr int DF = SCAN_DF;
     const double *agb = F + (((ch >> 4) * rg.n_runs) * 8) * 16 + (ch & 15);
-    double agn[N];
-    int lenn = 0;
-    if (G.r0 < G.r1) {
-      lenn = rg.run_len[G.r0];
+    double agq[DF][N];
+    int lenq[DF];
 #pragma unroll
-      for (int i = 0; i < N; ++i) agn[i] = agb[(G.r0 * 8 + i) * 16];
+    for (int u = 0; u < DF; ++u) {
+      const int64_t r = G.r0 + u;
+      lenq[u] = r < G.r1 ? rg.run_len[r] : 0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) agq[u][i] = r < G.r1 ? agb[(r * 8 + i) * 16] : 0.0;
     }
-    for (int64_t r = G.r0; r < G.r1; ++r) {
-      double agc[N];
+    for (int64_t rb = G.r0; rb < G.r1 && !(g_scan_diag & 2); rb += DF) {
 #pragma unroll
-      for (int i = 0; i < N; ++i) agc[i] = agn[i];
-      const int len = lenn;
-      if (r + 1 < G.r1) {
-        lenn = rg.run_len[r + 1];
+      for (int u = 0; u < DF; ++u) {
+        const int64_t r = rb + u;
+        if (r >= G.r1) break;
+        double agc[N];
 #pragma unroll
-        for (int i = 0; i < N; ++i) agn[i] = agb[((r + 1) * 8 + i) * 16];
+        for (int i = 0; i < N; ++i) agc[i] = agq[u][i];
+        const int len = lenq[u];
+        if (r + DF < G.r1) {
+          lenq[u] = rg.run_len[r + DF];
+#pragma unroll
+          for (int i = 0; i < N; ++i) agq[u][i] = agb[((r + DF) * 8 + i) * 16];
+        }
+        double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
+        const double *P = rc.PhiFp[len];
+        double ns[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          sr[i * SF_ISTRIDE] = S[i];
+          double acc = agc[i] + (r == G.r0 ? corr[i] : 0.0);
+#pragma unroll
+          for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
+          ns[i] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) S[i] = ns[i];
       }
-      double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
-      const double *P = rc.PhiFp[len];
-      double ns[N];
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        sr[i * SF_ISTRIDE] = S[i];
-        double acc = agc[i] + (r == G.r0 ? corr[i] : 0.0);
-#pragma unroll
-        for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
-        ns[i] = acc;
-      }
-#pragma unroll
-      for (int i = 0; i < N; ++i) S[i] = ns[i];
     }
   }
   for (int64_t k = G.kb; !RUNS && k < G.ke; ++k) {
@@ -587,12 +616,12 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   double *tp = TP + tid;
   int64_t ntp = 0;
   double ylast = 0.0;
-  for (int64_t t = G.tail_begin; t <= G.s1; ++t) {
+  for (int64_t t = G.tail_begin; t <= G.s1 && !(g_scan_diag & 4); ++t) {
     ylast = R.fwd(S, h, (double)xc[t * s_t]);
     tp[(ntp++) * n_thr] = ylast;
   }
   const float xr = xc[G.s1 * s_t];
-  for (int i = 0; i < E; ++i) {
+  for (int i = 0; i < E && !(g_scan_diag & 4); ++i) {
     ylast = R.fwd(S, h, (double)(2.0f * xr - xc[(G.s1 - 1 - i) * s_t]));
     tp[(ntp++) * n_thr] = ylast;
   }
@@ -641,16 +670,27 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
       for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = pp < o.len ? y0b[(o.ks + pp) * 16] : 0.0;
     };
-    RunIn cur, nxt;
-    if (G.r0 < G.r1) load_run(G.r1 - 1, cur);
-    for (int64_t r = G.r1 - 1; r >= G.r0; --r) {
-      if (r - 1 >= G.r0) load_run(r - 1, nxt);
+    // ring of SCAN_DB runs (r-1 .. r-SCAN_DB in flight while run r is applied)
+    constexpr int DB = SCAN_DB;
+    RunIn q[DB];
+#pragma unroll
+    for (int u = 0; u < DB; ++u)
+      if (G.r1 - 1 - u >= G.r0) load_run(G.r1 - 1 - u, q[u]);
+    for (int64_t rb = G.r1 - 1; rb >= G.r0 && !(g_scan_diag & 8); rb -= DB)
+#pragma unroll
+    for (int u = 0; u < DB; ++u) {
+      const int64_t r = rb - u;
+      if (r < G.r0) break;
+      const RunIn cur = q[u];
+      if (r - DB >= G.r0) load_run(r - DB, q[u]);
       const int len = cur.len;
       const int64_t ks = cur.ks;
       const double *sin = cur.sin;
+      float ov[RUN_R];
 #pragma unroll
       for (int pp = 0; pp < RUN_R; ++pp) {
         const int64_t k = ks + pp;
+        ov[pp] = 0.f;
         if (pp >= len || k < G.kout0 || k >= G.kout1) continue;
         double acc = cur.y0[pp] + (k == G.kb ? corr[2 * N] : 0.0);
         const double *A = rc.A[len][pp];
@@ -660,7 +700,29 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
           acc = fma(A[j], sin[j], acc);
           acc = fma(B[j], T[j], acc);
         }
-        y[ch * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t] = (float)acc;
+        ov[pp] = (float)acc;
+        if (!coal) y[ch * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t] = ov[pp];
+      }
+      if (coal) {
+        float(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
+#pragma unroll
+        for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int e = lane & 7;
+        const int64_t k = ks + e;
+        const bool ok = e < len && k >= G.kout0 && k < G.kout1;
+        float *yb = y + ch_w * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const int row = m * 8 + (lane >> 3);
+          const float v = wl[row][e];
+          if (ok) yb[row * ys_ch] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
       const double *PR = rc.PhiRp[len], *CC = rc.C[len];
       double nr[N];
@@ -676,7 +738,6 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) T[i] = nr[i];
-      cur = nxt;
     }
     return;
   }
@@ -1423,6 +1484,12 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
                                   float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
   const unsigned nb = nblk(n_chunks * g.n_ch, 256);
+  static int diag = -1;
+  if (diag < 0) {
+    const char *v = std::getenv("LFD_SCAN_DIAG");
+    diag = v ? std::atoi(v) : 0;
+    if (diag) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_scan_diag), &diag, sizeof(int));
+  }
   k_chunk_scan<2, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                             tp_len, y, ys_ch, ys_t, rg, Y0);
   return hipGetLastError();
