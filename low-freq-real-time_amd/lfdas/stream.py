@@ -43,6 +43,23 @@ class StreamOutput:
         return self.t_first_ns + np.arange(self.n_out, dtype=np.int64) * self.t_step_ns
 
 
+def _is_pinned_host(a) -> bool:
+    """True for pinned host memory: a pinned torch tensor, or a numpy view of
+    a ``pinned_empty`` buffer."""
+    try:
+        import torch
+        if isinstance(a, torch.Tensor):
+            return bool(a.is_pinned())
+    except ImportError:  # pragma: no cover
+        pass
+    b = a
+    while b is not None:
+        if getattr(b, "_lfd_owner", None) is not None:
+            return True
+        b = getattr(b, "base", None)
+    return False
+
+
 def _ns(t) -> int:
     if t is None:
         return 0
@@ -121,7 +138,11 @@ class LowpassStream:
         tensor, pinned or pageable) starting at time ``t0``."""
         ptr, s_ch, s_t, n_t, keep = self._host_view(x, time_axis)
         check(self._lib.lfd_stream_push(self._h, ptr, n_t, s_ch, s_t, _ns(t0)))
-        self._keep.append(keep)  # pinned pushes are copied asynchronously
+        if _is_pinned_host(keep):
+            # pinned pushes are DMA'd asynchronously: hold the buffer until the
+            # next fetch / wait_copy / synchronize (pageable ones are staged
+            # before push returns)
+            self._keep.append(keep)
         return self.last_output()
 
     def flush(self) -> StreamOutput:

@@ -179,3 +179,40 @@ def test_full_rate_filtfilt_parity():
     sos = oracle.butter_sos(4, 0.02)
     y = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos).cpu().numpy()
     assert _relrms(y, oracle.sosfiltfilt(sos, x)) < 1e-10
+
+
+def test_execute_is_graph_capturable():
+    """lfd_lowpass_execute allocates nothing and never synchronises, so a
+    whole chunked low-pass (K1 + scan) can be captured once as a HIP graph and
+    replayed (lfdas.h: "hipGraph-capturable")."""
+    import torch
+    from lfdas.plan import LowpassPlan
+    fs, dt_out, P, B, n_ch, dur = 500.0, 1.0, 120, 7, 48, 900.0
+    n = int(dur * fs)
+    dt_ns = int(round(1e9 / fs))
+    tg = S.time_grid(T0, T0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    lo, w = S.grid_positions(T0, dt_ns, tg)
+    chunks = [(*S.select_range(T0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    sos = oracle.butter_sos(4, (1 / dt_out / 2 * 0.9) / (fs / 2))
+    plan = LowpassPlan(sos, n_ch, n, lo, w, chunks)
+    x = torch.randn((n_ch, n), device="cuda") + 4.0
+    y_eager = torch.zeros((n_ch, len(tg)), device="cuda")
+    y_graph = torch.zeros_like(y_eager)
+    ws = plan.alloc_workspace()
+    plan.execute(x, y_eager, ws)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            plan.execute(x, y_graph, ws, stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y_graph, y_eager)
+    x.mul_(2.0)  # replay sees the new input in place
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.allclose(y_graph, 2.0 * y_eager, rtol=1e-6, atol=1e-5)
