@@ -44,8 +44,8 @@ def to_datetime64(obj):
 def to_timedelta64(obj):
     if isinstance(obj, np.timedelta64):
         return obj.astype("timedelta64[ns]")
-    if hasattr(obj, "to") and hasattr(obj, "magnitude"):  # quantity-like
-        obj = float(obj.magnitude)
+    if hasattr(obj, "to") and hasattr(obj, "magnitude"):  # quantity-like (lfdas.units)
+        obj = float(obj.to("s").magnitude)
     return np.timedelta64(int(round(float(obj) * 1e9)), "ns")
 
 
@@ -173,7 +173,11 @@ class Patch:
             if len(t):
                 a["time_min"] = t[0]
                 a["time_max"] = t[-1]
-            if len(t) > 1 and not any(k in a for k in ("time_step", "d_time", "step_time")):
+            if len(t) > 1:
+                # DASCore derives the step from the coordinate, so a decimated
+                # or rolled patch reports its own spacing (what chunk(time=None)
+                # merges on, lf_das.py:239); a user 'd_time' attr is kept as is
+                a.pop("step_time", None)
                 a["time_step"] = (t[1] - t[0]).astype("timedelta64[ns]")
         if "distance" in self.coords:
             d = self.coords["distance"]

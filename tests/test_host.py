@@ -155,3 +155,23 @@ def test_host_only_plan_cannot_execute():
     plan, _, _ = _plan_for(250.0, 0.2, 40, 6, 2, 6000)
     with pytest.raises((ValueError, TypeError)):
         plan.execute(torch.zeros(2, 6000), torch.zeros(2, 120), torch.zeros(10, dtype=torch.uint8))
+
+
+def test_units_and_coordinate_derived_time_step():
+    """dascore.units.s windows (rolling notebooks cell 7) and a time_step that
+    follows the time coordinate (what chunk(time=None) merges decimated or
+    rolled outputs on)."""
+    import lfdas.dc as dc
+    from lfdas.core import to_timedelta64
+    s = dc.units.s
+    assert to_timedelta64(10.0 * s) == np.timedelta64(10, "s")
+    assert to_timedelta64(250 * dc.units.ms) == np.timedelta64(250, "ms")
+    p = dc.get_example_patch()
+    assert p.attrs["step_time"] == np.timedelta64(4, "ms") == p.attrs["d_time"]
+    q = p.new(coords=p.coords.update(time=p.coords["time"][::50]), data=p.data[:, ::50])
+    assert q.attrs["time_step"] == np.timedelta64(200, "ms")
+    a = q.update_attrs(d_time=0.2)
+    assert a.attrs["d_time"] == 0.2 and a.attrs["time_step"] == np.timedelta64(200, "ms")
+    half = [q.select(time=(None, q.coords["time"][19])), q.select(time=(q.coords["time"][20], None))]
+    merged = dc.spool(half).chunk(time=None)
+    assert len(merged) == 1 and merged[0].shape == q.shape
