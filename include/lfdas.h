@@ -101,6 +101,11 @@ int lfd_set_timing(int enable);
 #define LFD_K1_RECURRENCE 1
 #define LFD_K1_MFMA 2
 #define LFD_K1_MFMA_RUNS 3 /* MFMA + in-register run folding (4th-order cascades) */
+/* 4th-order cascades whose K1 emits per-block functionals (recurrence K1, or
+ * MFMA taps too long for the in-register run buffers, e.g. L = 2000): a
+ * separate fold kernel turns them into runs before the scan. */
+#define LFD_K1_RECURRENCE_FOLD 4
+#define LFD_K1_MFMA_FOLD 5
 int lfd_lowpass_last_kernel(const lfd_lowpass_plan *plan);
 /* Testing hook: the plan's block taps Kx[n_comp][row_len] in natural layout,
  * F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p] (row_len = L + J).  With

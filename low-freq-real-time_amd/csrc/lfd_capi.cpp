@@ -508,7 +508,8 @@ struct lfd_lowpass_plan {
   lfd::TapGeom tg{};
   double *d_taps = nullptr;      // device layout (lfd_internal.h TapGeom)
   // run mode (lfd_internal.h RunConst): run table, K1 units, constants
-  bool run_ok = false;
+  bool run_ok = false;       // run table + constants (4th-order cascades)
+  bool run_mfma_ok = false;  // taps + 16 run buffers fit LDS: k_block_runs_mfma
   std::vector<int64_t> run_ks;
   std::vector<int> run_len, group_r0;
   lfd::RunConst rc{};
@@ -662,10 +663,13 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     }
   }
   p->bg.n_sf = p->sf_blocks;
-  // run mode: 4th-order cascade, MFMA taps, LDS for taps + 16 run buffers
-  if (n_sec == 2 && !p->taps.empty() &&
-      sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 8 * lfd::RUN_R * 5 * 16) <=
-          (size_t)lfd::TAP_LDS_MAX) {
+  // run mode: 4th-order cascades.  The MFMA K1 folds runs in registers when
+  // its LDS holds the taps + 16 run buffers; otherwise (and for the recurrence
+  // K1) k_fold_runs folds the per-block functionals.
+  if (n_sec == 2) {
+    p->run_mfma_ok = !p->taps.empty() &&
+        sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 8 * lfd::RUN_R * 5 * 16) <=
+            (size_t)lfd::TAP_LDS_MAX;
     std::vector<int64_t> cuts = {0, p->bg.nb};
     for (const auto &G : p->chunks) {
       cuts.push_back(G.kb);
@@ -715,9 +719,9 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   p->off_F = 0;
   p->off_SF = align256(p->off_F + sizeof(double) * (size_t)p->bg.nF * p->bg.nb * ch16);
   size_t end_F = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * ch64);
-  if (p->run_ok) {  // run-mode buffers alias the F / SF region (one mode per execute)
-    p->off_Y0 = 0;
-    p->off_AG = align256(sizeof(double) * (size_t)p->bg.nb * ch16);
+  if (p->run_ok) {  // run-mode buffers alias SF (unused in run mode); F stays for the fold
+    p->off_Y0 = p->off_SF;
+    p->off_AG = align256(p->off_Y0 + sizeof(double) * (size_t)p->bg.nb * ch16);
     p->off_SR = align256(p->off_AG + sizeof(double) * (size_t)p->run_ks.size() * 8 * ch16);
     end_F = std::max(end_F, align256(p->off_SR + sizeof(double) * (size_t)p->n_sr * 4 * ch64));
   }
@@ -810,15 +814,26 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
   const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !env_flag("LFD_K1_REC");
-  const bool runs = mfma && p->run_ok && !env_flag("LFD_NO_RUNS");
-  p->last_k1 = runs ? LFD_K1_MFMA_RUNS : (mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE);
+  const bool runs = p->run_ok && !env_flag("LFD_NO_RUNS");
+  const bool mfma_runs = runs && mfma && p->run_mfma_ok;
+  p->last_k1 = mfma_runs ? LFD_K1_MFMA_RUNS
+                         : runs ? (mfma ? LFD_K1_MFMA_FOLD : LFD_K1_RECURRENCE_FOLD)
+                                : (mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE);
   if (runs) {
     const lfd::RunGeom rg{(int64_t)p->run_ks.size(), (int64_t)p->group_r0.size() - 1, p->n_sr,
                           p->d_run_ks, p->d_run_len, p->d_group_r0, p->d_rc};
     double *Y0 = reinterpret_cast<double *>(ws + p->off_Y0);
     double *AG = reinterpret_cast<double *>(ws + p->off_AG);
     double *SR = reinterpret_cast<double *>(ws + p->off_SR);
-    LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
+    if (mfma_runs) {
+      LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
+    } else {
+      if (mfma)
+        LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, F, st));
+      else
+        LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
+      LFD_HIP(lfd::launch_fold_runs(F, p->bg, rg, Y0, AG, st));
+    }
     if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
     LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks,
                                         p->n_chunks, Y0, AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st));

@@ -157,6 +157,10 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
 hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
                                   double *Y0, double *AG, hipStream_t st);
+// Run epilogue applied to per-block functionals F (K1 kernels without run
+// mode): F -> Y0, AG (n_sec == 2).
+hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,
+                            double *AG, hipStream_t st);
 hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg_dev, int64_t n_chunks, const double *Y0,

@@ -1478,6 +1478,112 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   return run_k1<1, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 }
 
+// ---------------------------------------------------------------------------
+// k_fold_runs — run mode for the K1 kernels that emit per-block functionals
+// F (the recurrence kernels: strided / time-major / unaligned rows; the MFMA
+// kernel when taps + run buffers exceed LDS, L = 2000).  Applies the same
+// run epilogue as k_block_runs_mfma (forward prefix S0 over the run's blocks,
+// reverse inputs v = e_r0 + M S0 and pg = p0 + G0.S0, backward sweep from a
+// zero state) to F and writes Y0 and the run aggregates, so the scan walks
+// runs (9x fewer steps) instead of blocks.  One lane = one channel (64
+// consecutive channels per wave: 4 x 128-B pieces per F load), one wave = one
+// run; the whole run (<= RUN_R blocks) stays in registers.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fold_runs(const double *__restrict__ F, BlockGeom g,
+                                                   RunGeom rg, double *__restrict__ Y0,
+                                                   double *__restrict__ AG) {
+  constexpr int N = RUN_N;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t n_c64 = (g.n_ch + 63) / 64;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + wave;  // run-major: r = unit / n_c64
+  if (unit >= n_c64 * rg.n_runs) return;
+  const int64_t r = unit / n_c64, c64 = unit % n_c64;
+  const int64_t ch = c64 * 64 + lane;
+  if (ch >= g.n_ch) return;
+  const RunConst &rc = *rg.rc;
+  double PhiF[16], Mm[16], PhiR[16], G0[4], H0[4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    PhiF[i] = rc.PhiF[i];
+    Mm[i] = rc.M[i];
+    PhiR[i] = rc.PhiR[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    G0[i] = rc.G0[i];
+    H0[i] = rc.H0[i];
+  }
+  const int64_t ks = rg.run_ks[r];
+  const int len = rg.run_len[r];
+  double S0[N] = {0.0, 0.0, 0.0, 0.0};
+  double v[RUN_R][N], pg[RUN_R];
+#pragma unroll
+  for (int p = 0; p < RUN_R; ++p) {
+    if (p < len) {
+      const double *Fo = F + f_index(ks + p, 0, ch, g.nb, 2 * N + 1);
+      double ef[N], er[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        ef[i] = Fo[i * F_CSTRIDE];
+        er[i] = Fo[(N + i) * F_CSTRIDE];
+      }
+      double pgp = Fo[2 * N * F_CSTRIDE];
+      double sn[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double vi = er[i], si = ef[i];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          vi = fma(Mm[i * 4 + j], S0[j], vi);
+          si = fma(PhiF[i * 4 + j], S0[j], si);
+        }
+        v[p][i] = vi;
+        sn[i] = si;
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) pgp = fma(G0[j], S0[j], pgp);
+      pg[p] = pgp;
+#pragma unroll
+      for (int i = 0; i < N; ++i) S0[i] = sn[i];
+    }
+  }
+  double T[N] = {0.0, 0.0, 0.0, 0.0};
+  double *y0o = Y0 + ((ch >> 4) * g.nb + ks) * 16 + (ch & 15);
+#pragma unroll
+  for (int p = RUN_R - 1; p >= 0; --p) {
+    if (p < len) {
+      double y0 = pg[p];
+#pragma unroll
+      for (int j = 0; j < N; ++j) y0 = fma(H0[j], T[j], y0);
+      y0o[p * 16] = y0;
+      double nt[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double acc = v[p][i];
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = fma(PhiR[i * 4 + j], T[j], acc);
+        nt[i] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) T[i] = nt[i];
+    }
+  }
+  double *ag = AG + (((ch >> 4) * rg.n_runs + r) * 8) * 16 + (ch & 15);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    ag[i * 16] = S0[i];
+    ag[(4 + i) * 16] = T[i];
+  }
+}
+
+hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,
+                            double *AG, hipStream_t st) {
+  if (g.nF != 2 * RUN_N + 1 || rg.n_runs < 1) return hipErrorInvalidValue;
+  const int64_t units = ((g.n_ch + 63) / 64) * rg.n_runs;
+  k_fold_runs<<<nblk(units, 4), 256, 0, st>>>(F, g, rg, Y0, AG);
+  return hipGetLastError();
+}
+
 hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg, int64_t n_chunks, const double *Y0,

@@ -66,11 +66,13 @@ def test_lfproc_parity(cfg, dc, layout):
         produced[oa:ob] = True
     assert (num / den) ** 0.5 < 1e-4
     assert np.all(np.isnan(y[:, ~produced]))  # trimmed edges untouched
-    # contiguous rows run the fp64-MFMA block taps; strided rows the recurrence
-    if layout == "tc":  # run folding wherever its LDS fits (not at L = 2000)
-        assert _run.last_kernel == ("mfma" if fs * dt_out == 2000 else "mfma_runs")
+    # contiguous rows run the fp64-MFMA block taps; strided rows the recurrence;
+    # both fold into runs (in registers where the MFMA kernel's LDS fits the
+    # run buffers, else by the separate fold kernel: L = 2000, recurrence)
+    if layout == "tc":
+        assert _run.last_kernel == ("mfma_fold" if fs * dt_out == 2000 else "mfma_runs")
     else:
-        assert _run.last_kernel == "recurrence"
+        assert _run.last_kernel == "recurrence_fold"
 
 
 def _plan_cfg(fs, dt_out, P, B, n_ch, n):
@@ -101,23 +103,27 @@ def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
     xd = torch.from_numpy(x).cuda()
     ws = plan.alloc_workspace()
     out = {}
-    for mode in ("default", "noruns", "rec"):
+    for mode in ("default", "noruns", "rec", "recfold"):
         if mode == "noruns":
             monkeypatch.setenv("LFD_NO_RUNS", "1")
         if mode == "rec":
             monkeypatch.setenv("LFD_K1_REC", "1")
+        if mode == "recfold":
+            monkeypatch.delenv("LFD_NO_RUNS")
         yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
         plan.execute(xd, yd, ws)
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
     aligned = n % 4 == 0
     L = int(fs * dt_out)
-    assert out["default"][1] == (("mfma_runs" if L != 2000 else "mfma") if aligned else "recurrence")
+    assert out["default"][1] == (("mfma_runs" if L != 2000 else "mfma_fold") if aligned
+                                 else "recurrence_fold")
     assert out["noruns"][1] == ("mfma" if aligned else "recurrence")
     assert out["rec"][1] == "recurrence"
+    assert out["recfold"][1] == "recurrence_fold"
     b = out["rec"][0]
     m = ~np.isnan(b)
-    for mode in ("default", "noruns"):
+    for mode in ("default", "noruns", "recfold"):
         a = out[mode][0]
         assert np.array_equal(np.isnan(a), ~m)
         assert _relrms(a[m], b[m]) < 1e-6
@@ -125,7 +131,7 @@ def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
 
 def test_k1_unaligned_base_pointer():
     """A view starting one sample in (not 16-B aligned) takes the recurrence
-    kernel and still matches the oracle."""
+    kernel (+ run fold) and still matches the aligned MFMA path."""
     import torch
     fs, dt_out, P, B = 500.0, 1.0, 60, 7
     n_ch, n = 9, 40_000
@@ -136,7 +142,7 @@ def test_k1_unaligned_base_pointer():
     xd = full[:, 1:n + 1]
     yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
     plan.execute(xd, yd, plan.alloc_workspace())
-    assert plan.last_kernel() == "recurrence"
+    assert plan.last_kernel() == "recurrence_fold"
     y_ok = yd.cpu().numpy()
     xa = torch.from_numpy(np.ascontiguousarray(x[:, 1:n + 1])).cuda()
     yd2 = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
