@@ -36,6 +36,15 @@ namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
+// Nulls (SciPy semantics): a NaN / inf sample poisons every output of the
+// chunks that contain it and nothing else.  A block's functionals also read
+// samples outside its own L: J samples of FIR history and, in the MFMA
+// kernels, zero-tap padding past the row.  Those reads are finite-masked
+// (non-finite -> 0; finite values are unchanged) so that a null right
+// beside a chunk boundary cannot leak into the neighbouring chunk; the scan's
+// FIR-history correction masks the same samples the same way.
+__device__ __forceinline__ float finite_or_zero(float v) { return __builtin_isfinite(v) ? v : 0.0f; }
+
 // ---------------------------------------------------------------------------
 // TDF-II cascade step, SciPy's `_sosfilt` form (full-rate path only)
 // ---------------------------------------------------------------------------
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256, LFD_K1_MINW) void k_block_functionals_lds(
     const int64_t a = g.base + kc_ * (int64_t)L;
     const float *row = x + chc * s_ch;
 #pragma unroll
-    for (int j = 0; j < J; ++j) h[j] = (a - 1 - j >= 0) ? row[a - 1 - j] : 0.0f;
+    for (int j = 0; j < J; ++j) h[j] = (a - 1 - j >= 0) ? finite_or_zero(row[a - 1 - j]) : 0.0f;
   }
 
   const int nfull = L / TS;              // full slices
@@ -371,7 +380,7 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
   const float *row = x + ch * s_ch;
   float h[J];
 #pragma unroll
-  for (int j = 0; j < J; ++j) h[j] = (a - 1 - j >= 0) ? row[(a - 1 - j) * s_t] : 0.0f;
+  for (int j = 0; j < J; ++j) h[j] = (a - 1 - j >= 0) ? finite_or_zero(row[(a - 1 - j) * s_t]) : 0.0f;
   const float *p = row + a * s_t;
   float buf[D];
 #pragma unroll
@@ -522,7 +531,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
     for (int j = 0; j < J; ++j) {
       const int64_t t = G.head_end - 1 - j;
-      dh[j] = h[j] - (t >= 0 ? (double)xc[t * s_t] : 0.0);
+      dh[j] = h[j] - (t >= 0 ? (double)finite_or_zero(xc[t * s_t]) : 0.0);
     }
     double dw[J];
 #pragma unroll
@@ -962,6 +971,20 @@ __device__ __forceinline__ f4v mf_load_guarded(const float *__restrict__ xr, int
   return v;
 }
 
+// finite-mask the elements of one 64-sample iteration that lie outside the
+// block's own samples (row offsets [lo, hi) = [J + v, J + v + L)); o0 = this
+// lane's first offset (64 it + 4 q).  Only a block's first iteration (FIR
+// history) and last iteration (zero-tap padding) hold such elements.
+__device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o0, int lo, int hi) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = o0 + 16 * j + e;
+      if ((o < lo || o >= hi) && !__builtin_isfinite(cur[j][e])) cur[j][e] = 0.0f;
+    }
+}
+
 // 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur.
 // Lanes of A rows c >= nc read a copy of row nc-1 instead of zeros: MFMA rows
 // are independent (D[c][:] depends on A[c][:] only) and rows >= nc of D are
@@ -1058,6 +1081,7 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
       f4v cur[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+      if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
       mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
     mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
@@ -1110,6 +1134,10 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
         for (int j = 0; j < 4; ++j)
           acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
       } else {
+        if (it == 0 || it == nit - 1) {
+          const int v = (int)(s & 3);
+          mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+        }
         mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
       }
       if (++it == nit) {
@@ -1263,6 +1291,7 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
       f4v cur[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+      if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
       mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
     block_done(acc0, acc1, k);
@@ -1313,6 +1342,13 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
           for (int j = 0; j < 4; ++j)
             acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
         } else {
+          // every chunk's first and last full block is a run end, and inside
+          // a run the out-of-block samples belong to the run's own blocks:
+          // only a run's first and last iteration need the finite mask
+          if ((it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen)) {
+            const int v = (int)(s & 3);
+            mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+          }
           mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
         }
         if (++it == nit) {

@@ -222,3 +222,28 @@ def test_execute_is_graph_capturable():
     g.replay()
     torch.cuda.synchronize()
     assert torch.allclose(y_graph, 2.0 * y_eager, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("layout", ["tc", "cc"])
+@pytest.mark.parametrize("where", ["interior", "before_chunk_start", "after_chunk_end"])
+def test_nonfinite_samples_poison_their_chunk_only(where, layout):
+    """SciPy semantics for nulls: a NaN or inf sample turns every output of
+    its (chunk, channel) into NaN (forward pass, then the reverse pass from
+    its NaN end), and nothing else.  Samples right beside a chunk boundary
+    (FIR history of the next chunk's first block; zero-tap padding read past
+    the previous chunk's last block) must not leak into the neighbour."""
+    fs, dt_out, P, B, n_ch, dur = 500.0, 1.0, 600, 7, 8, 1500.0
+    n = int(dur * fs)
+    x = np.random.default_rng(1).standard_normal((n_ch, n)).astype(np.float32)
+    # chunks: samples [0, 600 s], [586 s, 1186 s], [1172 s, 1499 s]
+    pos = {"interior": (300.0, 900.0),
+           "before_chunk_start": (586.0 - 1 / fs, 1172.0 - 2 / fs),
+           "after_chunk_end": (600.0 + 1 / fs, 1186.0 + 3 / fs)}[where]
+    x[3, int(round(pos[0] * fs))] = np.nan
+    x[5, int(round(pos[1] * fs))] = np.inf
+    y, ref, sched = _run(x, fs, dt_out, P, B, layout)
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        yy = y[:, oa:ob]
+        assert np.array_equal(np.isnan(yy), np.isnan(r)), (where, a, b)
+        m = ~np.isnan(r)
+        assert _relrms(yy[m], r[m]) < 1e-4
