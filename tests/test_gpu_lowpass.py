@@ -177,6 +177,30 @@ def test_rolling_mean_parity():
             assert _relrms(y[m], ref[m]) < 1e-6
 
 
+def test_rolling_mean_nulls():
+    """A NaN / inf sample affects exactly the windows that contain it (per-window
+    mean over the raw values, like DASCore's numpy engine); window edges next to
+    it stay exact."""
+    import torch
+    from lfdas.plan import rolling_mean_device
+    rng = np.random.default_rng(4)
+    n_ch, n, W, S_ = 6, 10000, 1000, 1000
+    x = (rng.standard_normal((n_ch, n)) + 0.5).astype(np.float32)
+    x[1, 2999] = np.nan   # inside window k = 3 (samples 2001..3000)
+    x[2, 3000] = np.inf   # first sample after window k = 3
+    x[3, 4001] = -np.inf
+    x[4, 0] = np.nan      # only in the leading (NaN) window
+    ref = oracle.rolling_mean(x, W, S_)
+    for layout in ("tc", "cc"):
+        xd = torch.from_numpy(x).cuda() if layout == "tc" else torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()
+        y = rolling_mean_device(xd, W, S_).cpu().numpy()
+        assert np.array_equal(np.isnan(y), np.isnan(ref))
+        assert np.array_equal(np.isposinf(y), np.isposinf(ref))
+        assert np.array_equal(np.isneginf(y), np.isneginf(ref))
+        m = np.isfinite(ref)
+        assert _relrms(y[m], ref[m]) < 1e-6
+
+
 def test_full_rate_filtfilt_parity():
     import torch
     from lfdas.plan import sosfiltfilt_device
@@ -247,3 +271,48 @@ def test_nonfinite_samples_poison_their_chunk_only(where, layout):
         assert np.array_equal(np.isnan(yy), np.isnan(r)), (where, a, b)
         m = ~np.isnan(r)
         assert _relrms(yy[m], r[m]) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [
+    (250.0, 0.2, 40, 6, 37, 6000, 37),      # L = 50
+    (500.0, 1.0, 600, 7, 33, 750_001, 40),  # L = 500, channel subset of a wider (time, ch) array
+    (1000.0, 0.5, 40, 4, 18, 100_003, 18),  # odd n_t
+])
+def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
+    """(time, channel) storage viewed as (channel, time) (s_ch = 1, s_t =
+    row width): recurrence K1 + run fold agrees with the per-block scan and
+    with the oracle, nulls included."""
+    import torch
+    fs, dt_out, P, B, n_ch, n, width = cfg
+    rng = np.random.default_rng(9)
+    xt = (rng.standard_normal((n, width)) + 30.0).astype(np.float32)
+    xt[n // 3, 2] = np.nan  # a null: its chunks' outputs of channel 2 are NaN
+    plan, n_grid = _plan_cfg(fs, dt_out, P, B, n_ch, n)
+    xd = torch.from_numpy(xt).cuda()[:, :n_ch].t()
+    assert xd.stride() == (1, width)
+    ws = plan.alloc_workspace()
+    out = {}
+    for mode in ("default", "blocks"):
+        if mode == "blocks":
+            monkeypatch.setenv("LFD_NO_RUNS", "1")
+        yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
+        plan.execute(xd, yd, ws)
+        torch.cuda.synchronize()
+        out[mode] = (yd.cpu().numpy(), plan.last_kernel())
+    assert out["default"][1] == "recurrence_fold"
+    assert out["blocks"][1] == "recurrence"
+    a, b = out["default"][0], out["blocks"][0]
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    m = ~np.isnan(b)
+    assert _relrms(a[m], b[m]) < 1e-6
+    # oracle on the same channels
+    x = np.ascontiguousarray(xt[:, :n_ch].T)
+    dt_ns = int(round(1e9 / fs))
+    tg = S.time_grid(T0, T0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    ref = oracle.lfproc_process(x, T0, dt_ns, tg[0], tg[-1] + 1, dt_out, P, B)
+    for (tt, r), (_, _, oa, ob) in zip(ref, sched):
+        yy = a[:, oa:ob]
+        assert np.array_equal(np.isnan(yy), np.isnan(r))
+        mm = ~np.isnan(r)
+        assert _relrms(yy[mm], r[mm]) < 1e-4
