@@ -54,6 +54,59 @@ __global__ __launch_bounds__(256) void k_pattern(const float *__restrict__ x, fl
   if (acc == 1234.5f) out[unit] = acc;
 }
 
+// K1's per-block rows: block k of a unit reads 8 x 64 samples from
+// floor4(k*L - 4), i.e. 512 samples per 500-sample block (12 re-read), as
+// 16 rows x 64 B per instruction; OVL = 0 reads the same rows back to back
+// without the overlap (512-sample blocks) for comparison.
+template <int OVL>
+__global__ __launch_bounds__(256) void k_blockrows(const float *__restrict__ x, float *out, int bpu) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t unit = (int64_t)blockIdx.x * 4 + wave;
+  const int L = OVL ? 500 : 512;
+  const int64_t nb = (NT - 16) / L;
+  const int64_t n_cg = NCH / 16, runs = nb / bpu;
+  if (unit >= n_cg * runs) return;
+  const int64_t cg = unit % n_cg, run = unit / n_cg;
+  const int col = lane & 15, q = lane >> 4;
+  const float *xr = x + (cg * 16 + col) * NT + 4 * q;
+  float acc = 0.f;
+  for (int64_t k = run * bpu; k < (run + 1) * bpu; ++k) {
+    const int64_t a = OVL ? (k * L) & ~(int64_t)3 : k * L;
+    f4v v[8][4];
+#pragma unroll
+    for (int it = 0; it < 8; ++it)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[it][j] = *reinterpret_cast<const f4v *>(xr + a + 64 * it + 16 * j);
+#pragma unroll
+    for (int it = 0; it < 8; ++it)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += v[it][j].x + v[it][j].y + v[it][j].z + v[it][j].w;
+  }
+  if (acc == 1234.5f) out[unit] = acc;
+}
+
+template <int OVL>
+void run_blockrows(const float *x, float *out, const char *name) {
+  const int bpu = 32;
+  const int L = OVL ? 500 : 512;
+  const int64_t nb = (NT - 16) / L;
+  const int64_t units = (NCH / 16) * (nb / bpu);
+  const unsigned grid = (unsigned)((units + 3) / 4);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  k_blockrows<OVL><<<grid, 256>>>(x, out, bpu);
+  (void)hipEventRecord(e0);
+  for (int r = 0; r < 3; ++r) k_blockrows<OVL><<<grid, 256>>>(x, out, bpu);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  ms /= 3;
+  const double alg = (double)NCH * (double)(nb / bpu * bpu) * L * 4.0;  // distinct bytes
+  printf("%-34s %7.3f ms  %6.2f TB/s of distinct bytes (%.2f GB)\n", name, ms, alg / (ms * 1e-3) / 1e12, alg / 1e9);
+}
+
 __global__ void k_fill(float *x, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint32_t h = (uint32_t)(i * 2654435761u) ^ (uint32_t)(i >> 13);
@@ -106,6 +159,8 @@ int main() {
   run<1>(x, out, 18000, "rand: 1 row x 1 KB", 37 * 1024);
   run<16>(x, out, 16000, "rand: 16 rows x 64 B", 37 * 1024);
   run<16>(x, out, 16000, "rand: 16 rows x 64 B", 70 * 1024);
+  run_blockrows<1>(x, out, "blockrows L=500 (512-sample rows)");
+  run_blockrows<0>(x, out, "blockrows L=512 (no overlap)");
   // known-size store for WRITE_SIZE calibration: 360 M doubles = 2.88 GB
   k_store8<<<8192, 256>>>(reinterpret_cast<double *>(x), 360000000LL);
   (void)hipDeviceSynchronize();
