@@ -3,7 +3,7 @@
 set -e -o pipefail
 TAG=${1:-r01}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu_$TAG.log
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 tail -1 gpurun_out/bench_$TAG.json
