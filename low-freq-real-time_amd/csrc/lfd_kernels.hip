@@ -667,9 +667,20 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     };
     const double *agb = F + (((ch >> 4) * rg.n_runs) * 8) * 16 + (ch & 15);
     const double *y0b = Y0 + ((ch >> 4) * g.nb) * 16 + (ch & 15);
-    auto load_run = [&](int64_t r, RunIn &o) {
+    // a run's geometry (len, first block) is loaded SCAN_DB runs before its
+    // inputs: the Y0 addresses depend on it, and vmcnt waits are in order, so
+    // loading it together with the inputs drained the whole ring every run
+    struct RunGeo {
+      int len;
+      int64_t ks;
+    };
+    auto load_geo = [&](int64_t r, RunGeo &o) {
       o.len = rg.run_len[r];
       o.ks = rg.run_ks[r];
+    };
+    auto load_run = [&](int64_t r, const RunGeo &gg, RunIn &o) {
+      o.len = gg.len;
+      o.ks = gg.ks;
       const double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
 #pragma unroll
       for (int i = 0; i < N; ++i) {
@@ -681,17 +692,28 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     };
     // ring of SCAN_DB runs (r-1 .. r-SCAN_DB in flight while run r is applied)
     constexpr int DB = SCAN_DB;
+    // q[u] holds run r's inputs, gq[u] run r-DB's geometry (slot u = r mod DB)
     RunIn q[DB];
+    RunGeo gq[DB];
+#pragma unroll
+    for (int u = 0; u < DB; ++u) {
+      if (G.r1 - 1 - u >= G.r0) {
+        RunGeo g0;
+        load_geo(G.r1 - 1 - u, g0);
+        load_run(G.r1 - 1 - u, g0, q[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < DB; ++u)
-      if (G.r1 - 1 - u >= G.r0) load_run(G.r1 - 1 - u, q[u]);
+      if (G.r1 - 1 - u - DB >= G.r0) load_geo(G.r1 - 1 - u - DB, gq[u]);
     for (int64_t rb = G.r1 - 1; rb >= G.r0 && !(g_scan_diag & 8); rb -= DB)
 #pragma unroll
     for (int u = 0; u < DB; ++u) {
       const int64_t r = rb - u;
       if (r < G.r0) break;
       const RunIn cur = q[u];
-      if (r - DB >= G.r0) load_run(r - DB, q[u]);
+      if (r - DB >= G.r0) load_run(r - DB, gq[u], q[u]);
+      if (r - 2 * DB >= G.r0) load_geo(r - 2 * DB, gq[u]);
       const int len = cur.len;
       const int64_t ks = cur.ks;
       const double *sin = cur.sin;
