@@ -1647,14 +1647,20 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   const ChunkGeom *cg, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
                                   float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
-  const unsigned nb = nblk(n_chunks * g.n_ch, 256);
-  static int diag = -1;
+  static int diag = -1, threads = 256;
   if (diag < 0) {
     const char *v = std::getenv("LFD_SCAN_DIAG");
     diag = v ? std::atoi(v) : 0;
     if (diag) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_scan_diag), &diag, sizeof(int));
+    // workgroup size A/B knob (64, 128 or 256 threads; the kernel's LDS
+    // staging is per wave and its launch bound is 256)
+    if (const char *t = std::getenv("LFD_SCAN_THREADS")) {
+      const int w = std::atoi(t);
+      if (w == 64 || w == 128 || w == 256) threads = w;
+    }
   }
-  k_chunk_scan<2, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
+  const unsigned nb = nblk(n_chunks * g.n_ch, threads);
+  k_chunk_scan<2, true><<<nb, threads, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                             tp_len, y, ys_ch, ys_t, rg, Y0);
   return hipGetLastError();
 }
