@@ -471,6 +471,8 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 // left pad/head, 2 the forward run scan, 4 the right pad and its reverse,
 // 8 the backward run scan.
 __constant__ int g_scan_diag = 0;
+// K1 unit order (see k_block_runs_mfma; 0 = channel-group-major)
+__constant__ int g_k1_band = 0;
 
 template <int NS, bool RUNS>
 __global__ __launch_bounds__(256) void k_chunk_scan(
@@ -1221,8 +1223,22 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
   const int64_t n_cg = (g.n_ch + 15) / 16;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_cg * rg.n_groups) return;
-  // channel-group-major unit order (time-major measured 2 % slower on cfg3)
-  const int64_t cg = unit % n_cg, grp = unit / n_cg;
+  // channel-group-major unit order (time-major measured 2 % slower on cfg3);
+  // g_k1_band > 0 (A/B knob LFD_K1_BAND) walks bands of that many channel
+  // groups, time groups inside a band, so fewer pages are in flight at once
+  int64_t cg, grp;
+  if (g_k1_band > 0) {
+    const int64_t band = g_k1_band;
+    const int64_t b = unit / (band * rg.n_groups);
+    const int64_t base = b * band;
+    const int64_t bw = min(band, n_cg - base);
+    const int64_t rem = unit - b * band * rg.n_groups;
+    grp = rem / bw;
+    cg = base + rem % bw;
+  } else {
+    cg = unit % n_cg;
+    grp = unit / n_cg;
+  }
   int r = __builtin_amdgcn_readfirstlane(rg.group_r0[grp]);
   const int r_end = __builtin_amdgcn_readfirstlane(rg.group_r0[grp + 1]);
   // the unit's run table (<= 32 runs) is held one run per lane and read with
@@ -1522,6 +1538,19 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   // independently, unlike one 1024-thread group per CU: 12.3-12.7 ms vs
   // 12.65-13.0 on cfg3 (A/B, tools/ab_env.sh)
   int mode = 0, pf = 1, nt = 512;
+  {
+    static int band_set = 0;
+    const char *v = std::getenv("LFD_K1_BAND");
+    const int band = v ? std::max(0, std::atoi(v)) : 0;
+    if (band != band_set) {
+      hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_k1_band), &band, sizeof(int), 0,
+                                            hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return e;
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+      band_set = band;
+    }
+  }
   if (const char *v = std::getenv("LFD_RUN_MODE")) mode = std::atoi(v);
   if (const char *v = std::getenv("LFD_RUN_PF")) pf = std::atoi(v);
   if (const char *v = std::getenv("LFD_RUN_NT")) nt = std::atoi(v);
