@@ -1536,8 +1536,9 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
   // 512-thread workgroups (2 per CU: 16 waves, 2 x 77 KB LDS at cfg3) retire
   // independently, unlike one 1024-thread group per CU: 12.3-12.7 ms vs
-  // 12.65-13.0 on cfg3 (A/B, tools/ab_env.sh)
-  int mode = 0, pf = 1, nt = 512;
+  // 12.65-13.0 on cfg3 (A/B, tools/ab_env.sh). Prefetch depth 2: 0.6 % faster
+  // than depth 1 in 15 of 15 in-process pairs on two boxes (tools/probe_k1cfg.py)
+  int mode = 0, pf = 2, nt = 512;
   {
     static int band_set = 0;
     const char *v = std::getenv("LFD_K1_BAND");
