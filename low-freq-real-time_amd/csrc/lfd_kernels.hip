@@ -1559,6 +1559,8 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   if (mode == 4 && nt == 320) return run_k1<1, 4, 320>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (mode == 4 && nt == 512) return run_k1<1, 4, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (mode == 4) return run_k1<1, 4, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 3 && nt == 512) return run_k1<3, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 4 && nt == 512) return run_k1<4, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 2 && nt == 768) return run_k1<2, 0, 768>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 2 && nt == 384) return run_k1<2, 0, 384>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 2 && nt == 512) return run_k1<2, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);

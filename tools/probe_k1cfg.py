@@ -19,10 +19,9 @@ from lfdas.plan import set_timing  # noqa: E402
 
 CFGS = {
     "base": {},
-    "nt1024": {"LFD_RUN_NT": "1024"},
-    "pf2nt512": {"LFD_RUN_PF": "2", "LFD_RUN_NT": "512"},
-    "pf2nt384": {"LFD_RUN_PF": "2", "LFD_RUN_NT": "384"},
-    "pf2nt768": {"LFD_RUN_PF": "2", "LFD_RUN_NT": "768"},
+    "pf1nt512": {"LFD_RUN_PF": "1", "LFD_RUN_NT": "512"},
+    "pf3nt512": {"LFD_RUN_PF": "3", "LFD_RUN_NT": "512"},
+    "pf4nt512": {"LFD_RUN_PF": "4", "LFD_RUN_NT": "512"},
 }
 KNOBS = ("LFD_RUN_NT", "LFD_RUN_PF")
 
@@ -35,15 +34,20 @@ y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
 wsb = plan.alloc_workspace(dev)
 st = torch.cuda.current_stream(dev)
 set_timing(True)
+ref = None
 for rep in range(3):
     for name, env in CFGS.items():
         for kk in KNOBS:
             os.environ.pop(kk, None)
         os.environ.update(env)
         plan.execute(x, y, wsb, st)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = y.clone()
+        same = bool(torch.equal(y, ref))
         k = []
         for _ in range(5):
             plan.execute(x, y, wsb, st)
             k.append(plan.last_timing_ms()[0])
         print(f"rep {rep} {name:10s} {plan.last_kernel()} K1 {np.mean(k):.3f} "
-              f"(min {np.min(k):.3f} max {np.max(k):.3f})", flush=True)
+              f"(min {np.min(k):.3f} max {np.max(k):.3f}) bit-identical {same}", flush=True)
