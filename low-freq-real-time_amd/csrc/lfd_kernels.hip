@@ -902,21 +902,30 @@ __device__ __forceinline__ double window_part(const float *__restrict__ x, int64
 
 // One wave per output window (grid-stride).  Two windows per step: their
 // loads are issued together (8 KB per wave in flight at W = 1000).
+#ifndef ROLL_H
+#define ROLL_H 2  // windows per wave step
+#endif
 __global__ __launch_bounds__(256) void k_rolling_tc(
     const float *__restrict__ x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     int64_t W, int64_t S, float *__restrict__ y, int64_t ys_ch, int64_t ys_t,
     bool vec) {
+  constexpr int H = ROLL_H;
   const int64_t n_out = (n_t + S - 1) / S;
   const int64_t n_win = n_ch * n_out;
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const float nanv = __builtin_nanf("");
-  for (int64_t w0 = wave0; w0 < n_win; w0 += 2 * n_waves) {
-    double acc[2] = {0.0, 0.0};
-    float *out[2] = {nullptr, nullptr};
+  for (int64_t w0 = wave0; w0 < n_win; w0 += H * n_waves) {
+    double acc[H];
+    float *out[H];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
+      acc[h] = 0.0;
+      out[h] = nullptr;
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
       const int64_t wi = w0 + h * n_waves;
       if (wi >= n_win) continue;
       const int64_t ch = wi / n_out, k = wi % n_out;
@@ -931,7 +940,7 @@ __global__ __launch_bounds__(256) void k_rolling_tc(
       acc[h] = window_part(x, a, a + W, lane, vec);
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
       if (!out[h]) continue;
       const double t = wave_sum(acc[h]);
       if (lane == 0) *out[h] = (float)(t / (double)W);
