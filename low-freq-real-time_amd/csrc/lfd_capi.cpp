@@ -219,7 +219,9 @@ struct BlockSim {
 
 // One block of L samples with given initial forward state, reverse state
 // entering from the right and an optional unit impulse in w at offset imp.
-BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp) {
+// p0 is the output functional: (1 - ow) y[0] + ow y[1] (ow > 0 needs
+// L >= J + 2).
+BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp, R ow) {
   const int n = 2 * m.ns;
   R S[MAX_N], T[MAX_N];
   for (int i = 0; i < n; ++i) {
@@ -234,19 +236,33 @@ BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp) 
     o.ef[i] = S[i];
     o.er0[i] = T[i];
   }
-  R acc = 0;
-  for (int j = 0; j <= m.J; ++j) acc += m.c[j] * ql[j];
-  o.p0 = m.G * acc;
+  R acc0 = 0, acc1 = 0;
+  for (int j = 0; j <= m.J; ++j) {
+    acc0 += m.c[j] * ql[j];
+    if (ow != 0) acc1 += m.c[j] * ql[j + 1];
+  }
+  o.p0 = m.G * ((1.0L - ow) * acc0 + ow * acc1);
   return o;
 }
 
-// Fill the block-functional and scan constants for block length L.
-int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanConst &sc,
+// Weights e[i] (i <= J + 1) of the reverse outputs q_last[i] in the output
+// functional: (1 - ow) sum_j c_j q[j] + ow sum_j c_j q[j + 1].
+void out_weights(const RModel &m, R ow, R *e) {
+  for (int i = 0; i <= m.J + 1; ++i) {
+    e[i] = 0;
+    if (i <= m.J) e[i] += (1.0L - ow) * m.c[i];
+    if (i >= 1) e[i] += ow * m.c[i - 1];
+  }
+}
+
+// Fill the block-functional and scan constants for block length L and output
+// weight ow (the grid's constant fractional sample position).
+int block_constants(const Cascade &cs, int L, R ow, lfd::BlockConst &kc, lfd::ScanConst &sc,
                     bool &fir32) {
   RModel m;
   if (int e = make_rmodel(cs, m)) return e;
   const int n = 2 * m.ns, J = m.J;
-  if (L < J + 1) return fail(LFD_EUNSUPPORTED, "grid spacing shorter than the FIR span");
+  if (L < J + 1 + (ow != 0 ? 1 : 0)) return fail(LFD_EUNSUPPORTED, "block shorter than the FIR span");
   std::memset(&kc, 0, sizeof(kc));
   std::memset(&sc, 0, sizeof(sc));
   lfd::RCoef rc{};
@@ -287,9 +303,11 @@ int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanCons
   const Mat Tm = mpow(A, L - 1);
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) kc.T[i * MAX_N + j] = (double)(m.G * Tm.a[i][j]);
-  // p0 as a linear function of (u, y0[0..J-1]) (unscaled v_last inputs):
+  // p0 as a linear function of (u, y0[0..J]) (unscaled v_last inputs):
   // T(0) = Tm u, T(j) = A^{-j} (T(0) - sum_{q<j} A^q B y0[q]),
-  // p0 = G * G * sum_j c_j T(j)[2(ns-1)]
+  // p0 = G * G * sum_{j <= J+1} e_j T(j)[2(ns-1)]  (out_weights)
+  R ew[lfd::MAX_J + 2];
+  out_weights(m, ow, ew);
   auto p0_of = [&](const R *u, const R *y0) {
     R T0[MAX_N];
     for (int i = 0; i < n; ++i) {
@@ -297,7 +315,8 @@ int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanCons
       for (int j = 0; j < n; ++j) T0[i] += Tm.a[i][j] * u[j];
     }
     R val = 0;
-    for (int j = 0; j <= J; ++j) {
+    for (int j = 0; j <= J + 1; ++j) {
+      if (ew[j] == 0) continue;
       R acc[MAX_N];
       for (int i = 0; i < n; ++i) acc[i] = T0[i];
       Mat Aq = Mat::eye(n);
@@ -312,26 +331,27 @@ int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanCons
       const Mat Aij = mpow(Ai, j);
       R tj = 0;
       for (int l = 0; l < n; ++l) tj += Aij.a[2 * (m.ns - 1)][l] * acc[l];
-      val += m.c[j] * tj;
+      val += ew[j] * tj;
     }
     return m.G * m.G * val;
   };
   for (int i = 0; i < n; ++i) {
-    R u[MAX_N] = {0}, y0[lfd::MAX_J] = {0};
+    R u[MAX_N] = {0}, y0[lfd::MAX_J + 1] = {0};
     u[i] = 1;
     kc.cp[i] = (double)p0_of(u, y0);
   }
-  for (int q = 0; q < J; ++q) {
-    R u[MAX_N] = {0}, y0[lfd::MAX_J] = {0};
+  for (int q = 0; q <= J; ++q) {
+    R u[MAX_N] = {0}, y0[lfd::MAX_J + 1] = {0};
     y0[q] = 1;
     kc.dp[q] = (double)p0_of(u, y0);
   }
+  sc.ow = (double)ow;
   // scan matrices
   for (int i = 0; i < n; ++i) {
     R e[MAX_N] = {0};
     e[i] = 1;
-    const BlockSim bf = sim_block(m, L, e, nullptr, -1);
-    const BlockSim br = sim_block(m, L, nullptr, e, -1);
+    const BlockSim bf = sim_block(m, L, e, nullptr, -1, ow);
+    const BlockSim br = sim_block(m, L, nullptr, e, -1, ow);
     for (int r = 0; r < n; ++r) {
       sc.PhiF[r * MAX_N + i] = (double)bf.ef[r];
       sc.M[r * MAX_N + i] = (double)bf.er0[r];
@@ -341,7 +361,7 @@ int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanCons
     sc.H0[i] = (double)br.p0;
   }
   for (int q = 0; q < J; ++q) {
-    const BlockSim bi = sim_block(m, L, nullptr, nullptr, q);
+    const BlockSim bi = sim_block(m, L, nullptr, nullptr, q, ow);
     for (int r = 0; r < n; ++r) {
       sc.Kc[r * lfd::MAX_J + q] = (double)bi.ef[r];
       sc.Kc[(n + r) * lfd::MAX_J + q] = (double)bi.er0[r];
@@ -360,8 +380,11 @@ int block_constants(const Cascade &cs, int L, lfd::BlockConst &kc, lfd::ScanCons
 //   p0   : Kw[2n][k]   = G^2 sum_t hv[t] z[k+t],  z[m] = sum_j c_j hv[m-j]
 // (sum_t hv[t] s[k+t] is the all-pole cascade run backward over s), and
 //   Kx[c][p] = sum_j c_j Kw[c][p-J+j].
+// The output at offset 1 is the same backward run over z shifted by one
+// sample, so the blended output functional (weight ow) runs it over
+// (1 - ow) z[k] + ow z[k-1].
 // Same definitions as sim_block (impulse at w[k], zero states).
-int block_taps(const Cascade &cs, int L, std::vector<long double> &Kx, int &nc, int &row) {
+int block_taps(const Cascade &cs, int L, R ow, std::vector<long double> &Kx, int &nc, int &row) {
   RModel m;
   if (int e = make_rmodel(cs, m)) return e;
   const int n = 2 * m.ns, J = m.J;
@@ -385,11 +408,13 @@ int block_taps(const Cascade &cs, int L, std::vector<long double> &Kx, int &nc, 
     for (int k = 0; k < L; ++k) s[k] = hS[(size_t)k * n + i];
     backward(s, m.G, &Kw[(size_t)(n + i) * L]);
   }
+  std::vector<R> z(L);
   for (int k = 0; k < L; ++k) {
-    R z = 0;
-    for (int j = 0; j <= J && j <= k; ++j) z += m.c[j] * hv[k - j];
-    s[k] = z;
+    R acc = 0;
+    for (int j = 0; j <= J && j <= k; ++j) acc += m.c[j] * hv[k - j];
+    z[k] = acc;
   }
+  for (int k = 0; k < L; ++k) s[k] = (1.0L - ow) * z[k] + (k >= 1 ? ow * z[k - 1] : 0.0L);
   backward(s, m.G * m.G, &Kw[(size_t)(2 * n) * L]);
   Kx.assign((size_t)nc * row, 0.0L);
   for (int c = 0; c < nc; ++c)
@@ -491,12 +516,34 @@ inline int64_t floor_div(int64_t a, int64_t b) {
 inline int64_t ceil_div(int64_t a, int64_t b) { return -floor_div(-a, b); }
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Blocks per grid interval for grid spacing Rg: 1 while Rg <= SUB_L_MAX,
+// else the smallest divisor m with Rg/m <= SUB_L_MAX, preferring block
+// lengths that are multiples of 4 (one 16-B row alignment: a single tap
+// table) and never shorter than the FIR span (+1 for an off-sample grid).
+// LFD_SUBBLOCK=0 (A/B knob) keeps L = Rg; another value sets SUB_L_MAX.
+constexpr int64_t SUB_L_MAX = 504;  // Lp = 512: taps 36.9 KB + 8 run buffers = 2 groups/CU
+int64_t sub_block_step(int64_t Rg, int J, bool off_sample) {
+  int64_t lmax = SUB_L_MAX;
+  if (const char *v = std::getenv("LFD_SUBBLOCK")) {
+    lmax = std::atoll(v);
+    if (lmax <= 0) return 1;
+  }
+  if (Rg <= lmax) return 1;
+  const int64_t lmin = std::max<int64_t>(64, J + 1 + (off_sample ? 1 : 0));
+  for (int pass = 0; pass < 2; ++pass)
+    for (int64_t m = 2; Rg / m >= lmin; ++m)
+      if (Rg % m == 0 && Rg / m <= lmax && (pass == 1 || (Rg / m) % 4 == 0)) return m;
+  return 1;
+}
+
 }  // namespace
 
 struct lfd_lowpass_plan {
   int device = 0;
   int n_sec = 0, padlen = 0;
   int64_t n_ch = 0, n_t = 0, n_grid = 0, n_chunks = 0;
+  int64_t kstep = 1;  // blocks per output-grid interval
+  double ow = 0.0;    // the grid's fractional sample position
   lfd::BlockGeom bg{};
   lfd::BlockConst kc{};
   lfd::ScanConst sc{};
@@ -555,16 +602,25 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   if (n_grid < 2 || !grid_lo || !grid_w)
     return fail(LFD_EUNSUPPORTED, "block plan needs a uniform grid of >= 2 points");
   if (n_chunks < 1 || !chunks) return fail(LFD_EINVAL, "no chunks");
+  // uniform grid with one fractional position w for every point (an archive
+  // whose samples start off the output grid: t0 = 03:00:00.000372 etc.)
   const int64_t Rg = grid_lo[1] - grid_lo[0];
+  const double w0 = grid_w[0];
   for (int64_t j = 0; j < n_grid; ++j) {
-    if (grid_w[j] != 0.0)
-      return fail(LFD_EUNSUPPORTED, "grid points between samples need the general path");
+    if (!(grid_w[j] >= 0.0 && grid_w[j] < 1.0)) return fail(LFD_EINVAL, "grid weights must be in [0, 1)");
+    if (grid_w[j] != w0)
+      return fail(LFD_EUNSUPPORTED, "grid points at varying positions between samples need the general path");
     if (j > 0 && grid_lo[j] - grid_lo[j - 1] != Rg)
       return fail(LFD_EUNSUPPORTED, "non-uniform grid spacing needs the general path");
   }
   if (Rg < 2 || Rg > (int64_t)1 << 30)
     return fail(LFD_EUNSUPPORTED, "grid spacing must be in [2, 2^30] samples");
-  const int L = (int)Rg;
+  // Block length L = Rg / kstep: long grid spacings (Rg > 504: dt = 10 s at
+  // 200 Hz - 2 kHz, dt = 1 s at 2 kHz) are cut into sub-blocks of <= 504
+  // samples so that the MFMA tap table (L * 72 B) + run buffers fit two
+  // 512-thread workgroups per CU; outputs sit at every kstep-th block start.
+  const int64_t kstep = sub_block_step(Rg, 2 * n_sec, w0 != 0.0);
+  const int L = (int)(Rg / kstep);
   const int64_t base0 = ((grid_lo[0] % L) + L) % L;
 
   auto *p = new lfd_lowpass_plan();
@@ -599,10 +655,12 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     G.tail_out_pos = -1;
     G.kout0 = G.kout1 = G.kb;
     G.jout0 = 0;
+    G.kstep = kstep;
     bool any_block = false;
     for (int64_t j = ch.g0; j < ch.g1; ++j) {
       const int64_t pos = grid_lo[j];
-      if (pos < ch.s0 || pos > ch.s1) return bad(LFD_EINVAL, "output grid point outside the chunk");
+      if (pos < ch.s0 || pos > ch.s1 || (w0 != 0.0 && pos + 1 > ch.s1))
+        return bad(LFD_EINVAL, "output grid point outside the chunk");
       const int64_t kj = (pos - base0) / L;
       if (kj >= G.kb && kj < G.ke) {
         if (!any_block) {
@@ -641,14 +699,16 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   p->bg.base = base0 + kmin * L;
   p->bg.L = L;
   p->bg.nF = 2 * n + 1;
-  if (int e = block_constants(c, L, p->kc, p->sc, p->fir32)) {
+  p->kstep = kstep;
+  p->ow = w0;
+  if (int e = block_constants(c, L, (R)w0, p->kc, p->sc, p->fir32)) {
     delete p;
     return e;
   }
   if (2 * n + 1 <= 16) {
     std::vector<long double> Kx;
     int nc = 0, row = 0;
-    if (int e = block_taps(c, L, Kx, nc, row)) {
+    if (int e = block_taps(c, L, (R)w0, Kx, nc, row)) {
       delete p;
       return e;
     }
@@ -686,8 +746,11 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     const int64_t n_runs = (int64_t)p->run_ks.size();
     // K1 units: consecutive runs up to 32 blocks (fewer for narrow arrays, so
     // that >= ~4,096 wave units cover the chip)
+    // (k_block_runs_mfma holds a unit's run table one run per lane: a unit of
+    // <= 32 blocks has <= 32 runs, well inside the 64 lanes)
     int64_t unit_cap = 32;
-    if (const char *v = std::getenv("LFD_RUN_UNIT")) unit_cap = std::max(lfd::RUN_R, std::atoi(v));
+    if (const char *v = std::getenv("LFD_RUN_UNIT"))
+      unit_cap = std::min<int64_t>(32, std::max(lfd::RUN_R, std::atoi(v)));
     const int64_t unit_blocks =
         std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(unit_cap, ((n_ch + 15) / 16) * p->bg.nb / 4096));
     int acc = 0;
@@ -699,6 +762,11 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
       acc += p->run_len[r];
     }
     p->group_r0.push_back((int)n_runs);
+    for (size_t gi = 0; gi + 1 < p->group_r0.size(); ++gi)
+      if (p->group_r0[gi + 1] - p->group_r0[gi] > 64) {
+        delete p;
+        return fail(LFD_EINVAL, "internal: a K1 unit holds more than 64 runs");
+      }
     auto run_at = [&](int64_t k) {
       return (int64_t)(std::lower_bound(p->run_ks.begin(), p->run_ks.end(), k) - p->run_ks.begin());
     };

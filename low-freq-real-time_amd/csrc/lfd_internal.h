@@ -48,11 +48,16 @@ struct RCoef {
 // recurrence from zero all-pole state (true FIR history) and, in the same
 // sweep, the reverse pass's zero-state exit state through the inverse-time
 // accumulator  u <- A_r^{-1} u + B_r v_last[m]  (unscaled; G folded below).
+// The "output functional" p of a block is the zero-phase output at the
+// block's grid point lo + w: (1 - w) y[offset 0] + w y[offset 1] (linear
+// interp1d between the two samples, scipy/interpolate/_interpolate.py:457-484;
+// w = 0 on sample-aligned grids).  Every constant below that names p0 / G0 /
+// H0 is that blend.
 struct BlockConst {
   RCoef r;
   double T[MAX_N * MAX_N];   // G A_r^{L-1}: u -> e_r0
-  double cp[MAX_N];          // p0 = cp.u + dp.y0  (output at offset 0)
-  double dp[MAX_J];
+  double cp[MAX_N];          // p0 = cp.u + dp.y0[0..J]  (output functional)
+  double dp[MAX_J + 1];
 };
 
 // Constants of the per-chunk scan kernel (k_chunk_scan).
@@ -64,6 +69,7 @@ struct ScanConst {
   double G0[MAX_N];            // output(offset 0) response to S_f
   double H0[MAX_N];            // output(offset 0) response to T entering
   double Kc[(2 * MAX_N + 1) * MAX_J];  // functionals' response to w[0..J-1]
+  double ow;                   // weight of the offset-1 sample in an output (grid w)
 };
 
 struct ZiVec {
@@ -76,12 +82,13 @@ struct ChunkGeom {
   int64_t kb, ke;        // full blocks [kb, ke) inside the chunk
   int64_t head_end;      // first sample of block kb  (== s0 when no head)
   int64_t tail_begin;    // first sample after block ke-1
-  int64_t kout0, kout1;  // blocks whose offset-0 sample is an output
+  int64_t kout0, kout1;  // output blocks: kout0, kout0 + kstep, ... < kout1
   int64_t jout0;         // grid index of block kout0's output
   int64_t sf_off;        // offset (in blocks) of this chunk in the s_f scratch
   int64_t tail_out_pos, tail_out_j;  // output inside the tail (j < 0: none)
   int64_t r0, r1;        // run-mode: runs [r0, r1) tile blocks [kb, ke) (run r0 = [kb])
   int64_t sr_off;        // run-mode: offset (in runs) of this chunk in the S_in scratch
+  int64_t kstep;         // blocks per output-grid interval (sub-blocks: L = R / kstep)
 };
 
 struct BlockGeom {

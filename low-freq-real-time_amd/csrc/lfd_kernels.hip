@@ -45,6 +45,14 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // FIR-history correction masks the same samples the same way.
 __device__ __forceinline__ float finite_or_zero(float v) { return __builtin_isfinite(v) ? v : 0.0f; }
 
+// wave-uniform 64-bit value into SGPRs (VALU-computed values, e.g. 64-bit
+// divisions, otherwise make every dependent branch divergent)
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // ---------------------------------------------------------------------------
 // TDF-II cascade step, SciPy's `_sosfilt` form (full-rate path only)
 // ---------------------------------------------------------------------------
@@ -305,13 +313,13 @@ __global__ __launch_bounds__(256, LFD_K1_MINW) void k_block_functionals_lds(
         const f4v v = *reinterpret_cast<const f4v *>(rd + 4 * j);
         double yv;
         LFD_R_SAMPLE(rec, v.x, h, S, u, yv);
-        if (4 * j + 0 < J) p0y = fma(kc.dp[4 * j + 0], yv, p0y);
+        if (4 * j + 0 <= J) p0y = fma(kc.dp[4 * j + 0], yv, p0y);
         LFD_R_SAMPLE(rec, v.y, h, S, u, yv);
-        if (4 * j + 1 < J) p0y = fma(kc.dp[4 * j + 1], yv, p0y);
+        if (4 * j + 1 <= J) p0y = fma(kc.dp[4 * j + 1], yv, p0y);
         LFD_R_SAMPLE(rec, v.z, h, S, u, yv);
-        if (4 * j + 2 < J) p0y = fma(kc.dp[4 * j + 2], yv, p0y);
+        if (4 * j + 2 <= J) p0y = fma(kc.dp[4 * j + 2], yv, p0y);
         LFD_R_SAMPLE(rec, v.w, h, S, u, yv);
-        if (4 * j + 3 < J) p0y = fma(kc.dp[4 * j + 3], yv, p0y);
+        if (4 * j + 3 <= J) p0y = fma(kc.dp[4 * j + 3], yv, p0y);
       }
     }
   }
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
       buf[d] = p[(int64_t)min(nxt + d, L - 1) * s_t];
       double yv;
       LFD_R_SAMPLE(rec, v, h, S, u, yv);
-      if (gi == 0 && d < J) p0y = fma(kc.dp[d < J ? d : 0], yv, p0y);
+      if (gi * D + d <= J) p0y = fma(kc.dp[min(gi * D + d, J)], yv, p0y);
     }
   }
   const int rem = L - Gn * D;
@@ -404,7 +412,7 @@ __global__ __launch_bounds__(256) void k_block_functionals_gen(
       double yv;
       LFD_R_SAMPLE(rec, buf[d], h, S, u, yv);
       const int m = Gn * D + d;
-      if (m < J) p0y = fma(kc.dp[m < J ? m : 0], yv, p0y);
+      if (m <= J) p0y = fma(kc.dp[m <= J ? m : 0], yv, p0y);
     }
   }
   store_functionals<NS>(kc, S, u, p0y, F, k, ch, g.nb);
@@ -512,6 +520,14 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   const int E = padlen;
   const SeqR<NS> R(sc.r);
   (void)tp_len;
+  // output blocks: kout0, kout0 + kstep, ... (kstep > 1: sub-blocks)
+  const int kst = (int)G.kstep;
+  auto is_out = [&](int64_t k) {
+    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
+  };
+  auto out_j = [&](int64_t k) -> int64_t {
+    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
+  };
 
   // ---- left edge: odd extension (float32 like numpy), steady state of ext[0]
   double S[N], h[J];
@@ -644,13 +660,18 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
     for (int j = 0; j < J; ++j) qw[j] = qss;
   }
+  double y_next = 0.0;  // zero-phase output one sample after the tail output
   for (int64_t i = ntp - 1; i >= 0; --i) {
     const double q = R.rev(T, tp[i * n_thr]);
-    if (G.tail_out_j >= 0 && G.tail_begin + i == G.tail_out_pos) {
+    if (G.tail_out_j >= 0 && (G.tail_begin + i == G.tail_out_pos || G.tail_begin + i == G.tail_out_pos + 1)) {
       double acc = q;  // c[0] = 1
 #pragma unroll
       for (int j = 1; j <= J; ++j) acc = fma(sc.r.c64[j], qw[j - 1], acc);
-      y[ch * ys_ch + G.tail_out_j * ys_t] = (float)(sc.r.G * acc);
+      acc *= sc.r.G;
+      if (G.tail_begin + i == G.tail_out_pos + 1)
+        y_next = acc;
+      else  // interp1d between the two samples (w = sc.ow)
+        y[ch * ys_ch + G.tail_out_j * ys_t] = (float)fma(sc.ow, y_next - acc, acc);
     }
 #pragma unroll
     for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
@@ -690,7 +711,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         o.er[i] = agb[(r * 8 + 4 + i) * 16];
       }
 #pragma unroll
-      for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = pp < o.len ? y0b[(o.ks + pp) * 16] : 0.0;
+      for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = is_out(o.ks + pp) && pp < o.len ? y0b[(o.ks + pp) * 16] : 0.0;
     };
     // ring of SCAN_DB runs (r-1 .. r-SCAN_DB in flight while run r is applied)
     constexpr int DB = SCAN_DB;
@@ -724,7 +745,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       for (int pp = 0; pp < RUN_R; ++pp) {
         const int64_t k = ks + pp;
         ov[pp] = 0.f;
-        if (pp >= len || k < G.kout0 || k >= G.kout1) continue;
+        if (pp >= len || !is_out(k)) continue;
         double acc = cur.y0[pp] + (k == G.kb ? corr[2 * N] : 0.0);
         const double *A = rc.A[len][pp];
         const double *B = rc.B[len - 1 - pp];
@@ -734,7 +755,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
           acc = fma(B[j], T[j], acc);
         }
         ov[pp] = (float)acc;
-        if (!coal) y[ch * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t] = ov[pp];
+        if (!coal) y[ch * ys_ch + out_j(k) * ys_t] = ov[pp];
       }
       if (coal) {
         float(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
@@ -745,8 +766,8 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int e = lane & 7;
         const int64_t k = ks + e;
-        const bool ok = e < len && k >= G.kout0 && k < G.kout1;
-        float *yb = y + ch_w * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t;
+        const bool ok = e < len && is_out(k);
+        float *yb = y + ch_w * ys_ch + (ok ? out_j(k) : 0) * ys_t;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
           const int row = m * 8 + (lane >> 3);
@@ -781,14 +802,14 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     double sfv[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) sfv[i] = sf[i * SF_ISTRIDE];
-    if (k >= G.kout0 && k < G.kout1) {
+    if (is_out(k)) {
       double acc = f[2 * N * F_CSTRIDE] + (first ? corr[2 * N] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         acc = fma(sc.H0[j], T[j], acc);
         acc = fma(sc.G0[j], sfv[j], acc);
       }
-      y[ch * ys_ch + (G.jout0 + (k - G.kout0)) * ys_t] = (float)acc;
+      y[ch * ys_ch + out_j(k) * ys_t] = (float)acc;
     }
     double nr[N];
 #pragma unroll
@@ -948,26 +969,223 @@ __global__ __launch_bounds__(256) void k_rolling_tc(
   }
 }
 
-// generic strides (e.g. channel-contiguous): one thread per (window, channel)
-// with channel fastest, so a wave reads 64 consecutive channels per sample.
-__global__ __launch_bounds__(256) void k_rolling_generic(
+// Running window sum for step < window (every sample read once from HBM; the
+// sample leaving the window, x[t - W], is re-read W positions later from L2):
+//   Wsum(t) = Wsum(t-1) + m(x[t]) - m(x[t-W]),  m(v) = v if finite else 0,
+// float64, with a count of the non-finite samples in the window carried the
+// same way.  A window holding a null is summed directly over its raw values
+// (NaN / inf exactly as numpy's mean of that window), the rest are
+// Wsum / W.  Windows with kS < W - 1 are NaN (pandas right-aligned rolling).
+__device__ __forceinline__ float window_direct(const float *__restrict__ row, int64_t e, int64_t W,
+                                               int64_t s_t) {
+  double acc = 0.0;
+  for (int64_t m = e - W + 1; m <= e; ++m) acc += (double)row[m * s_t];
+  return (float)(acc / (double)W);
+}
+
+// Generic strides (the (time, distance) layout: s_ch = 1): one thread per
+// channel and segment of outputs, channels adjacent in a wave so each sample
+// row is one coalesced 256-B read; grid-stride over (segment, channel group)
+// units, so any n_ch * n_out fits the launch.  S >= W: each output's window
+// is summed directly (no sample is read twice); S < W: running sum.
+__global__ __launch_bounds__(256) void k_rolling_cols(
     const float *__restrict__ x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     int64_t s_t, int64_t W, int64_t S, float *__restrict__ y, int64_t ys_ch,
-    int64_t ys_t) {
+    int64_t ys_t, int64_t seg_out) {
   const int64_t n_out = (n_t + S - 1) / S;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_ch * n_out) return;
-  const int64_t ch = i % n_ch, k = i / n_ch;
-  const int64_t e = k * S;
-  float *out = y + ch * ys_ch + k * ys_t;
-  if (e < W - 1) {
-    *out = __builtin_nanf("");
-    return;
+  const int64_t n_seg = (n_out + seg_out - 1) / seg_out;
+  const int64_t n_units = n_seg * n_ch;
+  const float nanv = __builtin_nanf("");
+  const int64_t k_first = (W - 1 + S - 1) / S;  // first output with a full window
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ch = u % n_ch, seg = u / n_ch;
+    const int64_t k0 = seg * seg_out;
+    const int64_t k1 = min(n_out, k0 + seg_out);
+    const float *row = x + ch * s_ch;
+    float *yo = y + ch * ys_ch;
+    int64_t k = k0;
+    for (; k < k1 && k < k_first; ++k) yo[k * ys_t] = nanv;
+    if (k >= k1) continue;
+    if (S >= W) {
+      for (; k < k1; ++k) {
+        const int64_t e = k * S;
+        double acc = 0.0;
+        int bad = 0;
+        for (int64_t m = e - W + 1; m <= e; ++m) {
+          const float v = row[m * s_t];
+          bad |= !__builtin_isfinite(v);
+          acc += (double)v;
+        }
+        yo[k * ys_t] = bad ? window_direct(row, e, W, s_t) : (float)(acc / (double)W);
+      }
+      continue;
+    }
+    // running sum from the window ending at k*S
+    int64_t e = k * S;
+    double sum = 0.0;
+    int64_t cnt = 0;
+    for (int64_t m = e - W + 1; m <= e; ++m) {
+      const float v = row[m * s_t];
+      const bool f = __builtin_isfinite(v);
+      sum += f ? (double)v : 0.0;
+      cnt += !f;
+    }
+    yo[k * ys_t] = cnt ? window_direct(row, e, W, s_t) : (float)(sum / (double)W);
+    for (++k; k < k1; ++k) {
+      const int64_t e1 = k * S;
+      for (int64_t t = e + 1; t <= e1; ++t) {
+        const float vi = row[t * s_t], vo = row[(t - W) * s_t];
+        const bool fi = __builtin_isfinite(vi), fo = __builtin_isfinite(vo);
+        sum += (fi ? (double)vi : 0.0) - (fo ? (double)vo : 0.0);
+        cnt += (int64_t)!fi - (int64_t)!fo;
+      }
+      e = e1;
+      yo[k * ys_t] = cnt ? window_direct(row, e, W, s_t) : (float)(sum / (double)W);
+    }
   }
-  const float *p = x + ch * s_ch + (e - W + 1) * s_t;
-  double acc = 0.0;
-  for (int64_t m = 0; m < W; ++m) acc += (double)p[m * s_t];
-  *out = (float)(acc / (double)W);
+}
+
+// Time-contiguous rows, step < window: one wave per (channel, segment of
+// outputs).  A wave step covers 256 consecutive positions (4 per lane,
+// float4 loads when the row and W allow): per position d = m(x[t]) -
+// m(x[t-W]) in float64, a lane-local prefix, a wave exclusive scan of the
+// lane totals (__shfl_up) and the carried window sum give Wsum at all 256
+// positions; outputs are the positions t = kS.  The segment's first window is
+// summed directly (a halo of W samples per segment: segments are >= 4W).
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rolling_scan_tc(
+    const float *__restrict__ x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t W,
+    int64_t S, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int64_t seg_out, bool vec_out) {
+  const int64_t n_out = (n_t + S - 1) / S;
+  const int64_t n_seg = (n_out + seg_out - 1) / seg_out;
+  const int64_t n_units = n_seg * n_ch;
+  const int lane = threadIdx.x & 63;
+  const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const float nanv = __builtin_nanf("");
+  const int64_t k_first = (W - 1 + S - 1) / S;
+  const double inv_w = 1.0 / (double)W;
+  for (int64_t u = uniform64(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); u < n_units;
+       u += n_waves) {
+    const int64_t useg = u % n_seg;
+    const int64_t ch = u / n_seg;
+    const int64_t k0 = useg * seg_out;
+    const int64_t k1 = min(n_out, k0 + seg_out);
+    const float *row = x + ch * s_ch;
+    float *yo = y + ch * ys_ch;
+    int64_t ka = k0 > k_first ? k0 : k_first;
+    for (int64_t k = k0 + lane; k < k1 && k < k_first; k += 64) yo[k * ys_t] = nanv;
+    if (ka >= k1) continue;
+    const int64_t p0 = ka * S, p1 = (k1 - 1) * S;  // output positions [p0, p1]
+    // Wsum(p0 - 1): window [p0 - W, p0 - 1] (x[-1] = 0 when p0 = W - 1)
+    double carry = 0.0;
+    int64_t ccnt = 0;
+    {
+      double acc = 0.0;
+      int cnt = 0;
+      for (int64_t m = p0 - W + lane; m < p0; m += 64) {
+        if (m < 0) continue;
+        const float v = row[m];
+        const bool f = __builtin_isfinite(v);
+        acc += f ? (double)v : 0.0;
+        cnt += !f;
+      }
+      carry = wave_sum(acc);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+      ccnt = cnt;
+    }
+    // tiles of 256 positions from the 4-aligned position at or below p0
+    const int64_t tb0 = VEC ? (p0 & ~(int64_t)3) : p0;
+    const int64_t step_mod = 256 % S;
+    int64_t ph = (tb0 + 4 * lane) % S;  // phase of this lane's first position
+    for (int64_t tb = tb0; tb <= p1; tb += 256) {
+      const int64_t t = tb + 4 * lane;
+      float xi[4], xo[4];
+      const bool full = tb + 256 <= n_t && tb - W >= 0;
+      if (VEC && full) {
+        const f4v a = *reinterpret_cast<const f4v *>(row + t);
+        xi[0] = a.x, xi[1] = a.y, xi[2] = a.z, xi[3] = a.w;
+        if ((W & 3) == 0) {
+          const f4v b = *reinterpret_cast<const f4v *>(row + t - W);
+          xo[0] = b.x, xo[1] = b.y, xo[2] = b.z, xo[3] = b.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xo[e] = row[t + e - W];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t ti = t + e;
+          xi[e] = ti < n_t ? row[ti] : 0.0f;
+          xo[e] = (ti - W >= 0 && ti < n_t) ? row[ti - W] : 0.0f;
+        }
+      }
+      double d[4];
+      int c[4];
+      bool anynf = false;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t ti = t + e;
+        const bool in = ti >= p0 && ti <= p1;
+        const bool fi = __builtin_isfinite(xi[e]), fo = __builtin_isfinite(xo[e]);
+        d[e] = in ? (fi ? (double)xi[e] : 0.0) - (fo ? (double)xo[e] : 0.0) : 0.0;
+        c[e] = in ? (int)!fi - (int)!fo : 0;
+        anynf |= in && (!fi || !fo);
+      }
+      // lane-local inclusive prefix, then the wave's exclusive scan
+      d[1] += d[0];
+      d[2] += d[1];
+      d[3] += d[2];
+      double v = d[3];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double w_ = __shfl_up(v, o, 64);
+        if (lane >= o) v += w_;
+      }
+      const double excl = carry + (v - d[3]);
+      const double tot = __shfl(v, 63, 64);
+      // non-finite counts only when this step or the carried window has one
+      int cc[4] = {0, 0, 0, 0};
+      const bool need_cnt = __any(anynf) || ccnt != 0;
+      if (need_cnt) {
+        c[1] += c[0];
+        c[2] += c[1];
+        c[3] += c[2];
+        int vc = c[3];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int w_ = __shfl_up(vc, o, 64);
+          if (lane >= o) vc += w_;
+        }
+        const int64_t ex = ccnt + (vc - c[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cc[e] = (int)(ex + c[e]);
+        ccnt += __shfl(vc, 63, 64);
+      }
+      float o4[4];
+      bool is_out[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t ti = t + e;
+        int64_t pe = ph + e;
+        while (pe >= S) pe -= S;  // at most 3 subtractions (ph < S, e < 4)
+        is_out[e] = ti >= p0 && ti <= p1 && pe == 0;
+        o4[e] = (float)((excl + d[e]) * inv_w);
+        if (is_out[e] && cc[e] != 0) o4[e] = window_direct(row, ti, W, 1);
+      }
+      if (S == 1 && vec_out && is_out[0] && is_out[3]) {
+        *reinterpret_cast<f4v *>(yo + t) = f4v{o4[0], o4[1], o4[2], o4[3]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (is_out[e]) yo[((t + e) / S) * ys_t] = o4[e];
+      }
+      carry += tot;
+      ph += step_mod;
+      ph = ph >= S ? ph - S : ph;
+    }
+  }
 }
 
 
@@ -1053,14 +1271,6 @@ __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, doubl
 // 18.5 vs 13.1 ms — the 64-B row pieces of consecutive iterations no longer
 // meet in L2)
 __device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
-
-// wave-uniform 64-bit value into SGPRs (VALU-computed values, e.g. 64-bit
-// divisions, otherwise make every dependent branch divergent)
-__device__ __forceinline__ int64_t uniform64(int64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 // MODE 0: production.  Diagnostic modes (timing experiments only, results
 // invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
@@ -1574,7 +1784,10 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   if (pf == 2 && nt == 384) return run_k1<2, 0, 384>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 2 && nt == 512) return run_k1<2, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (pf == 1 && nt == 1024) return run_k1<1, 0, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  return run_k1<1, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  if (pf == 1 && nt == 512) return run_k1<1, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  // an A/B knob combination without an instantiation: refuse rather than run
+  // (and let a record label) a configuration that never ran
+  return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------
@@ -1761,16 +1974,40 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                float *y, int64_t ys_ch, int64_t ys_t,
                                hipStream_t st) {
   const int64_t n_out = (n_t + S - 1) / S;
-  if (s_t == 1) {
+  const int64_t cap = 256 * 32;  // workgroups of the grid-stride launches
+  if (s_t == 1 && S >= W) {
+    // windows do not overlap: each is summed directly by one wave
     const int64_t waves = n_ch * n_out;
     int64_t blocks = (waves + 3) / 4;
-    if (blocks > 256 * 32) blocks = 256 * 32;
+    if (blocks > cap) blocks = cap;
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     k_rolling_tc<<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y,
                                                    ys_ch, ys_t, vec);
+  } else if (s_t == 1) {
+    // overlapping windows: running sum over segments of >= max(32768, 4W)
+    // positions (halo W per segment), fewer when that leaves the chip idle
+    int64_t seg_pos = std::max<int64_t>(32768, 4 * W);
+    while (seg_pos > std::max<int64_t>(4096, 4 * W) && n_ch * ((n_t + seg_pos - 1) / seg_pos) < 16384)
+      seg_pos /= 2;
+    const int64_t seg_out = std::max<int64_t>(1, seg_pos / S);
+    const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
+    int64_t blocks = (units + 3) / 4;
+    if (blocks > cap) blocks = cap;
+    const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
+    const bool vec_out = vec && ys_t == 1 && ys_ch % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+    if (vec)
+      k_rolling_scan_tc<true><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y, ys_ch, ys_t,
+                                                                seg_out, vec_out);
+    else
+      k_rolling_scan_tc<false><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y, ys_ch, ys_t,
+                                                                 seg_out, false);
   } else {
-    k_rolling_generic<<<nblk(n_ch * n_out, 256), 256, 0, st>>>(
-        x, n_ch, n_t, s_ch, s_t, W, S, y, ys_ch, ys_t);
+    const int64_t seg_out = S >= W ? 64 : std::max<int64_t>(1, std::max<int64_t>(4096, 4 * W) / S);
+    const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
+    int64_t blocks = (units + 255) / 256;
+    if (blocks > cap) blocks = cap;
+    k_rolling_cols<<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, s_t, W, S, y, ys_ch, ys_t,
+                                                    seg_out);
   }
   return hipGetLastError();
 }

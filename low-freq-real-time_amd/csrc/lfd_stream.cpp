@@ -325,7 +325,9 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
     const int64_t rel = t_grid0 + (j0 + j) * s->out_ns - s->t_col0;
     lo[j] = floor_div(rel, dts);
     w[j] = (double)(rel - lo[j] * dts) / (double)dts;
-    aligned = aligned && w[j] == 0.0 && (j == 0 || lo[j] - lo[j - 1] == lo[1] - lo[0]);
+    // uniform grid, one fractional position for every point (the block plan's
+    // domain; w != 0 when the archive's samples start off the output grid)
+    aligned = aligned && w[j] == w[0] && (j == 0 || lo[j] - lo[j - 1] == lo[1] - lo[0]);
   }
   int64_t w0 = INT64_MAX, w1 = INT64_MIN;
   for (auto &c : cs) w0 = std::min(w0, c[0]), w1 = std::max(w1, c[1]);
@@ -344,7 +346,9 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
   const float *x = s->arena[s->cur] + x0;
   lfd_lowpass_plan *plan = nullptr;
   if (aligned && n_out >= 2) {
-    std::vector<int64_t> key = {nt, lo[0] - x0, lo[1] - lo[0], n_out};
+    int64_t wbits = 0;
+    std::memcpy(&wbits, &w[0], sizeof(wbits));
+    std::vector<int64_t> key = {nt, lo[0] - x0, lo[1] - lo[0], n_out, wbits};
     for (auto &c : cs) key.insert(key.end(), {c[0] - x0, c[1] - x0, c[2] - j0, c[3] - j0});
     auto it = s->plans.find(key);
     if (it != s->plans.end()) {

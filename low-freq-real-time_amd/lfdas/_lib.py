@@ -31,14 +31,14 @@ _RCOEF = np.dtype([("na1", "f8", MAX_SEC), ("na2", "f8", MAX_SEC), ("nia2", "f8"
                    ("nra", "f8", MAX_SEC), ("dcg", "f8", MAX_SEC), ("c64", "f8", MAX_J + 1),
                    ("c32", "f4", MAX_J + 1), ("G", "f8"), ("csum", "f8")], align=True)
 BLOCK_CONST_DTYPE = np.dtype([("r", _RCOEF), ("T", "f8", (MAX_N, MAX_N)), ("cp", "f8", MAX_N),
-                              ("dp", "f8", MAX_J)], align=True)
+                              ("dp", "f8", MAX_J + 1)], align=True)
 SCAN_CONST_DTYPE = np.dtype([("r", _RCOEF), ("PhiF", "f8", (MAX_N, MAX_N)),
                              ("PhiR", "f8", (MAX_N, MAX_N)), ("M", "f8", (MAX_N, MAX_N)),
                              ("G0", "f8", MAX_N), ("H0", "f8", MAX_N),
-                             ("Kc", "f8", (2 * MAX_N + 1, MAX_J))], align=True)
+                             ("Kc", "f8", (2 * MAX_N + 1, MAX_J)), ("ow", "f8")], align=True)
 CHUNK_GEOM_DTYPE = np.dtype([(n, "i8") for n in (
     "s0", "s1", "kb", "ke", "head_end", "tail_begin", "kout0", "kout1", "jout0",
-    "sf_off", "tail_out_pos", "tail_out_j", "r0", "r1", "sr_off")])
+    "sf_off", "tail_out_pos", "tail_out_j", "r0", "r1", "sr_off", "kstep")])
 RUN_R = 8  # lfd::RUN_R
 RUN_CONST_DTYPE = np.dtype([("PhiFp", "f8", (RUN_R + 1, 16)), ("PhiRp", "f8", (RUN_R + 1, 16)),
                             ("C", "f8", (RUN_R + 1, 16)), ("A", "f8", (RUN_R + 1, RUN_R, 4)),

@@ -7,8 +7,8 @@ them back (lf_das.py:214-217).
   The layout is restated from DASCore's public writer; DASCore/pytables are
   not installed, so byte-level compatibility with DASCore's reader is
   unpinned.
-* ``npz``: the NPZ stand-in (also used when liblfdas_h5.so is absent), under
-  the same file names.
+* ``npz``: the NPZ stand-in, written only when asked for by name (a
+  ``dasdae`` write without liblfdas_h5.so raises instead of falling back).
 
 Readers sniff the file signature, so a folder may mix both."""
 from __future__ import annotations
@@ -46,7 +46,7 @@ def h5_available() -> bool:
 
 
 def _h5():
-    """liblfdas_h5.so, or None (then files fall back to the NPZ stand-in)."""
+    """liblfdas_h5.so, or None (``dasdae`` writes then raise)."""
     global _h5lib
     if _h5lib is None:
         path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblfdas_h5.so")
@@ -218,9 +218,13 @@ def _attrs_from_json(d):
 
 
 def write_patch(patch: Patch, path: str, file_format: str = "dasdae"):
-    """``dasdae``: HDF5 (DASDAE layout) when liblfdas_h5.so is available,
-    else the NPZ stand-in; ``npz``: the stand-in."""
-    if str(file_format).lower() == "dasdae" and _h5() is not None:
+    """``dasdae``: HDF5 (DASDAE layout) through liblfdas_h5.so — raises
+    ``OSError`` when that library is missing rather than writing other bytes
+    under a DASDAE file name; ``npz``: the NPZ stand-in (explicit only)."""
+    if str(file_format).lower() == "dasdae":
+        if _h5() is None:
+            raise OSError("DASDAE output needs liblfdas_h5.so (build it with "
+                          "__graft_entry__.build()); write format 'npz' explicitly for the stand-in")
         _write_h5(patch, path)
         return
     coords = patch.coords.coord_map

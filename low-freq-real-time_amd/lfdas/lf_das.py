@@ -7,6 +7,28 @@ Reference line map: ``_check_merge`` lf_das.py:16-20, ``_get_timestr`` /
 ``_get_filename`` :23-31, ``_down_sample_processing`` :34-44,
 ``get_edge_effect_time`` :47-87, ``get_patch_time`` :90-107,
 ``waterfall_plot`` :110-178, ``LFProc`` :182-295.
+
+The helper functions and LFProc's parameter/housekeeping methods restate the
+reference's own code (their exact names, messages and arithmetic are the
+drop-in specification), so that reference's notice applies to them:
+
+    MIT License — Copyright (c) 2023 DASDAE
+
+    Permission is hereby granted, free of charge, to any person obtaining a
+    copy of this software and associated documentation files (the
+    "Software"), to deal in the Software without restriction, including
+    without limitation the rights to use, copy, modify, merge, publish,
+    distribute, sublicense, and/or sell copies of the Software, and to permit
+    persons to whom the Software is furnished to do so, subject to the
+    following conditions: The above copyright notice and this permission
+    notice shall be included in all copies or substantial portions of the
+    Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY
+    KIND, EXPRESS OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF
+    MERCHANTABILITY, FITNESS FOR A PARTICULAR PURPOSE AND NONINFRINGEMENT. IN
+    NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR ANY CLAIM,
+    DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR
+    OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE
+    USE OR OTHER DEALINGS IN THE SOFTWARE.
 """
 from __future__ import annotations
 

@@ -45,7 +45,7 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
             H[j, :, k] = x[:, t] if t >= 0 else 0.0
     S = np.zeros((n, n_ch, nb))
     u = np.zeros((n, n_ch, nb))
-    y0 = np.zeros((J, n_ch, nb))
+    y0 = np.zeros((J + 1, n_ch, nb))
     for m in range(L):
         xm = X[:, :, m]
         if fir32:
@@ -63,7 +63,7 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
             S[2 * s + 1] = S[2 * s].copy()
             S[2 * s] = vn
             v = vn
-        if m < J:
+        if m <= J:
             y0[m] = v
         t = u.copy()
         for s in range(ns):
@@ -72,7 +72,7 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
             u[2 * s + 1] = nra[s] * t[2 * s + 1] + nia2[s] * d
     ef = S
     er0 = np.einsum("ij,jab->iab", bc["T"][:n, :n], u)
-    p0 = np.einsum("j,jab->ab", bc["cp"][:n], u) + np.einsum("m,mab->ab", bc["dp"][:J], y0)
+    p0 = np.einsum("j,jab->ab", bc["cp"][:n], u) + np.einsum("m,mab->ab", bc["dp"][:J + 1], y0)
     if k1 in ("taps", "runs"):
         F = block_functionals_taps(plan, x)
         ef, er0, p0 = F[:n], F[n:2 * n], F[2 * n]
@@ -165,27 +165,39 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
             tp.append(fwd(Sf, h, (2 * xr - x[:, s1 - 1 - i]).astype(np.float32).astype(np.float64)))
         T, qss = steady(tp[-1], False)
         qw = [qss] * J
+        y_next = 0.0
         for i in range(len(tp) - 1, -1, -1):
             q = rev(T, tp[i])
-            if Gc["tail_out_j"] >= 0 and tb + i == Gc["tail_out_pos"]:
-                y[:, Gc["tail_out_j"]] = G * (q + sum(c64[j] * qw[j - 1] for j in range(1, J + 1)))
+            if Gc["tail_out_j"] >= 0 and tb + i in (Gc["tail_out_pos"], Gc["tail_out_pos"] + 1):
+                yv = G * (q + sum(c64[j] * qw[j - 1] for j in range(1, J + 1)))
+                if tb + i == Gc["tail_out_pos"] + 1:
+                    y_next = yv
+                else:  # interp1d between the two samples (the grid's w)
+                    y[:, Gc["tail_out_j"]] = yv + float(sc["ow"]) * (y_next - yv)
             qw = [q] + qw[:-1]
+        kst = int(Gc["kstep"])
+
+        def is_out(k):
+            return Gc["kout0"] <= k < Gc["kout1"] and (k - Gc["kout0"]) % kst == 0
+
+        def out_j(k):
+            return Gc["jout0"] + (k - Gc["kout0"]) // kst
         if k1 == "runs":
             for ri in range(r1 - 1, r0 - 1, -1):
                 sin, ks, ln = SFs[ri], int(run_ks[ri]), int(run_len[ri])
                 for p in range(ln):
                     k = ks + p
-                    if Gc["kout0"] <= k < Gc["kout1"]:
+                    if is_out(k):
                         yk = Y0[:, k] + (corr[2 * n] if k == kb else 0)
                         yk = yk + rc["A"][ln][p] @ sin + rc["B"][ln - 1 - p] @ T
-                        y[:, Gc["jout0"] + k - Gc["kout0"]] = yk
+                        y[:, out_j(k)] = yk
                 T = (rc["PhiRp"][ln].reshape(4, 4) @ T + AG[ri, 4:] + (corr[n:2 * n] if ri == r0 else 0)
                      + rc["C"][ln].reshape(4, 4) @ sin)
             continue
         for k in range(ke - 1, kb - 1, -1):
             sf = SFs[k]
-            if Gc["kout0"] <= k < Gc["kout1"]:
+            if is_out(k):
                 pk = p0[:, k] + (corr[2 * n] if k == kb else 0)
-                y[:, Gc["jout0"] + k - Gc["kout0"]] = pk + H0 @ T + G0 @ sf
+                y[:, out_j(k)] = pk + H0 @ T + G0 @ sf
             T = PhiR @ T + er0[:, :, k] + (corr[n:2 * n] if k == kb else 0) + M @ sf
     return y

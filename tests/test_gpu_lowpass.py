@@ -18,15 +18,20 @@ def _relrms(a, b):
     return float(np.sqrt(np.sum((a - b) ** 2) / np.sum(b ** 2)))
 
 
-def _run(x, fs, dt_out, P, B, layout="tc"):
+def _run(x, fs, dt_out, P, B, layout="tc", off_ns=0):
+    """off_ns > 0: the samples start off_ns after the whole second on which
+    the output grid starts (a real archive's bgtime; every grid point then
+    lies the same fraction w of a sample past a sample)."""
     import torch
     from lfdas.plan import LowpassPlan
     n_ch, n = x.shape
     dt_ns = int(round(1e9 / fs))
-    tg = S.time_grid(T0, T0 + n * dt_ns, dt_out)
+    t0 = T0 + off_ns
+    t1 = T0 if off_ns == 0 else T0 + 1_000_000_000
+    tg = S.time_grid(t1, t0 + n * dt_ns, dt_out)
     sched = S.lfproc_chunks(len(tg), P, B)
-    lo, w = S.grid_positions(T0, dt_ns, tg)
-    chunks = [(*S.select_range(T0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    lo, w = S.grid_positions(t0, dt_ns, tg)
+    chunks = [(*S.select_range(t0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
     sos = oracle.butter_sos(4, (1 / dt_out / 2 * 0.9) / (fs / 2))
     plan = LowpassPlan(sos, n_ch, n, lo, w, chunks)
     if layout == "tc":
@@ -38,7 +43,8 @@ def _run(x, fs, dt_out, P, B, layout="tc"):
     torch.cuda.synchronize()
     _run.last_kernel = plan.last_kernel()
     y = yd.cpu().numpy()
-    ref = oracle.lfproc_process(x, T0, dt_ns, tg[0], tg[-1] + 1, dt_out, P, B)
+    ref = oracle.lfproc_process(x, t0, dt_ns, tg[0], tg[-1] + 1, dt_out, P, B)
+    _run.w = w
     return y, ref, sched
 
 
@@ -46,17 +52,18 @@ def _run(x, fs, dt_out, P, B, layout="tc"):
 @pytest.mark.parametrize("cfg", [
     (250.0, 0.2, 40, 6, 24, 24.0),     # cfg1 geometry (R = 50)
     (500.0, 1.0, 600, 7, 16, 1500.0),  # cfg3 parameters (R = 500, Wn = 1.8e-3)
-    (200.0, 10.0, 100, 7, 8, 3000.0),  # cfg5 parameters (R = 2000, Wn = 4.5e-4)
+    (200.0, 10.0, 100, 7, 8, 3000.0),  # cfg5 parameters (R = 2000 = 4 sub-blocks, Wn = 4.5e-4)
     (1000.0, 1.0, 30, 3, 70, 100.0),   # ragged channel count, short chunks
 ])
-@pytest.mark.parametrize("dc", [0.0, 1000.0])
-def test_lfproc_parity(cfg, dc, layout):
+@pytest.mark.parametrize("dc,off_ns", [(0.0, 0), (1000.0, 0), (0.0, 370_000), (0.0, 1_900_000)])
+def test_lfproc_parity(cfg, dc, layout, off_ns):
     fs, dt_out, P, B, n_ch, dur = cfg
     n = int(dur * fs)
     rng = np.random.default_rng(11)
     t = np.arange(n) / fs
     x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.01 * t) + dc).astype(np.float32)
-    y, ref, sched = _run(x, fs, dt_out, P, B, layout)
+    y, ref, sched = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
+    assert np.all(_run.w == _run.w[0]) and (_run.w[0] != 0) == (off_ns % int(round(1e9 / fs)) != 0)
     produced = np.zeros(y.shape[1], bool)
     num = den = 0.0
     for (tt, r), (a, b, oa, ob) in zip(ref, sched):
@@ -69,8 +76,9 @@ def test_lfproc_parity(cfg, dc, layout):
     # contiguous rows run the fp64-MFMA block taps; strided rows the recurrence;
     # both fold into runs (in registers where the MFMA kernel's LDS fits the
     # run buffers, else by the separate fold kernel: L = 2000, recurrence)
+    # (off-sample grids stay on the block plan: the blended output functional)
     if layout == "tc":
-        assert _run.last_kernel == ("mfma_fold" if fs * dt_out == 2000 else "mfma_runs")
+        assert _run.last_kernel == "mfma_runs"
     else:
         assert _run.last_kernel == "recurrence_fold"
 
@@ -89,7 +97,7 @@ def _plan_cfg(fs, dt_out, P, B, n_ch, n):
 @pytest.mark.parametrize("cfg", [
     (250.0, 0.2, 40, 6, 37, 6000),      # L = 50: four row-shift tap tables
     (500.0, 1.0, 600, 7, 33, 750_000),  # L = 500
-    (200.0, 10.0, 100, 7, 5, 600_000),  # L = 2000: 147 KB of taps, 1024-thread workgroups
+    (200.0, 10.0, 100, 7, 5, 600_000),  # R = 2000: 4 sub-blocks of 500
     (1000.0, 0.5, 40, 4, 18, 100_003),  # L = 500, odd n_t (channel stride % 4 != 0 -> recurrence)
 ])
 def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
@@ -115,9 +123,7 @@ def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
     aligned = n % 4 == 0
-    L = int(fs * dt_out)
-    assert out["default"][1] == (("mfma_runs" if L != 2000 else "mfma_fold") if aligned
-                                 else "recurrence_fold")
+    assert out["default"][1] == ("mfma_runs" if aligned else "recurrence_fold")
     assert out["noruns"][1] == ("mfma" if aligned else "recurrence")
     assert out["rec"][1] == "recurrence"
     assert out["recfold"][1] == "recurrence_fold"
@@ -159,6 +165,81 @@ def test_cfg1_random_das():
     y, ref, sched = _run(x, 250.0, 0.2, 40, 6)
     for (tt, r), (a, b, oa, ob) in zip(ref, sched):
         assert _relrms(y[:, oa:ob], r) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [
+    (1000.0, 10.0, 30, 6, 8, 1200.0),   # the batch notebook's d_t = 10 s at 1 kHz: R = 10,000
+    (2000.0, 10.0, 30, 6, 5, 900.0),    # ... at 2 kHz: R = 20,000
+    (2000.0, 1.0, 125, 7, 12, 400.0),   # cfg4 parameters: R = 2000
+])
+@pytest.mark.parametrize("off_ns", [0, 370_000])
+def test_long_grid_spacing_runs_mfma(cfg, off_ns):
+    """Grid spacings far beyond one LDS tap table run as sub-blocks of <= 504
+    samples (outputs at every kstep-th block start) on the MFMA run kernel."""
+    fs, dt_out, P, B, n_ch, dur = cfg
+    n = int(dur * fs)
+    rng = np.random.default_rng(17)
+    t = np.arange(n) / fs
+    x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.004 * t) + 20.0).astype(np.float32)
+    y, ref, sched = _run(x, fs, dt_out, P, B, "tc", off_ns=off_ns)
+    assert _run.last_kernel == "mfma_runs"
+    num = den = 0.0
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        assert r.shape == (n_ch, ob - oa)
+        num += float(np.sum((y[:, oa:ob] - r) ** 2))
+        den += float(np.sum(r ** 2))
+    assert (num / den) ** 0.5 < 1e-4
+
+
+@pytest.mark.parametrize("W,S_", [(1000, 1), (1000, 250), (1000, 1000), (1000, 3), (999, 7), (64, 1)])
+def test_rolling_mean_window_step(W, S_):
+    """Overlapping windows (step < window) run the running-sum scan kernel
+    (every sample read once); step >= window sums each window directly."""
+    import torch
+    from lfdas.plan import rolling_mean_device
+    rng = np.random.default_rng(W + S_)
+    n_ch, n = 5, 12_345
+    x = (rng.standard_normal((n_ch, n)) + 3.0).astype(np.float32)
+    ref = oracle.rolling_mean(x, W, S_)
+    for layout in ("tc", "cc", "tc_unaligned"):
+        if layout == "tc":
+            xd = torch.from_numpy(x).cuda()
+        elif layout == "cc":
+            xd = torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()
+        else:
+            full = torch.from_numpy(np.concatenate([np.zeros((n_ch, 1), np.float32), x], 1)).cuda()
+            xd = full[:, 1:]
+        y = rolling_mean_device(xd, W, S_).cpu().numpy()
+        assert y.shape == ref.shape
+        m = ~np.isnan(ref)
+        assert np.array_equal(np.isnan(y), ~m), layout
+        assert _relrms(y[m], ref[m]) < 1e-6, layout
+
+
+def test_rolling_mean_overlapping_nulls():
+    """step < window: a NaN / inf sample turns exactly the windows holding it
+    into NaN / inf (the running sum carries a count of nulls), the rest stay
+    exact, also right after the null leaves the window."""
+    import torch
+    from lfdas.plan import rolling_mean_device
+    rng = np.random.default_rng(8)
+    n_ch, n, W, S_ = 5, 20_000, 1000, 1
+    x = (rng.standard_normal((n_ch, n)) + 0.5).astype(np.float32)
+    x[0, 2999] = np.nan
+    x[1, 5000] = np.inf
+    x[2, 7001] = -np.inf
+    x[2, 7002] = np.inf    # +inf and -inf in one window: NaN
+    x[3, 0] = np.nan       # inside the leading NaN windows and the first full one
+    x[4, n - 1] = np.nan   # last window only
+    ref = oracle.rolling_mean(x, W, S_)
+    for layout in ("tc", "cc"):
+        xd = torch.from_numpy(x).cuda() if layout == "tc" else torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()
+        y = rolling_mean_device(xd, W, S_).cpu().numpy()
+        assert np.array_equal(np.isnan(y), np.isnan(ref)), layout
+        assert np.array_equal(np.isposinf(y), np.isposinf(ref)), layout
+        assert np.array_equal(np.isneginf(y), np.isneginf(ref)), layout
+        m = np.isfinite(ref)
+        assert _relrms(y[m], ref[m]) < 1e-6, layout
 
 
 def test_rolling_mean_parity():

@@ -138,14 +138,81 @@ def test_block_taps_reproduce_golden(name):
     Kx = plan.block_taps()
     assert Kx.shape == (4 * plan.n_sec + 1, plan.block_len + 2 * plan.n_sec)
     m = ~np.isnan(ref)
+    # cfg5's R = 2000 runs as 4 sub-blocks of 500 (taps + run buffers fit LDS)
+    assert plan.runs() is not None and plan.block_len <= 504
     for k1 in ("taps", "runs"):
-        if k1 == "runs" and plan.runs() is None:
-            assert plan.block_len == 2000  # cfg5: 147 KB of taps leave no LDS for run buffers
-            continue
         y = emulate(plan, x, 15, k1=k1)
         assert np.array_equal(np.isnan(y), ~m)
         rel = np.sqrt(np.sum((y[m] - ref[m]) ** 2) / np.sum(ref[m] ** 2))
         assert rel < 1e-6, (k1, rel)
+
+
+def _plan_off(fs, dt_out, P, B, n_ch, n, off_ns, grid_start_s=1.0):
+    """Samples at t0 + i dt with t0 = T0 + off_ns; the output grid starts on a
+    whole second (the notebooks' bgtime): every grid point falls the same
+    fraction w of a sample past a sample."""
+    dt_ns = int(round(1e9 / fs))
+    t0 = synth.T0_NS + off_ns
+    t1 = synth.T0_NS + int(grid_start_s * 1e9)
+    t2 = t0 + (n - 1) * dt_ns
+    tg = S.time_grid(t1, t2, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    lo, w = S.grid_positions(t0, dt_ns, tg)
+    chunks = [(*S.select_range(t0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    sos = lowpass_sos(fs, 1 / dt_out / 2 * 0.9)
+    return LowpassPlan(sos, n_ch, n, lo, w, chunks), sched, tg, t0, t1, t2, dt_ns, w
+
+
+@pytest.mark.parametrize("cfg", [
+    (250.0, 0.2, 40, 6, 6000, 370_000),       # cfg1 geometry, t0 0.37 ms past the grid
+    (500.0, 1.0, 60, 7, 90_000, 1_900_000),   # cfg3 parameters, 1.9 ms
+    (200.0, 10.0, 40, 6, 200_000, 1_900_000),  # cfg5 parameters: R = 2000 -> 4 sub-blocks of 500
+    (1000.0, 10.0, 20, 3, 400_000, 0),        # dt = 10 s at 1 kHz: R = 10,000 -> 20 sub-blocks
+])
+@pytest.mark.parametrize("k1", ["recurrence", "taps", "runs"])
+def test_offsample_and_subblock_plans_match_oracle(cfg, k1):
+    """Off-sample uniform grids (constant w) and long grid spacings (sub-blocks)
+    stay in the block plan: its host constants, driven through the NumPy
+    kernel model, reproduce the oracle's chunked sosfiltfilt + interp1d."""
+    fs, dt_out, P, B, n, off = cfg
+    x = synth.noise_sine(3, n, fs, seed=21, dc=50.0)
+    plan, sched, tg, t0, t1, t2, dt_ns, w = _plan_off(fs, dt_out, P, B, 3, n, off)
+    R = int(round(fs * dt_out))
+    assert np.all(w == w[0]) and (w[0] > 0) == (off > 0)
+    assert plan.block_len * (R // plan.block_len) == R and plan.block_len <= 504
+    _, _, cg = plan.constants()
+    assert np.all(cg["kstep"] == R // plan.block_len)
+    if k1 == "runs":
+        assert plan.runs() is not None
+    y = emulate(plan, x, 15, k1=k1)
+    ref = oracle.lfproc_process(x, t0, dt_ns, t1, t2, dt_out, P, B)
+    num = den = 0.0
+    produced = np.zeros(len(tg), bool)
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        np.testing.assert_array_equal(tt, tg[oa:ob])
+        num += float(np.sum((y[:, oa:ob] - r) ** 2))
+        den += float(np.sum(r ** 2))
+        produced[oa:ob] = True
+    assert (num / den) ** 0.5 < 1e-6
+    assert np.all(np.isnan(y[:, ~produced]))
+
+
+def test_offsample_tail_output_blends_two_samples():
+    """A single chunk whose last grid point lies in the partial tail block
+    (the one-shot Patch.pass_filter().interpolate() shape): the scan's tail
+    output interpolates between the two zero-phase samples around it."""
+    fs, n = 250.0, 2000
+    x = synth.noise_sine(2, n, fs, seed=5)
+    lo = np.arange(3, n - 1, 50, dtype=np.int64)
+    w = np.full(len(lo), 0.25)
+    sos = lowpass_sos(fs, 1.0)
+    plan = LowpassPlan(sos, 2, n, lo, w, [(0, n - 1, 0, len(lo))])
+    _, _, cg = plan.constants()
+    assert cg[0]["tail_out_j"] == len(lo) - 1
+    y = emulate(plan, x, 15, k1="runs")
+    yf = oracle.sosfiltfilt(oracle.butter_sos(4, 1.0 / 125.0), x)
+    ref = yf[:, lo] + 0.25 * (yf[:, lo + 1] - yf[:, lo])
+    assert np.sqrt(np.sum((y - ref) ** 2) / np.sum(ref ** 2)) < 1e-6
 
 
 def test_host_only_plan_cannot_execute():

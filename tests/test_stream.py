@@ -41,7 +41,7 @@ def _edge_cfg_cases():
         (250.0, 0.2, 40, 6, 8.0, 6, 0.0),      # cfg1 geometry, file = 8 s
         (200.0, 10.0, 30, 6, 125.0, 5, 0.0),   # d_t = 10 s (notebook default)
         (100.0, 1.0, 20, 3, 7.3, 9, 2.0),      # ragged files, late start
-        (250.0, 1.0, 40, 6, 20.0, 5, 0.0005),  # grid between samples: general device path
+        (250.0, 1.0, 40, 6, 20.0, 5, 0.0005),  # grid between samples: blended output functional
     ]
 
 
