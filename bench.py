@@ -7,11 +7,15 @@ Butterworth at 0.45 Hz, decimate to 1 Hz, LFProc chunking P = 600, B = 7.
 One step = one pass of the hot path over the whole hour (7 overlapping chunks,
 3,585 outputs per channel), inputs resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--weak]
 
-N > 1 is launched by torch.distributed.run (one rank per GPU); channels shard
-across ranks with no data-path collective (weak scaling: every rank owns a
-10,000-channel spool).  Rank 0 prints ONE JSON line.
+N > 1 is launched by torch.distributed.run (one rank per GPU).  Default
+(strong scaling, the config's "channel-sharded at 1/2/4/8 GPUs"): the
+10,000 channels are split into contiguous blocks (lfdas.shard.channel_range),
+no data-path collective; ``value`` = all channel-samples / max-over-ranks
+time.  ``--weak``: every rank owns its own 10,000-channel spool; with N > 1
+the weak figure is also reported as ``secondary.weak_scaling_cfg3``.
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -45,6 +49,9 @@ def _args():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-rolling", action="store_true")
     p.add_argument("--no-stream", action="store_true", help="skip the cfg4 / cfg5 streaming lines")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the extra low-pass lines (off-sample grid, 1 kHz dt = 10 s, time-major)")
+    p.add_argument("--weak", action="store_true", help="every rank owns --channels channels (weak scaling)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 PMC traffic summary (tools/pmc_summary.py) for roofline.traffic")
     return p.parse_args()
@@ -74,13 +81,34 @@ def synth_fill(x, fs, seed):
         blk += torch.sin(t[None, :] + phi) + 0.5
 
 
-def build_plan(n_ch, n, fs, dt_out, P, B):
+def synth_fill_time_major(x, fs, seed):
+    """The same kind of synthetic samples in (time, channel) storage."""
+    import torch
+    g = torch.Generator(device=x.device)
+    g.manual_seed(seed)
+    n, n_ch = x.shape
+    phi = torch.rand((1, n_ch), device=x.device, generator=g) * (2 * np.pi)
+    step = max(1, int(2e9 // (n_ch * 4)))
+    for t0 in range(0, n, step):
+        t1 = min(n, t0 + step)
+        blk = x[t0:t1]
+        torch.randn(blk.shape, device=x.device, generator=g, out=blk)
+        t = torch.arange(t0, t1, device=x.device, dtype=torch.float32)[:, None] * (2 * np.pi * 0.05 / fs)
+        blk += torch.sin(t + phi) + 0.5
+
+
+def build_plan(n_ch, n, fs, dt_out, P, B, off_ns=0):
+    """The LFProc plan of ``n`` samples per channel.  ``off_ns`` > 0: the
+    samples start that long after the whole second on which the output grid
+    starts (a real archive: every grid point lies a fraction of a sample past
+    a sample)."""
     from lfdas import schedule as S
     from lfdas.design import lowpass_sos
     from lfdas.plan import LowpassPlan
     dt_ns = int(round(1e9 / fs))
-    t0 = 1_505_692_800_000_000_000
-    tg = S.time_grid(t0, t0 + n * dt_ns, dt_out)
+    t_grid = 1_505_692_800_000_000_000
+    t0 = t_grid + off_ns
+    tg = S.time_grid(t_grid if off_ns == 0 else t_grid + 1_000_000_000, t0 + n * dt_ns, dt_out)
     sched = S.lfproc_chunks(len(tg), P, B)
     lo, w = S.grid_positions(t0, dt_ns, tg)
     chunks = [(*S.select_range(t0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
@@ -88,27 +116,114 @@ def build_plan(n_ch, n, fs, dt_out, P, B):
     return LowpassPlan(sos, n_ch, n, lo, w, chunks), sched, sos, t0, dt_ns, tg
 
 
-def cpu_baseline(args, sos, sched, t0, dt_ns, tg):
-    """Oracle C restatement of scipy's sosfiltfilt (+ interp) over the same
-    LFProc chunks, 1 process / 1 thread, on a bounded channel sample."""
-    sys.path.insert(0, ROOT)
-    import oracle
-    n = int(args.seconds * args.fs)
-    rng = np.random.default_rng(0)
-    n_c = args.cpu_channels
-    t = np.arange(n, dtype=np.float64) * (2 * np.pi * 0.05 / args.fs)
-    x = (rng.standard_normal((n_c, n)) + 0.5 + np.sin(t)[None, :]).astype(np.float32)
+K1_KERNELS = {"mfma_runs": "k_block_runs_mfma", "mfma": "k_block_functionals_mfma",
+              "mfma_fold": "k_block_functionals_mfma + k_fold_runs",
+              "recurrence": "k_block_functionals_lds|gen",
+              "recurrence_fold": "k_block_functionals_lds|gen + k_fold_runs"}
+
+
+def time_plan(plan, x, y, wsb, stream, steps, warmup, barrier=None):
+    """Warm up, then time ``steps`` executes between two barriers; returns
+    (wall seconds, per-step K1 ms, per-step scan ms) from HIP events on the
+    execution stream (lfd_lowpass_last_timing)."""
+    import torch
+    from lfdas.plan import set_timing
+    barrier = barrier or (lambda: torch.cuda.synchronize(x.device))
+    set_timing(True)
+    for _ in range(warmup):
+        plan.execute(x, y, wsb, stream)
+    barrier()
+    k1, sc = [], []
+    t_a = time.perf_counter()
+    for _ in range(steps):
+        plan.execute(x, y, wsb, stream)
+        a, b = plan.last_timing_ms()  # syncs on this step's events
+        k1.append(a)
+        sc.append(b)
+    barrier()
+    el = time.perf_counter() - t_a
+    set_timing(False)
+    return el, k1, sc
+
+
+def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_major=False, steps=5,
+                       label=""):
+    """One extra low-pass workload, timed like the headline (inputs in HBM,
+    K1 roofline from its HIP-event time)."""
+    import torch
+    n = int(seconds * fs)
+    plan, sched, sos, t0, dt_ns, tg = build_plan(n_ch, n, fs, dt_out, P, B, off_ns)
+    if time_major:  # (time, distance) storage, viewed as (channel, time)
+        xs = torch.empty((n, n_ch), dtype=torch.float32, device=dev)
+        synth_fill_time_major(xs, fs, 77)
+        x = xs.t()
+    else:
+        x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
+        synth_fill(x, fs, 77)
+    y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
+    wsb = plan.alloc_workspace(dev)
+    stream = torch.cuda.current_stream(dev)
+    el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, steps, 1)
+    R = int(round(fs * dt_out))
+    k1 = float(np.mean(k1_ms))
+    gbs = n_ch * n * (4.0 + 4.0 / R) / (k1 * 1e-3) / 1e9
+    out = {"value": n_ch * n * steps / el, "unit": "channel-samples/s", "ms_per_step": el / steps * 1e3,
+           "config": label, "k1": plan.last_kernel(), "block_len": plan.block_len,
+           "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS, "kernel": K1_KERNELS.get(plan.last_kernel()),
+                        "kernel_ms": k1, "scan_kernel_ms": float(np.mean(scan_ms)),
+                        "alg_bytes_per_sample": 4.0 + 4.0 / R}}
+    plan.close()
+    del x, y, wsb
+    torch.cuda.empty_cache()
+    return out
+
+
+def _cpu_chunks(backend, x, sos, sched, t0, dt_ns, tg):
+    """The LFProc chunks of the channel rows ``x`` on the CPU: ``"port"`` =
+    the oracle's C restatement of scipy's _sosfilt (+ its interp1d);
+    ``"scipy"`` = scipy.signal.sosfiltfilt + scipy.interpolate.interp1d, the
+    library DASCore's pass_filter / interpolate call (lf_das.py:223-225)."""
     from lfdas import schedule as S
-    t_start = time.perf_counter()
+    n = x.shape[1]
+    if backend == "scipy":
+        import scipy.interpolate as si
+        import scipy.signal as ss
+    else:
+        sys.path.insert(0, ROOT)
+        import oracle
     for a, b, oa, ob in sched:
         s0, s1 = S.select_range(t0, dt_ns, n, tg[a], tg[b])
-        y = oracle.sosfiltfilt_rows_c(sos, x[:, s0:s1 + 1])
         tt = (np.arange(s0, s1 + 1, dtype=np.int64) * dt_ns).astype(np.float64)
-        oracle.interp1d_linear(tt, y, (tg[oa:ob] - t0).astype(np.float64))
+        tq = (tg[oa:ob] - t0).astype(np.float64)
+        if backend == "scipy":
+            y = ss.sosfiltfilt(sos, x[:, s0:s1 + 1], axis=-1)
+            si.interp1d(tt, y, axis=-1, kind="linear")(tq)
+        else:
+            y = oracle.sosfiltfilt_rows_c(sos, x[:, s0:s1 + 1])
+            oracle.interp1d_linear(tt, y, tq)
+
+
+def _cpu_data(n_c, n, fs, seed):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n, dtype=np.float64) * (2 * np.pi * 0.05 / fs)
+    return (rng.standard_normal((n_c, n)) + 0.5 + np.sin(t)[None, :]).astype(np.float32)
+
+
+def cpu_baseline(args, sos, sched, t0, dt_ns, tg, backend="port", n_c=None):
+    """One process, one thread, over a bounded channel sample of the full hour."""
+    n = int(args.seconds * args.fs)
+    n_c = n_c or args.cpu_channels
+    x = _cpu_data(n_c, n, args.fs, 0)
+    t_start = time.perf_counter()
+    _cpu_chunks(backend, x, sos, sched, t0, dt_ns, tg)
     el = time.perf_counter() - t_start
-    return {"value": n_c * n / el, "unit": "channel-samples/s", "cores": 1, "kind": "port",
+    what = ("oracle C sosfiltfilt + interp1d" if backend == "port"
+            else "scipy.signal.sosfiltfilt + scipy.interpolate.interp1d")
+    return {"value": n_c * n / el, "unit": "channel-samples/s", "cores": 1,
+            "kind": "port" if backend == "port" else "reference-lib",
             "sample": f"{n_c} ch x {n} samples ({args.seconds:.0f} s @ {args.fs:.0f} Hz), same LFProc "
-                      f"chunks, oracle C sosfiltfilt + interp1d, 1 thread, {el:.1f} s"}
+                      f"chunks, {what}, 1 thread, {el:.1f} s"}
 
 
 def _pinned_blocks(dev, n_blocks, shape, fs, seed):
@@ -170,68 +285,118 @@ def bench_edge_cfg4(dev, n_push=12, warm=2, time_major=False):
                       "layout), dt = 1 s, P = 125, B = 7, resume buffer (B-1) s; latency = push -> host outputs"}
 
 
+CFG5_ROWS = [0, 15, 16, 24_999, 49_999]
+
+
 def bench_ooc_cfg5(dev, n_ch=50_000, seconds=3600.0, push_s=60.0):
     """cfg5 (bounded sample): out-of-core process_time_range over a 50,000-ch
     @ 200 Hz spool streamed from a pinned host ring, dt = 10 s (fc = 0.045 Hz),
-    P = 120 (1,200 s chunks), B = 6 (planner edge 60 s).  Bound: PCIe."""
+    P = 120 (1,200 s chunks), B = 6 (planner edge 60 s).  Bound: PCIe.  The
+    timed loop includes downloading every output; afterwards (untimed) the
+    sampled channels are checked against the oracle's process_time_range."""
     import torch
+    from lfdas.plan import set_timing
     from lfdas.stream import LowpassStream
     fs = 200.0
     push = int(push_s * fs)
     n = int(seconds * fs)
+    n_push = n // push
     dt_ns = int(1e9 / fs)
     t0 = 1_679_464_800_000_000_000
+    t_end = t0 + (n - 1) * dt_ns
     blocks = _pinned_blocks(dev, 2, (n_ch, push), fs, 777)
     st = LowpassStream(n_ch, dt_ns, 10.0, 120, 6, mode="continuous", t_start=t0,
-                       t_end=t0 + (n - 1) * dt_ns, capacity=int(1300 * fs) + 2 * push)
-    from lfdas.plan import set_timing
+                       t_end=t_end, capacity=int(1300 * fs) + 2 * push)
     st.reserve(push)
     n_out = 0
     cp = []
+    ys, ts = [], []
     torch.cuda.synchronize(dev)
     set_timing(True)
     ta = time.perf_counter()
-    for k in range(n // push):
+    for k in range(n_push):
         o = st.push(blocks[k % 2], t0 + k * push * dt_ns)
         n_out += o.n_out
-        st.wait_copy()  # ring buffer (k+1) % 2 is free again
+        if o.n_out:
+            y = st.fetch()  # outputs to the host (also frees the pinned block)
+            ys.append(y[CFG5_ROWS].copy())
+            ts.append(o.times_ns)
+        else:
+            st.wait_copy()  # ring buffer (k+1) % 2 is free again
         cp.append(st.last_timing_ms()[0])
     set_timing(False)
     o = st.flush()
     n_out += o.n_out
+    if o.n_out:
+        ys.append(st.fetch()[CFG5_ROWS].copy())
+        ts.append(o.times_ns)
     st.synchronize()
     el = time.perf_counter() - ta
     st.close()
+    xs = np.concatenate([blocks[k % 2][CFG5_ROWS].numpy() for k in range(n_push)], axis=1)
     del blocks
-    samples = n_ch * (n // push) * push
-    return {"value": samples / el, "unit": "channel-samples/s", "seconds_streamed": seconds,
-            "wall_s": el, "h2d_GBps": samples * 4 / el / 1e9, "pcie_peak_GBps": 63.0,
-            "pcie_frac": samples * 4 / el / 1e9 / 63.0, "outputs_per_channel": n_out,
-            "copy_ms_p50": float(np.median(cp)), "copy_ms_max": float(np.max(cp)),
-            "config": f"{n_ch:,} ch @ 200 Hz, {seconds:.0f} s of the 24 h spool in {push_s:.0f} s pinned "
-                      "pushes, dt = 10 s, P = 120, B = 6, 1 GPU"}
+    samples = n_ch * n_push * push
+    out = {"value": samples / el, "unit": "channel-samples/s", "seconds_streamed": seconds,
+           "wall_s": el, "h2d_GBps": samples * 4 / el / 1e9, "pcie_peak_GBps": 63.0,
+           "pcie_frac": samples * 4 / el / 1e9 / 63.0, "outputs_per_channel": n_out,
+           "copy_ms_p50": float(np.median(cp)), "copy_ms_max": float(np.max(cp)),
+           "config": f"{n_ch:,} ch @ 200 Hz, {seconds:.0f} s of the 24 h spool in {push_s:.0f} s pinned "
+                     "pushes, dt = 10 s, P = 120, B = 6, 1 GPU; outputs downloaded inside the timed loop"}
+    # parity of the sampled channels (the checker, outside the timed region)
+    sys.path.insert(0, ROOT)
+    import oracle
+    ref = oracle.lfproc_process(xs, t0, dt_ns, t0, t_end, 10.0, 120, 6)
+    want = np.concatenate([r for _, r in ref], axis=1)
+    got = np.concatenate(ys, axis=1) if ys else np.zeros((len(CFG5_ROWS), 0))
+    times_ok = bool(np.array_equal(np.concatenate(ts) if ts else np.zeros(0, np.int64),
+                                   np.concatenate([t for t, _ in ref])))
+    rel = (float(np.sqrt(np.sum((got.astype(np.float64) - want) ** 2) / np.sum(want ** 2)))
+           if got.shape == want.shape else float("inf"))
+    out["check"] = {"rows": CFG5_ROWS, "relrms_vs_oracle": rel, "times_identical": times_ok,
+                    "pass": bool(times_ok and rel < 1e-4),
+                    "checker": "oracle.lfproc_process on the sampled rows (untimed)"}
+    if not out["check"]["pass"]:
+        print(f"WARNING: cfg5 sampled-channel check failed: {out['check']}", file=sys.stderr)
+    return out
+
+
+def bench_rolling(dev, W, S_, reps=10):
+    """cfg2 rolling mean (5,000 ch x 10 min @ 1 kHz), window W, step S_;
+    algorithmic bytes 4 + 4/S per channel-sample."""
+    import torch
+    from lfdas.plan import rolling_mean_device
+    xr = torch.empty((5000, 600_000), dtype=torch.float32, device=dev)
+    synth_fill(xr, 1000.0, 99)
+    for _ in range(2):
+        y = rolling_mean_device(xr, W, S_)
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y = rolling_mean_device(xr, W, S_)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    gbs = 5000 * 600_000 * (4 + 4 / S_) / (ms * 1e-3) / 1e9
+    del xr, y
+    torch.cuda.empty_cache()
+    return {"value": 5000 * 600_000 / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms,
+            "config": f"5,000 ch x 10 min @ 1 kHz fp32, W = {W}, S = {S_}",
+            "kernel": "k_rolling_tc" if S_ >= W else "k_rolling_scan_tc",
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_sample": 4 + 4 / S_}}
 
 
 def _cpu_worker(a, barrier=None, q=None):
     """One CPU-baseline process: the LFProc chunks of ``n_c`` channels x the
-    full hour through the oracle C sosfiltfilt + interp1d (own data, made
-    before the start barrier)."""
-    fs, seconds, n_c, seed, sos, sched, t0, dt_ns, tg = a
-    sys.path.insert(0, ROOT)
-    import oracle
-    from lfdas import schedule as S
-    n = int(seconds * fs)
-    rng = np.random.default_rng(seed)
-    t = np.arange(n, dtype=np.float64) * (2 * np.pi * 0.05 / fs)
-    x = (rng.standard_normal((n_c, n)) + 0.5 + np.sin(t)[None, :]).astype(np.float32)
+    full hour (own data, made before the start barrier)."""
+    backend, fs, seconds, n_c, seed, sos, sched, t0, dt_ns, tg = a
+    x = _cpu_data(n_c, int(seconds * fs), fs, seed)
     if barrier is not None:
         barrier.wait()
     ta = time.perf_counter()
-    for a_, b_, oa, ob in sched:
-        s0, s1 = S.select_range(t0, dt_ns, n, tg[a_], tg[b_])
-        y = oracle.sosfiltfilt_rows_c(sos, x[:, s0:s1 + 1])
-        tt = (np.arange(s0, s1 + 1, dtype=np.int64) * dt_ns).astype(np.float64)
-        oracle.interp1d_linear(tt, y, (tg[oa:ob] - t0).astype(np.float64))
+    _cpu_chunks(backend, x, sos, sched, t0, dt_ns, tg)
     el = time.perf_counter() - ta
     if q is not None:
         q.put(el)
@@ -249,7 +414,7 @@ def cpu_workers() -> int:
     return max(1, min(aff, cap, 16))
 
 
-def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48):
+def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48, backend="port"):
     """SURVEY §8(d) figure 2: one worker PROCESS per core over channel blocks
     (SciPy's _sosfilt does not scale with threads).  Forked before the GPU is
     initialised.  Channel-sample rate of the whole pool (wall clock)."""
@@ -258,7 +423,7 @@ def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48):
     ctx = mp.get_context("fork")
     barrier = ctx.Barrier(nw + 1)
     q = ctx.Queue()
-    procs = [ctx.Process(target=_cpu_worker, args=((args.fs, args.seconds, n_c_per, 100 + i, sos, sched,
+    procs = [ctx.Process(target=_cpu_worker, args=((backend, args.fs, args.seconds, n_c_per, 100 + i, sos, sched,
                                                      t0, dt_ns, tg), barrier, q)) for i in range(nw)]
     for p in procs:
         p.start()
@@ -269,29 +434,21 @@ def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48):
     for p in procs:
         p.join()
     n = int(args.seconds * args.fs)
+    what = "oracle C sosfiltfilt + interp1d" if backend == "port" else "scipy sosfiltfilt + interp1d"
     return {"value": nw * n_c_per * n / wall, "cores": nw, "wall_s": wall,
-            "sample": f"{nw} processes x {n_c_per} ch x {n} samples, same LFProc chunks, oracle C "
-                      f"sosfiltfilt + interp1d; per-process {min(per):.1f}-{max(per):.1f} s"}
+            "sample": f"{nw} processes x {n_c_per} ch x {n} samples, same LFProc chunks, {what}; "
+                      f"per-process {min(per):.1f}-{max(per):.1f} s"}
 
 
 def main():
     args = _args()
     import torch
     ws, rank, local = _dist()
-    if ws > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if ws > 1 else 0)
-    torch.cuda.set_device(dev)
-
-    from lfdas.plan import set_timing
-    n_ch = args.channels
     n = int(args.seconds * args.fs)
     cpu = None
     if ws == 1 and not args.no_cpu:
         # host-only plan geometry (the library's schedule), then the CPU legs
-        # before the GPU is initialised (the parallel leg forks)
+        # before the GPU is initialised (the parallel legs fork)
         from lfdas import schedule as S
         from lfdas.design import lowpass_sos
         c_dt_ns = int(round(1e9 / args.fs))
@@ -299,13 +456,37 @@ def main():
         c_tg = S.time_grid(c_t0, c_t0 + n * c_dt_ns, args.dt_out)
         c_sched = S.lfproc_chunks(len(c_tg), args.patch_size, args.edge_buff)
         c_sos = lowpass_sos(args.fs, 1 / args.dt_out / 2 * 0.9, 4)
-        one = cpu_baseline(args, c_sos, c_sched, c_t0, c_dt_ns, c_tg)
-        par = cpu_baseline_parallel(args, c_sos, c_sched, c_t0, c_dt_ns, c_tg)
+        geo = (c_sos, c_sched, c_t0, c_dt_ns, c_tg)
+        one = cpu_baseline(args, *geo)
+        par = cpu_baseline_parallel(args, *geo)
         cpu = {"value": par["value"], "unit": "channel-samples/s", "cores": par["cores"], "kind": "port",
                "extrapolated": True,
                "sample": par["sample"] + "; rate extrapolated linearly to the full 10,000-channel step",
                "single_process": {"value": one["value"], "cores": 1, "sample": one["sample"]},
                "workers": "processes (fork) over channel blocks"}
+        try:  # the reference's own numeric library (scipy), timed the same way
+            one_s = cpu_baseline(args, *geo, backend="scipy", n_c=192)
+            par_s = cpu_baseline_parallel(args, *geo, n_c_per=16, backend="scipy")
+            cpu["reference_lib"] = {"value": par_s["value"], "unit": "channel-samples/s", "cores": par_s["cores"],
+                                    "kind": "reference-lib", "extrapolated": True, "sample": par_s["sample"],
+                                    "single_process": {"value": one_s["value"], "cores": 1,
+                                                       "sample": one_s["sample"]}}
+        except ImportError as e:  # pragma: no cover
+            cpu["reference_lib"] = {"error": repr(e)}
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if ws > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from lfdas.shard import channel_range
+    if args.weak:
+        n_ch_total, (c0, c1) = args.channels * ws, (0, args.channels)
+    else:
+        n_ch_total = args.channels
+        c0, c1 = channel_range(args.channels, ws, rank)
+    n_ch = c1 - c0
     plan, sched, sos, t0, dt_ns, tg = build_plan(n_ch, n, args.fs, args.dt_out, args.patch_size,
                                                  args.edge_buff)
     x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
@@ -319,30 +500,19 @@ def main():
         if ws > 1:
             torch.distributed.barrier()
 
-    set_timing(True)
-    for _ in range(args.warmup):
-        plan.execute(x, y, wsb, stream)
-    barrier()
-    k1_ms = []
-    scan_ms = []
-    t_a = time.perf_counter()
-    for _ in range(args.steps):
-        plan.execute(x, y, wsb, stream)
-        a, b = plan.last_timing_ms()  # syncs on this step's events
-        k1_ms.append(a)
-        scan_ms.append(b)
-    barrier()
-    el = time.perf_counter() - t_a
-    set_timing(False)
-    k1_kernel = plan.last_kernel()
-    if ws > 1:
-        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+    def max_over_ranks(v):
+        if ws == 1:
+            return v
+        tt = torch.tensor([v], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        el = float(tt.item())
+        return float(tt.item())
+
+    el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, args.steps, args.warmup, barrier)
+    el = max_over_ranks(el)
+    k1_kernel = plan.last_kernel()
 
     R = int(round(args.fs * args.dt_out))
-    samples = n_ch * n * ws
-    value = samples * args.steps / el
+    value = n_ch_total * n * args.steps / el
     k1 = float(np.mean(k1_ms))
     alg_bytes = n_ch * n * (4.0 + 4.0 / R)
     achieved = alg_bytes / (k1 * 1e-3) / 1e9
@@ -359,61 +529,64 @@ def main():
     if ws > 1:
         # the path's one collective, outside the timed step: RCCL all-gather of
         # the decimated outputs (lfdas.shard.all_gather_channels), every rank
-        # ends with all n_ch * ws channels
+        # ends with all n_ch_total channels
         from lfdas.shard import all_gather_channels
         try:
             g_ms = []
             for i in range(4):
                 barrier()
                 t_g = time.perf_counter()
-                full = all_gather_channels(y, n_ch * ws)
+                full = all_gather_channels(y, n_ch_total)
                 torch.cuda.synchronize(dev)
                 if i:
                     g_ms.append((time.perf_counter() - t_g) * 1e3)
             del full
-            tt = torch.tensor([float(np.median(g_ms))], device=dev, dtype=torch.float64)
-            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            gm = max_over_ranks(float(np.median(g_ms)))
             secondary["allgather_outputs"] = {
-                "ms": float(tt.item()), "bytes_per_rank": int(y.numel() * 4),
-                "frac_of_step": float(tt.item()) / (el / args.steps * 1e3),
+                "ms": gm, "bytes_per_rank": int(y.numel() * 4), "frac_of_step": gm / (el / args.steps * 1e3),
                 "note": "RCCL all_gather of every rank's (n_ch, n_grid) float32 outputs; not in the timed step"}
         except Exception as e:  # the optional gather never voids the bench line
             secondary["allgather_outputs"] = {"error": repr(e)}
-    if ws == 1:
-        del x, y, wsb
-        plan.close()
+    del x, y, wsb
+    plan.close()
+    torch.cuda.empty_cache()
+    if ws > 1 and not args.weak:
+        # weak scaling: every rank its own 10,000-channel spool
+        plan_w, _, _, _, _, _ = build_plan(args.channels, n, args.fs, args.dt_out, args.patch_size, args.edge_buff)
+        xw = torch.empty((args.channels, n), dtype=torch.float32, device=dev)
+        synth_fill(xw, args.fs, 4321 + rank)
+        yw = torch.empty((args.channels, plan_w.n_grid), dtype=torch.float32, device=dev)
+        ww = plan_w.alloc_workspace(dev)
+        el_w, k1_w, _ = time_plan(plan_w, xw, yw, ww, stream, args.steps, 1, barrier)
+        el_w = max_over_ranks(el_w)
+        secondary["weak_scaling_cfg3"] = {
+            "value": ws * args.channels * n * args.steps / el_w, "unit": "channel-samples/s",
+            "ms_per_step": el_w / args.steps * 1e3, "kernel_ms_rank0": float(np.mean(k1_w)),
+            "scaling": "weak", "config": f"{args.channels:,} ch x 1 h @ 500 Hz per GPU x {ws} GPUs"}
+        del xw, yw, ww
+        plan_w.close()
         torch.cuda.empty_cache()
+    if ws == 1 and not args.no_extra:
+        secondary["cfg3_offsample_grid"] = bench_lowpass_line(
+            dev, args.channels, args.fs, args.seconds, args.dt_out, args.patch_size, args.edge_buff,
+            off_ns=1_900_000, label="cfg3 with the samples starting 1.9 ms after the output grid's second "
+                                    "(every output interpolated between two samples, w = 0.05)")
+        secondary["cfg3_time_major"] = bench_lowpass_line(
+            dev, args.channels, args.fs, args.seconds, args.dt_out, args.patch_size, args.edge_buff,
+            time_major=True, label="cfg3 stored (time, distance) like the real files (data[:, ch])")
+        secondary["lowpass_1khz_dt10"] = bench_lowpass_line(
+            dev, 10_000, 1000.0, 3600.0, 10.0, 120, 6,
+            label="10,000 ch x 1 h @ 1 kHz (144 GB), dt = 10 s (the batch notebook's d_t), P = 120, B = 6: "
+                  "R = 10,000 as 20 sub-blocks of 500")
     if not args.no_rolling and ws == 1:
-        from lfdas.plan import rolling_mean_device
-        xr = torch.empty((5000, 600_000), dtype=torch.float32, device=dev)
-        synth_fill(xr, 1000.0, 99)
-        for _ in range(2):
-            rolling_mean_device(xr, 1000, 1000)
-        torch.cuda.synchronize(dev)
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        reps = 10
-        for _ in range(reps):
-            rolling_mean_device(xr, 1000, 1000)
-        e1.record()
-        torch.cuda.synchronize(dev)
-        ms = e0.elapsed_time(e1) / reps
-        gbs = 5000 * 600_000 * (4 + 4 / 1000) / (ms * 1e-3) / 1e9
-        secondary["rolling_mean_cfg2"] = {
-            "value": 5000 * 600_000 / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms,
-            "config": "5,000 ch x 10 min @ 1 kHz fp32, W = S = 1000",
-            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS}}
-        del xr
-        torch.cuda.empty_cache()
+        secondary["rolling_mean_cfg2"] = bench_rolling(dev, 1000, 1000)
+        secondary["rolling_mean_cfg2_step1"] = bench_rolling(dev, 1000, 1, reps=5)
     if not args.no_stream and ws == 1:
         secondary["edge_latency_cfg4"] = bench_edge_cfg4(dev)
         secondary["edge_latency_cfg4_time_major"] = bench_edge_cfg4(dev, time_major=True)
         torch.cuda.empty_cache()
         secondary["out_of_core_cfg5"] = bench_ooc_cfg5(dev)
         torch.cuda.empty_cache()
-
 
     if rank == 0:
         out = {
@@ -425,20 +598,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (0.5 + sin + N(0,1), generated on device)",
-            "config": {"workload": "cfg3: 10,000 ch x 1 h @ 500 Hz fp32 (72 GB) per GPU, 4th-order "
-                                   "Butterworth 0.45 Hz zero-phase, decimate to 1 Hz, LFProc P=600 B=7",
-                       "channels_per_gpu": n_ch, "samples": n, "fs": args.fs, "dt_out": args.dt_out,
-                       "chunks": len(sched), "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),
+            "config": {"workload": "cfg3: 10,000 ch x 1 h @ 500 Hz fp32 (72 GB), 4th-order Butterworth "
+                                   "0.45 Hz zero-phase, decimate to 1 Hz, LFProc P=600 B=7"
+                                   + (", per GPU" if args.weak else ", channel-sharded over the GPUs"),
+                       "channels": n_ch_total, "channels_rank0": n_ch, "samples": n, "fs": args.fs,
+                       "dt_out": args.dt_out, "chunks": len(sched),
+                       "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),
                        "parallelism": f"channel-shard x{ws}", "io_dtype": "f32"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": {"mfma_runs": "k_block_runs_mfma", "mfma": "k_block_functionals_mfma"}
-                                   .get(k1_kernel, "k_block_functionals_lds"), "kernel_ms": k1,
-                         "scan_kernel_ms": float(np.mean(scan_ms))},
+                         "kernel": K1_KERNELS.get(k1_kernel), "kernel_ms": k1,
+                         "scan_kernel_ms": float(np.mean(scan_ms)),
+                         "alg_bytes_per_sample": 4.0 + 4.0 / R, "samples_per_launch": n_ch * n},
             "cpu_baseline": cpu,
             "secondary": secondary,
         }

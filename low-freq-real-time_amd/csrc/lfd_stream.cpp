@@ -533,8 +533,22 @@ int lfd_stream_push(lfd_stream *s, const float *x, int64_t n_t, int64_t s_ch, in
   s->timed = !s->dry && lfd::timing_enabled();
   s->timed_run = false;
   if (s->have) {
-    if (t0_ns != s->t_col0 + s->a_hi * s->cfg.sample_ns)
+    // the merge rule of Spool.chunk(time=None) (lfdas/core.py _contiguous,
+    // tolerance 1.5 samples): a push whose first sample lies within
+    // (0, 1.5] sample intervals after the last held sample continues the
+    // arena's sample grid (its t0 snaps to the next column, as the resident
+    // path's merged patch indexes it); a first sample AT the last held time
+    // is a duplicated boundary sample and is dropped; anything else is a gap
+    const int64_t dts = s->cfg.sample_ns;
+    const int64_t last = s->t_col0 + (s->a_hi - 1) * dts;
+    const int64_t gap = t0_ns - last;
+    if (gap == 0 && n_t > 0) {
+      x += s_t;
+      --n_t;
+    } else if (!(gap > 0 && 2 * gap <= 3 * dts)) {
       return fail(LFD_EINVAL, "patch merge failed! Gap in data exists");
+    }
+    t0_ns = last + dts;
   } else {
     s->t_col0 = t0_ns;
     s->a_lo = s->a_hi = 0;
@@ -545,7 +559,7 @@ int lfd_stream_push(lfd_stream *s, const float *x, int64_t n_t, int64_t s_ch, in
   } else if (s->a_hi + n_t > s->cap) {
     LFD_TRY(make_room(s, n_t));
   }
-  if (!s->dry) LFD_TRY(copy_in(s, x, n_t, s_ch, s_t));
+  if (!s->dry && n_t > 0) LFD_TRY(copy_in(s, x, n_t, s_ch, s_t));
   s->have = true;
   s->a_hi += n_t;
   return s->cfg.mode == LFD_STREAM_EDGE ? run_edge(s) : run_continuous(s, false);

@@ -146,16 +146,20 @@ class LFProc:
     ``verbose``: print the reference's per-chunk progress lines.
     Processed patches of the last ``process_time_range`` call are kept in
     ``self.outputs`` (and written to the output folder like the reference).
+    Patches merged by ``chunk(time=None)`` (boundary gap up to 1.5 samples)
+    are processed on the first patch's sample grid, resident or streamed.
     """
 
-    def __init__(self, sp=None, device=None, verbose=True, max_resident_bytes=None):
+    def __init__(self, sp=None, device=None, verbose=True, max_resident_bytes=None, write_files=True):
         self._spool = sp
         self._para = self._default_process_parameters()
         self._output_folder = None
         self._device = device
         self.verbose = verbose
         self.outputs = []
-        self.write_files = True
+        # False: keep the output patches in self.outputs only (no folder
+        # needed; the sharded driver gathers them and writes on rank 0)
+        self.write_files = write_files
         # time ranges whose samples exceed this many bytes stream through the
         # device arena (out-of-core); default: env LFDAS_MAX_RESIDENT_BYTES,
         # else half of the free HBM
@@ -202,7 +206,7 @@ class LFProc:
     # ------------------------------------------------------------------
     def process_time_range(self, bgtime, edtime):
         """lf_das.py:219-290, one device pass for all chunks."""
-        if self._output_folder is None:
+        if self._output_folder is None and self.write_files:
             raise Exception("Please setup output folder first")
         dt = self._para["output_sample_interval"]
         patch_size = self._para["process_patch_size"]
@@ -297,24 +301,27 @@ class LFProc:
                     out.io.write(self._output_folder + "/" + fn, "dasdae")
                 j += cnt
 
-        expected = None
+        last_t = None
         try:
             for p in pats:
                 sel = p.select(time=(t_lo, t_hi))
                 t_ns = sel.sample_times_ns()
-                if expected is not None and len(t_ns) and t_ns[0] < expected:
-                    sel = sel.select(time=(np.datetime64(int(expected), "ns"), None))  # duplicated boundary
-                    t_ns = sel.sample_times_ns()
                 if not len(t_ns):
                     continue
+                if last_t is not None and t_ns[0] < last_t:
+                    # overlapping patches do not merge (core._contiguous)
+                    raise Exception("patch merge failed! Gap in data exists")
                 data = np.asarray(sel.data, dtype=np.float32)
                 try:
+                    # the stream applies chunk(time=None)'s merge rule: a
+                    # duplicated boundary sample is dropped, a boundary gap
+                    # of up to 1.5 samples continues the sample grid
                     emit(st.push(data, int(t_ns[0]), time_axis=tdim))
                 except ValueError as e:
                     if "Gap in data" in str(e):
                         raise Exception("patch merge failed! Gap in data exists") from None
                     raise
-                expected = int(t_ns[-1]) + dt_ns
+                last_t = int(t_ns[-1])
             emit(st.flush())
         finally:
             st.close()

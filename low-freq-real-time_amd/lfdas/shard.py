@@ -3,8 +3,22 @@
 Every op of the path is per channel, so ranks own contiguous channel ranges
 and run the whole plan on their shard with no data-path exchange
 (SURVEY §8e).  ``all_gather_channels`` assembles the decimated outputs (the
-only collective; RCCL over xGMI with backend "nccl", gloo on CPU)."""
+only collective; RCCL over xGMI with backend "nccl", gloo on CPU).
+
+* ``process_time_range_sharded`` — the product's multi-GPU form of
+  ``LFProc.process_time_range`` (lf_das.py:219-290, the single-process loop
+  it replaces): rank r runs LFProc on ``spool.select(distance=...)`` of its
+  channel block, then the per-chunk outputs are all-gathered and rank 0
+  writes the reference's full-width files.
+* ``shard_stream`` — the out-of-core form (cfg5 across 8 GPUs): every rank
+  opens its own ``LowpassStream`` on its channel block and pushes its rows of
+  each host block (``push_rows``); the streams never exchange data.
+"""
 from __future__ import annotations
+
+import os
+
+import numpy as np
 
 
 def channel_range(n_ch: int, world: int, rank: int):
@@ -12,6 +26,16 @@ def channel_range(n_ch: int, world: int, rank: int):
     per = -(-int(n_ch) // int(world))
     c0 = min(rank * per, n_ch)
     return c0, min(c0 + per, n_ch)
+
+
+def _world(group=None):
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(group), dist.get_rank(group)
+    except ImportError:  # pragma: no cover
+        pass
+    return 1, 0
 
 
 def all_gather_channels(y_local, n_ch: int, group=None):
@@ -27,3 +51,133 @@ def all_gather_channels(y_local, n_ch: int, group=None):
     parts = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(parts, pad, group=group)
     return torch.cat(parts, 0)[:n_ch]
+
+
+def shard_spool(sp, world: int, rank: int):
+    """Rank ``rank``'s contiguous channel block of a spool, as
+    ``Spool.select(distance=(d[c0], d[c1 - 1]))`` (inclusive, DASCore);
+    returns (sub-spool or None when the block is empty, (c0, c1))."""
+    d = np.asarray(sp[0].coords["distance"])
+    c0, c1 = channel_range(len(d), world, rank)
+    if c1 <= c0:
+        return None, (c0, c1)
+    return sp.select(distance=(d[c0], d[c1 - 1])), (c0, c1)
+
+
+def lfproc_shard(sub, bgtime, edtime, params, device=None):
+    """Default per-rank compute: LFProc.process_time_range on the rank's
+    sub-spool (device plan, no files) → its output patches in chunk order."""
+    from .lf_das import LFProc
+    lfp = LFProc(sub, device=device, verbose=False, write_files=False)
+    lfp.update_processing_parameter(**params)
+    lfp.process_time_range(bgtime, edtime)
+    return lfp.outputs
+
+
+def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=None, group=None,
+                               device=None, run_shard=None, gather=True, verbose=True):
+    """``LFProc(sp).process_time_range(bgtime, edtime)`` over the ranks of the
+    default process group: rank r processes channel block r (``shard_spool``)
+    with ``run_shard(sub_spool, bgtime, edtime, params)`` (default
+    ``lfproc_shard``: the device plan), the decimated outputs of every chunk
+    are all-gathered (RCCL on backend "nccl", gloo on CPU) and rank 0 writes
+    the reference's files (``LFDAS_<t0>_<t1>.h5``, lf_das.py:230-232) into
+    ``output_folder``.  Returns the full-width output patches (every rank when
+    ``gather``; else this rank's own block).  A failure on any rank (e.g. the
+    gap exception of lf_das.py:18) is raised on every rank, after the
+    collective, so no rank is left waiting."""
+    import torch
+
+    from . import schedule as S
+    from .core import Patch
+    from .lf_das import LFProc, _get_filename
+    params = dict(params or {})
+    world, rank = _world(group)
+    para = LFProc(None)._default_process_parameters()
+    para.update({k: v for k, v in params.items() if k in para})
+    tg = S.time_grid(bgtime, edtime, para["output_sample_interval"])
+    sched = S.lfproc_chunks(len(tg), para["process_patch_size"], para["edge_buff_size"])
+    counts = [ob - oa for _, _, oa, ob in sched]
+    sub, (c0, c1) = shard_spool(sp, world, rank)
+    run_shard = run_shard or (lambda s, a, b, p: lfproc_shard(s, a, b, p, device))
+    outs, err = [], None
+    if sub is not None:
+        try:
+            outs = run_shard(sub, bgtime, edtime, params)
+        except Exception as e:  # re-raised below, after every rank agreed
+            err = e
+    if world > 1:
+        import torch.distributed as dist
+        flag = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device=_comm_device(group))
+        dist.all_reduce(flag, group=group)
+        if int(flag.item()):
+            raise err if err is not None else RuntimeError("process_time_range failed on another rank")
+    elif err is not None:
+        raise err
+    p0 = sp[0]
+    tdim = p0.dims.index("time")
+    n_ch = len(np.asarray(p0.coords["distance"]))
+    n_local = c1 - c0
+    # this rank's block, chunks side by side: (n_local, sum(counts)) float64
+    blk = np.zeros((n_local, sum(counts)), np.float64)
+    j = 0
+    for out, cnt in zip(outs, counts):
+        d = np.asarray(out.data, np.float64)
+        blk[:, j:j + cnt] = d.T if tdim == 0 else d
+        j += cnt
+    if world > 1 and gather:
+        t = torch.from_numpy(blk).to(_comm_device(group))
+        full = all_gather_channels(t, n_ch, group=group).cpu().numpy()
+        dist_coords = np.asarray(p0.coords["distance"])
+    else:
+        full = blk
+        dist_coords = np.asarray(sub[0].coords["distance"]) if sub is not None else np.zeros(0)
+    res = []
+    j = 0
+    attrs = p0._attrs_wo_coords()
+    for i, ((_, _, oa, ob), cnt) in enumerate(zip(sched, counts), start=1):
+        seg = full[:, j:j + cnt]
+        coords = dict(p0.coords.coord_map)
+        coords["distance"] = dist_coords
+        coords["time"] = tg[oa:ob].astype("datetime64[ns]")
+        out = Patch(data=seg.T.copy() if tdim == 0 else seg.copy(), coords=coords, dims=p0.dims,
+                    attrs=attrs).update_attrs(d_time=para["output_sample_interval"])
+        res.append(out)
+        if rank == 0 and output_folder and (world == 1 or gather):
+            if verbose:
+                print("Processing patch ", str(i))
+            os.makedirs(output_folder, exist_ok=True)
+            out.io.write(os.path.join(output_folder, _get_filename(out.attrs["time_min"], out.attrs["time_max"])),
+                         "dasdae")
+        j += cnt
+    return res
+
+
+def _comm_device(group=None):
+    """Tensors of the group's collectives live here (HBM for RCCL, host for gloo)."""
+    import torch
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def shard_stream(n_ch: int, sampling_interval_ns: int, group=None, **stream_kw):
+    """This rank's ``LowpassStream`` over its channel block (out-of-core
+    cfg5 across GPUs: one host→HBM stream per GPU, no data exchange).
+    Returns (stream, (c0, c1)); push this rank's rows with ``push_rows``."""
+    from .stream import LowpassStream
+    world, rank = _world(group)
+    c0, c1 = channel_range(n_ch, world, rank)
+    if c1 <= c0:
+        return None, (c0, c1)
+    return LowpassStream(c1 - c0, sampling_interval_ns, **stream_kw), (c0, c1)
+
+
+def push_rows(stream, block, c_range, t0, time_axis: int = 1):
+    """Push rows [c0, c1) of a full-width host block (channel axis 0 for
+    ``time_axis=1``, axis 1 for ``time_axis=0``) — a strided host view, no
+    copy of the other ranks' channels."""
+    c0, c1 = c_range
+    view = block[c0:c1] if time_axis == 1 else block[:, c0:c1]
+    return stream.push(view, t0, time_axis=time_axis)

@@ -22,7 +22,9 @@ def _rel(a, b):
 
 
 def _write_archive(folder, n_files=6, n_ch=24, n_t=2000, fs=250.0, dims=("distance", "time"),
-                   skip=None, seed=1):
+                   skip=None, seed=1, jitter=None):
+    """jitter = (file i, ns): files >= i start that much later (a boundary gap
+    of one sample + jitter before file i)."""
     import lfdas.dc as dc
     os.makedirs(folder, exist_ok=True)
     x = synth.noise_sine(n_ch, n_files * n_t, fs, seed=seed, dc=5.0).astype(np.float64)
@@ -32,6 +34,8 @@ def _write_archive(folder, n_files=6, n_ch=24, n_t=2000, fs=250.0, dims=("distan
             continue
         blk = x[:, i * n_t:(i + 1) * n_t]
         t = T0 + (i * n_t + np.arange(n_t)) * step
+        if jitter is not None and i >= jitter[0]:
+            t = t + np.timedelta64(int(jitter[1]), "ns")
         data = blk if dims[0] == "distance" else np.ascontiguousarray(blk.T)
         p = dc.Patch(data=data, coords={"distance": np.arange(float(n_ch)), "time": t}, dims=dims,
                      attrs={"time_step": step})
@@ -103,3 +107,41 @@ def test_out_of_core_gap_error(tmp_path):
         lfp.process_time_range(T0, T0 + np.timedelta64(47, "s"))
     # the chunks before the gap were written, as the reference does
     assert 0 < len(os.listdir(tmp_path / "out")) == len(lfp.outputs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jitter_ns,merges", [(800_000, True), (2_400_000, False)])
+def test_jittered_boundary_same_rule_resident_and_stream(tmp_path, jitter_ns, merges):
+    """One continuity rule on both paths (chunk(time=None), tolerance 1.5
+    samples): a 1.2-sample boundary gap merges onto the first file's sample
+    grid whether the range is processed resident or streamed (identical
+    outputs, equal to the oracle on the regular-grid series); a 1.6-sample
+    gap raises the reference's gap error on both."""
+    import lf_das
+    import lfdas.dc as dc
+    x = _write_archive(str(tmp_path / "raw"), jitter=(3, jitter_ns))
+    t1, t2 = T0, T0 + np.timedelta64(6 * 8, "s") - np.timedelta64(4, "ms")
+    res = {}
+    for mode, budget in (("resident", None), ("stream", 1)):
+        lfp = lf_das.LFProc(dc.spool(str(tmp_path / "raw")), max_resident_bytes=budget, verbose=False)
+        lfp.update_processing_parameter(output_sample_interval=0.2, process_patch_size=40, edge_buff_size=6)
+        lfp.set_output_folder(str(tmp_path / f"out_{mode}"))
+        if not merges:
+            with pytest.raises(Exception, match="patch merge failed! Gap in data exists"):
+                lfp.process_time_range(t1, t2)
+            res[mode] = len(lfp.outputs)
+            continue
+        lfp.process_time_range(t1, t2)
+        assert lfp.last_mode == mode
+        res[mode] = lfp.outputs
+    if not merges:
+        assert res["resident"] == res["stream"]
+        return
+    ref = oracle.lfproc_process(x.astype(np.float32), int(T0.astype(np.int64)), 4_000_000,
+                                int(t1.astype(np.int64)), int(t2.astype(np.int64)), 0.2, 40, 6)
+    assert len(res["resident"]) == len(res["stream"]) == len(ref)
+    for a, b, (rt, ry) in zip(res["resident"], res["stream"], ref):
+        np.testing.assert_array_equal(a.coords["time"].astype(np.int64), rt)
+        np.testing.assert_array_equal(b.coords["time"].astype(np.int64), rt)
+        assert _rel(b.data, a.data) < 1e-6
+        assert _rel(a.data, ry) < 1e-4

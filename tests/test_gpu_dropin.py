@@ -67,6 +67,27 @@ def test_lfproc_errors(tmp_path):
     assert len(lfp.outputs) == 1  # chunk 1 (0-8 s) precedes the gap at ~8 s
 
 
+def test_sharded_driver_world1_matches_lfproc(tmp_path):
+    """lfdas.shard.process_time_range_sharded without a process group (one
+    rank): the device plan on the whole spool, the same outputs and files as
+    LFProc.process_time_range."""
+    import lf_das
+    from lfdas.shard import process_time_range_sharded
+    sp = _example_spool()
+    params = {"output_sample_interval": 0.2, "process_patch_size": 40, "edge_buff_size": 6}
+    t1, t2 = np.datetime64("2017-09-18T00:00:00"), np.datetime64("2017-09-18T00:00:24")
+    outs = process_time_range_sharded(sp, t1, t2, params, output_folder=str(tmp_path / "sh"), verbose=False)
+    lfp = lf_das.LFProc(sp, verbose=False)
+    lfp.update_processing_parameter(**params)
+    lfp.set_output_folder(str(tmp_path / "one"))
+    lfp.process_time_range(t1, t2)
+    assert len(outs) == len(lfp.outputs) == 4
+    for a, b in zip(outs, lfp.outputs):
+        np.testing.assert_array_equal(a.coords["time"], b.coords["time"])
+        np.testing.assert_array_equal(a.data, b.data)
+    assert sorted(os.listdir(tmp_path / "sh")) == sorted(os.listdir(tmp_path / "one"))
+
+
 def test_realtime_resume_contiguous(tmp_path):
     """low_pass_dascore_edge.ipynb:215-233: second run starts at
     last_out - (ceil(edge/dt)-1)*dt and continues the output grid."""

@@ -118,6 +118,73 @@ def test_cfg2_rolling_full_size_sampled_channels():
     torch.cuda.empty_cache()
 
 
+CFG5_ROWS = [0, 15, 16, 24_999, 49_999]
+
+
+def cfg5_push_block(k, n_ch, push, fs, rows, dev):
+    """Push k of the cfg5 check spool, generated on the device: every channel
+    holds its own constant 100 + ch/1000, the sampled rows carry noise + a
+    slow sine on top (seeded per push)."""
+    import torch
+    x = (torch.arange(n_ch, device=dev, dtype=torch.float32) * 1e-3 + 100.0)[:, None].repeat(1, push)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5000 + k)
+    t = (torch.arange(push, device=dev, dtype=torch.float64) + k * push) / fs
+    sig = torch.sin(2 * np.pi * 0.002 * t).float()
+    idx = torch.as_tensor(rows, device=dev)
+    x[idx] += torch.randn((len(rows), push), device=dev, generator=g) + sig[None, :]
+    return x
+
+
+def test_cfg5_out_of_core_stream_full_width():
+    """cfg5 geometry through the continuous (out-of-core) stream: 50,000 ch @
+    200 Hz in 60 s pinned pushes, dt = 10 s, P = 120, B = 6, 45 min (3 LFProc
+    chunks).  Sampled channels against the oracle's process_time_range, every
+    other channel's constant back as itself, identical output times."""
+    import torch
+
+    from lfdas.stream import LowpassStream
+    n_ch, fs, push_s, dur = 50_000, 200.0, 60.0, 2700.0
+    push, n = int(push_s * fs), int(dur * fs)
+    dt_ns = int(1e9 / fs)
+    t_end = T0 + (n - 1) * dt_ns
+    dev = torch.device("cuda")
+    rows = CFG5_ROWS
+    st = LowpassStream(n_ch, dt_ns, 10.0, 120, 6, mode="continuous", t_start=T0, t_end=t_end,
+                       capacity=int(1300 * fs) + 2 * push)
+    st.reserve(push)
+    host = [torch.empty((n_ch, push), dtype=torch.float32).pin_memory() for _ in range(2)]
+    xs = np.empty((len(rows), n), np.float32)
+    ys, ts = [], []
+    for k in range(n // push):
+        h = host[k % 2]
+        h.copy_(cfg5_push_block(k, n_ch, push, fs, rows, dev))
+        xs[:, k * push:(k + 1) * push] = h[rows].numpy()
+        o = st.push(h, T0 + k * push * dt_ns)
+        if o.n_out:
+            ys.append(st.fetch())  # also frees the pinned buffer
+            ts.append(o.times_ns)
+        else:
+            st.wait_copy()
+    o = st.flush()
+    if o.n_out:
+        ys.append(st.fetch())
+        ts.append(o.times_ns)
+    st.close()
+    y = np.concatenate(ys, axis=1)
+    ref = oracle.lfproc_process(xs, T0, dt_ns, T0, t_end, 10.0, 120, 6)
+    np.testing.assert_array_equal(np.concatenate(ts), np.concatenate([t for t, _ in ref]))
+    want = np.concatenate([r for _, r in ref], axis=1)
+    assert y.shape == (n_ch, want.shape[1]) and want.shape[1] == 257
+    assert _rel(y[rows], want) < 1e-4
+    mask = np.ones(n_ch, bool)
+    mask[rows] = False
+    expect = (np.arange(n_ch, dtype=np.float32) * np.float32(1e-3) + np.float32(100.0)).astype(np.float64)
+    dc = y[mask].astype(np.float64)
+    assert float(np.max(np.abs(dc - expect[mask, None]) / expect[mask, None])) < 1e-6
+    torch.cuda.empty_cache()
+
+
 def test_cfg4_edge_full_width_sampled_channels():
     """cfg4 (2,000 ch @ 2 kHz, 30 s pushes) through the edge stream, a sample
     of channels against the oracle's notebook loop."""

@@ -116,6 +116,27 @@ def test_stream_gap_and_config_errors():
         ST.LowpassStream(2, 4_000_000, 1.0, 40, 6, mode="continuous", dry_run=True)
 
 
+def test_stream_merge_rule_matches_chunk_merge():
+    """Pushes follow Spool.chunk(time=None)'s merge rule (tolerance 1.5
+    samples): a duplicated boundary sample is dropped, a first sample up to
+    1.5 intervals after the last one continues the sample grid, more is a gap."""
+    dt = 4_000_000
+    s = ST.LowpassStream(2, dt, 1.0, 40, 6, dry_run=True, t_start=T0)
+    s.push(np.zeros((2, 100), np.float32), T0)
+    assert s.info()[1] == 100
+    s.push(np.zeros((2, 100), np.float32), T0 + 99 * dt)  # first sample duplicates the last
+    assert s.info()[1] == 199
+    s.push(np.zeros((2, 100), np.float32), T0 + 199 * dt + dt // 5)  # 1.2-sample gap: merged
+    assert s.info()[1] == 299
+    s.push(np.zeros((2, 10), np.float32), T0 + 298 * dt + 3 * dt // 2)  # exactly 1.5: merged
+    assert s.info()[1] == 309
+    with pytest.raises(ValueError, match="patch merge failed! Gap in data exists"):
+        s.push(np.zeros((2, 10), np.float32), T0 + 308 * dt + 3 * dt // 2 + 1)
+    with pytest.raises(ValueError, match="patch merge failed! Gap in data exists"):
+        s.push(np.zeros((2, 10), np.float32), T0 + 300 * dt)  # overlap
+    s.close()
+
+
 # ---------------------------------------------------------------- GPU ---
 def _edge_gpu(x, case, time_axis=1, pinned=False):
     import torch
