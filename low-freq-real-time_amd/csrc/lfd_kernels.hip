@@ -1055,35 +1055,36 @@ __global__ __launch_bounds__(256) void k_rolling_cols(
 // summed directly (a halo of W samples per segment: segments are >= 4W).
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_rolling_scan_tc(
-    const float *__restrict__ x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t W,
-    int64_t S, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int64_t seg_out, bool vec_out) {
-  const int64_t n_out = (n_t + S - 1) / S;
-  const int64_t n_seg = (n_out + seg_out - 1) / seg_out;
-  const int64_t n_units = n_seg * n_ch;
+    const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
+    float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out) {
+  // positions are row-relative int32 (the launcher checks n_t < 2^31 - 512)
+  const int n_out = (n_t + S - 1) / S;
+  const int n_seg = (n_out + seg_out - 1) / seg_out;
+  const int64_t n_units = (int64_t)n_seg * n_ch;
   const int lane = threadIdx.x & 63;
   const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const float nanv = __builtin_nanf("");
-  const int64_t k_first = (W - 1 + S - 1) / S;
+  const int k_first = (W - 1 + S - 1) / S;
   const double inv_w = 1.0 / (double)W;
   for (int64_t u = uniform64(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); u < n_units;
        u += n_waves) {
-    const int64_t useg = u % n_seg;
+    const int useg = (int)(u % n_seg);
     const int64_t ch = u / n_seg;
-    const int64_t k0 = useg * seg_out;
-    const int64_t k1 = min(n_out, k0 + seg_out);
+    const int k0 = useg * seg_out;
+    const int k1 = min(n_out, k0 + seg_out);
     const float *row = x + ch * s_ch;
     float *yo = y + ch * ys_ch;
-    int64_t ka = k0 > k_first ? k0 : k_first;
-    for (int64_t k = k0 + lane; k < k1 && k < k_first; k += 64) yo[k * ys_t] = nanv;
+    const int ka = k0 > k_first ? k0 : k_first;
+    for (int k = k0 + lane; k < k1 && k < k_first; k += 64) yo[k * ys_t] = nanv;
     if (ka >= k1) continue;
-    const int64_t p0 = ka * S, p1 = (k1 - 1) * S;  // output positions [p0, p1]
+    const int p0 = ka * S, p1 = (k1 - 1) * S;  // output positions [p0, p1]
     // Wsum(p0 - 1): window [p0 - W, p0 - 1] (x[-1] = 0 when p0 = W - 1)
     double carry = 0.0;
-    int64_t ccnt = 0;
+    int ccnt = 0;
     {
       double acc = 0.0;
       int cnt = 0;
-      for (int64_t m = p0 - W + lane; m < p0; m += 64) {
+      for (int m = p0 - W + lane; m < p0; m += 64) {
         if (m < 0) continue;
         const float v = row[m];
         const bool f = __builtin_isfinite(v);
@@ -1095,41 +1096,48 @@ __global__ __launch_bounds__(256) void k_rolling_scan_tc(
       for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
       ccnt = cnt;
     }
-    // tiles of 256 positions from the 4-aligned position at or below p0
-    const int64_t tb0 = VEC ? (p0 & ~(int64_t)3) : p0;
-    const int64_t step_mod = 256 % S;
-    int64_t ph = (tb0 + 4 * lane) % S;  // phase of this lane's first position
-    for (int64_t tb = tb0; tb <= p1; tb += 256) {
-      const int64_t t = tb + 4 * lane;
+    // tiles of 256 positions from the 4-aligned position at or below p0; the
+    // next tile's loads are in flight while the current one is scanned (two
+    // static register buffers: moving prefetched registers would wait)
+    const int tb0 = VEC ? (p0 & ~3) : p0;
+    const int step_mod = 256 % S;
+    int ph = (tb0 + 4 * lane) % S;  // phase of this lane's first position
+    struct Tile {
       float xi[4], xo[4];
+    };
+    auto load = [&](int tb, Tile &T) {
+      const int t = tb + 4 * lane;
       const bool full = tb + 256 <= n_t && tb - W >= 0;
       if (VEC && full) {
         const f4v a = *reinterpret_cast<const f4v *>(row + t);
-        xi[0] = a.x, xi[1] = a.y, xi[2] = a.z, xi[3] = a.w;
+        T.xi[0] = a.x, T.xi[1] = a.y, T.xi[2] = a.z, T.xi[3] = a.w;
         if ((W & 3) == 0) {
           const f4v b = *reinterpret_cast<const f4v *>(row + t - W);
-          xo[0] = b.x, xo[1] = b.y, xo[2] = b.z, xo[3] = b.w;
+          T.xo[0] = b.x, T.xo[1] = b.y, T.xo[2] = b.z, T.xo[3] = b.w;
         } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) xo[e] = row[t + e - W];
+          for (int e = 0; e < 4; ++e) T.xo[e] = row[t + e - W];
         }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int64_t ti = t + e;
-          xi[e] = ti < n_t ? row[ti] : 0.0f;
-          xo[e] = (ti - W >= 0 && ti < n_t) ? row[ti - W] : 0.0f;
+          const int ti = t + e;
+          T.xi[e] = ti < n_t ? row[ti] : 0.0f;
+          T.xo[e] = (ti - W >= 0 && ti < n_t) ? row[ti - W] : 0.0f;
         }
       }
+    };
+    auto process = [&](int tb, const Tile &T) {
+      const int t = tb + 4 * lane;
       double d[4];
       int c[4];
       bool anynf = false;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t ti = t + e;
+        const int ti = t + e;
         const bool in = ti >= p0 && ti <= p1;
-        const bool fi = __builtin_isfinite(xi[e]), fo = __builtin_isfinite(xo[e]);
-        d[e] = in ? (fi ? (double)xi[e] : 0.0) - (fo ? (double)xo[e] : 0.0) : 0.0;
+        const bool fi = __builtin_isfinite(T.xi[e]), fo = __builtin_isfinite(T.xo[e]);
+        d[e] = in ? (fi ? (double)T.xi[e] : 0.0) - (fo ? (double)T.xo[e] : 0.0) : 0.0;
         c[e] = in ? (int)!fi - (int)!fo : 0;
         anynf |= in && (!fi || !fo);
       }
@@ -1147,8 +1155,7 @@ __global__ __launch_bounds__(256) void k_rolling_scan_tc(
       const double tot = __shfl(v, 63, 64);
       // non-finite counts only when this step or the carried window has one
       int cc[4] = {0, 0, 0, 0};
-      const bool need_cnt = __any(anynf) || ccnt != 0;
-      if (need_cnt) {
+      if (__any(anynf) || ccnt != 0) {
         c[1] += c[0];
         c[2] += c[1];
         c[3] += c[2];
@@ -1158,32 +1165,51 @@ __global__ __launch_bounds__(256) void k_rolling_scan_tc(
           const int w_ = __shfl_up(vc, o, 64);
           if (lane >= o) vc += w_;
         }
-        const int64_t ex = ccnt + (vc - c[3]);
+        const int ex = ccnt + (vc - c[3]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) cc[e] = (int)(ex + c[e]);
+        for (int e = 0; e < 4; ++e) cc[e] = ex + c[e];
         ccnt += __shfl(vc, 63, 64);
       }
       float o4[4];
       bool is_out[4];
+      bool direct = false;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t ti = t + e;
-        int64_t pe = ph + e;
+        const int ti = t + e;
+        int pe = ph + e;
         while (pe >= S) pe -= S;  // at most 3 subtractions (ph < S, e < 4)
         is_out[e] = ti >= p0 && ti <= p1 && pe == 0;
         o4[e] = (float)((excl + d[e]) * inv_w);
-        if (is_out[e] && cc[e] != 0) o4[e] = window_direct(row, ti, W, 1);
+        direct |= is_out[e] && cc[e] != 0;
+      }
+      if (__any(direct)) {  // windows holding a null: numpy's mean of the raw values
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (is_out[e] && cc[e] != 0) o4[e] = window_direct(row, t + e, W, 1);
       }
       if (S == 1 && vec_out && is_out[0] && is_out[3]) {
         *reinterpret_cast<f4v *>(yo + t) = f4v{o4[0], o4[1], o4[2], o4[3]};
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (is_out[e]) yo[((t + e) / S) * ys_t] = o4[e];
+          if (is_out[e]) yo[(int64_t)((t + e) / S) * ys_t] = o4[e];
       }
       carry += tot;
       ph += step_mod;
       ph = ph >= S ? ph - S : ph;
+    };
+    Tile A, B;
+    int tb = tb0;
+    load(tb, A);
+    while (true) {
+      if (tb + 256 <= p1) load(tb + 256, B);
+      process(tb, A);
+      tb += 256;
+      if (tb > p1) break;
+      if (tb + 256 <= p1) load(tb + 256, A);
+      process(tb, B);
+      tb += 256;
+      if (tb > p1) break;
     }
   }
 }
@@ -1983,7 +2009,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     k_rolling_tc<<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y,
                                                    ys_ch, ys_t, vec);
-  } else if (s_t == 1) {
+  } else if (s_t == 1 && n_t < (int64_t)INT32_MAX - 512 && W < INT32_MAX / 2) {
     // overlapping windows: running sum over segments of >= max(32768, 4W)
     // positions (halo W per segment), fewer when that leaves the chip idle
     int64_t seg_pos = std::max<int64_t>(32768, 4 * W);
@@ -1996,11 +2022,11 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
     const bool vec_out = vec && ys_t == 1 && ys_ch % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
     if (vec)
-      k_rolling_scan_tc<true><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y, ys_ch, ys_t,
-                                                                seg_out, vec_out);
+      k_rolling_scan_tc<true><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch,
+                                                                ys_t, (int)seg_out, vec_out);
     else
-      k_rolling_scan_tc<false><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y, ys_ch, ys_t,
-                                                                 seg_out, false);
+      k_rolling_scan_tc<false><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch,
+                                                                 ys_t, (int)seg_out, false);
   } else {
     const int64_t seg_out = S >= W ? 64 : std::max<int64_t>(1, std::max<int64_t>(4096, 4 * W) / S);
     const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);

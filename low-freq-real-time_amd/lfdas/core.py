@@ -380,8 +380,16 @@ class Spool:
 
     def chunk(self, time=None, overlap=None, keep_partial=False, tolerance=1.5):
         """``chunk(time=None)``: merge time-contiguous patches (lf_das.py:239,
-        265); ``chunk(time=T, overlap=O)``: windows of T seconds stepping by
-        T - O (the north-star surface of LFProc's schedule)."""
+        265); ``chunk(time=T, overlap=O)``: windows ``[start, start + T)`` of
+        each merged patch, ``start`` stepping by ``T - O`` from its first
+        sample; a last window running past the data is dropped unless
+        ``keep_partial`` (then it ends at the last sample).  With
+        ``T = P dt`` and ``O = 2 B dt`` these are LFProc's chunks
+        (lf_das.py:236-240, 264-266) up to the inclusive end
+        sample.  The windows of one merged patch share a chunk group:
+        ``pass_filter(...).interpolate(...)`` requests made on them are
+        computed together, as one device plan over the merged samples, when
+        the first of them is read (lfdas.proc)."""
         pats = sorted(self._patches, key=lambda p: p.coords["time"][0])
         merged = []
         for p in pats:
@@ -396,17 +404,19 @@ class Spool:
         O = to_timedelta64(overlap or 0)
         if O >= T:
             raise ValueError("overlap must be smaller than the chunk length")
+        from .proc import ChunkGroup
         res = []
         for p in out:
             t = p.coords["time"]
+            group = ChunkGroup(p)
             start = t[0]
             while True:
                 stop = start + T
                 if stop > t[-1] + p.attrs["time_step"]:
                     if keep_partial and start <= t[-1]:
-                        res.append(p.select(time=(start, t[-1])))
+                        res.append(group.window(start, t[-1]))
                     break
-                res.append(p.select(time=(start, stop - np.timedelta64(1, "ns"))))
+                res.append(group.window(start, stop - np.timedelta64(1, "ns")))
                 start = stop - O
         return Spool(res, self._source)
 

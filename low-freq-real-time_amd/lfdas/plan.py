@@ -13,6 +13,16 @@ import numpy as np
 from . import _lib
 from ._lib import check, load
 
+# device launches of the low-pass path issued through this module (a plan
+# execute, a one-shot fused call or a full-rate filter each count 1) — lets
+# tests see how many passes a Python-level workflow turned into
+launch_count = 0
+
+
+def _count():
+    global launch_count
+    launch_count += 1
+
 
 def _ptr(a) -> int:
     """Device pointer of a torch tensor (or None)."""
@@ -102,6 +112,7 @@ class LowpassPlan:
             raise ValueError(f"y shape {tuple(y.shape)} != {(self.n_ch, self.n_grid)}")
         if workspace.numel() * workspace.element_size() < self.workspace_bytes:
             raise ValueError("workspace too small")
+        _count()
         check(self._lib.lfd_lowpass_execute(
             self._h, _ptr(x), x.stride(0), x.stride(1), _ptr(y), y.stride(0), y.stride(1),
             _ptr(workspace), _stream_ptr(stream)))
@@ -179,6 +190,7 @@ def sosfiltfilt_device(x, sos, padlen: int = -1, stream=None):
     wsb = lib.lfd_sosfiltfilt_workspace_bytes(n_ch, n_t, int(padlen), sos.shape[0])
     ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=x.device)
     y = torch.empty((n_ch, n_t), dtype=torch.float64, device=x.device)
+    _count()
     check(lib.lfd_sosfiltfilt_f32(_ptr(x), n_ch, n_t, x.stride(0), x.stride(1), sos.ctypes.data,
                                   sos.shape[0], int(padlen), _ptr(y), y.stride(0), y.stride(1),
                                   _ptr(ws), _stream_ptr(stream)))
@@ -210,6 +222,7 @@ def filtfilt_resample_device(x, sos, lo, w, padlen: int = -1, stream=None):
     w = np.ascontiguousarray(w, dtype=np.float64)
     n_ch, n_t = x.shape
     y = torch.empty((n_ch, len(lo)), dtype=torch.float32, device=x.device)
+    _count()
     check(lib.lfd_sos_filtfilt_resample_f32(
         _ptr(x), n_ch, n_t, x.stride(0), x.stride(1), sos.ctypes.data, sos.shape[0], int(padlen),
         lo.ctypes.data, w.ctypes.data, len(lo), _ptr(y), y.stride(0), y.stride(1),

@@ -108,6 +108,110 @@ def _positions(patch: Patch, new_times):
     return lo, w
 
 
+class ChunkGroup:
+    """The windows ``Spool.chunk(time=T, overlap=O)`` cut from one merged
+    patch (the reference's overlapping LFProc chunks, lf_das.py:236-240).
+    ``window`` returns a window patch that remembers its sample range in the
+    parent.  ``pass_filter(...).interpolate(...)`` on such windows registers a
+    request here instead of computing at once; reading any of them computes
+    every request registered so far together — one ``LowpassPlan`` execute
+    over the parent's samples, each window a chunk of the plan (overlapping
+    samples read from HBM once) — when their output grids interleave into one
+    uniform grid, else one fused call per window."""
+
+    def __init__(self, parent: Patch):
+        self.parent = parent
+        self.t_ns = parent.sample_times_ns()
+        self.pending = []
+        self.results = {}
+
+    def window(self, start, stop) -> Patch:
+        """Inclusive time window [start, stop] of the parent."""
+        p = self.parent.select(time=(start, stop))
+        tw = p.sample_times_ns()
+        if len(tw):
+            s0 = int(np.searchsorted(self.t_ns, tw[0]))
+            p._chunk_window = (self, s0, s0 + len(tw) - 1)
+        return p
+
+    def request(self, window, sos, padlen, lo, w, dims, shape):
+        req = _GroupResample(self, window, sos, padlen, lo, w, dims, shape)
+        self.pending.append(req)
+        return req
+
+    def _run(self, req):
+        batch = [r for r in self.pending
+                 if r.padlen == req.padlen and np.array_equal(r.sos, req.sos)]
+        self.pending = [r for r in self.pending if r not in batch]
+        done = self._run_batched(batch) if len(batch) > 1 else False
+        if not done:
+            for r in batch:
+                self.results[r] = r.compute_alone()
+
+    def _run_batched(self, batch) -> bool:
+        """One plan over the parent for every request of ``batch``; False
+        when their grids do not form one uniform, non-overlapping grid."""
+        from ._lib import LFDUnsupported
+        from .plan import LowpassPlan
+        batch = sorted(batch, key=lambda r: (int(r.lo[0]) + float(r.w[0])) if len(r.lo) else np.inf)
+        if any(len(r.lo) == 0 for r in batch):
+            return False
+        lo = np.concatenate([r.lo + r.s0 for r in batch])
+        w = np.concatenate([r.w for r in batch])
+        pos = lo + w
+        if np.any(np.diff(pos) <= 0):
+            return False  # overlapping output grids: windows would write one column twice
+        chunks, g = [], 0
+        for r in batch:
+            chunks.append((r.s0, r.s1, g, g + len(r.lo)))
+            g += len(r.lo)
+        n_t = len(self.t_ns)
+        try:
+            plan = LowpassPlan(batch[0].sos, _n_channels(self.parent), n_t, lo, w, chunks, batch[0].padlen)
+        except (LFDUnsupported, ValueError):
+            return False
+        import torch
+        x = to_device_ct(self.parent)
+        y = torch.empty((x.shape[0], len(lo)), dtype=torch.float32, device=x.device)
+        plan.execute(x, y, plan.alloc_workspace(x.device))
+        plan.close()
+        yh = y.cpu().numpy()
+        for r, (_, _, g0, g1) in zip(batch, chunks):
+            seg = yh[:, g0:g1].astype(np.float64)
+            self.results[r] = seg.T.copy() if r.dims.index("time") == 0 else seg
+        return True
+
+
+def _n_channels(patch: Patch) -> int:
+    return int(np.prod([n for d, n in zip(patch.dims, patch.shape) if d != "time"]))
+
+
+class _GroupResample:
+    """A pending ``pass_filter(...).interpolate(...)`` of one chunk window."""
+
+    def __init__(self, group, window, sos, padlen, lo, w, dims, shape):
+        self.group = group
+        self.window = window
+        _, self.s0, self.s1 = window._chunk_window
+        self.sos = np.ascontiguousarray(sos, dtype=np.float64)
+        self.padlen = int(padlen)
+        self.lo = np.asarray(lo, np.int64)
+        self.w = np.asarray(w, np.float64)
+        self.dims = tuple(dims)
+        self.shape = tuple(shape)
+
+    def compute_alone(self):
+        from .plan import filtfilt_resample_device
+        x = to_device_ct(self.window)
+        y = filtfilt_resample_device(x, self.sos, self.lo, self.w, self.padlen)
+        return _from_ct(y, self.dims).astype(np.float64)
+
+    def materialize(self, patch: Patch):
+        if self not in self.group.results:
+            self.group._run(self)
+        return self.group.results.pop(self)
+
+
 def interpolate(patch: Patch, kind="linear", **kwargs):
     if kind != "linear":
         raise NotImplementedError("only linear interpolation is on the device path")
@@ -121,6 +225,13 @@ def interpolate(patch: Patch, kind="linear", **kwargs):
     coords = dict(patch.coords.coord_map)
     coords["time"] = new
     lazy = patch._lazy
+    cw = getattr(lazy.src, "_chunk_window", None) if isinstance(lazy, _LazyFiltfilt) else None
+    if cw is not None:
+        # a Spool.chunk window: computed with its siblings on first read
+        shape = list(patch.shape)
+        shape[patch.dims.index("time")] = len(new)
+        req = cw[0].request(lazy.src, lazy.sos, lazy.padlen, lo, w, patch.dims, shape)
+        return Patch(data=None, coords=coords, dims=patch.dims, attrs=patch._attrs_wo_coords(), _lazy=req)
     if isinstance(lazy, _LazyFiltfilt):
         from .plan import filtfilt_resample_device
         x = to_device_ct(lazy.src)

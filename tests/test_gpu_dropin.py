@@ -158,3 +158,49 @@ def test_get_edge_effect_time_matches_oracle():
     assert abs(e - e_ref) < 1e-9
     with pytest.raises(ValueError):
         lf_das.get_edge_effect_time(sampling_interval=1 / 200.0, total_T=20.8, tol=1e-3, freq=0.1)
+
+
+def test_spool_chunk_windows_reproduce_lfproc_in_one_plan():
+    """LFProc's schedule is Spool.chunk(time=P dt, overlap=2B dt)
+    trimmed by B dt per side.  The windows' pass_filter().interpolate() at the
+    trimmed grid reproduce LFProc's outputs and the oracle, and the whole
+    list runs as ONE plan execute over the merged samples."""
+    import lf_das
+    import lfdas.dc as dc
+    from lfdas import plan as PL
+    from lfdas import schedule as S
+    sp = _example_spool()
+    P, B, dt = 40, 6, 0.2
+    t1, t2 = np.datetime64("2017-09-18T00:00:00", "ns"), np.datetime64("2017-09-18T00:00:24", "ns")
+    tg = S.time_grid(t1, t2, dt)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    windows = sp.chunk(time=P * dt, overlap=2 * B * dt, keep_partial=True)
+    assert len(windows) == len(sched) == 4
+    fc = 1 / dt / 2 * 0.9
+    n0 = PL.launch_count
+    outs = [w.pass_filter(time=(None, fc)).interpolate(time=tg[oa:ob].astype("datetime64[ns]"))
+            for w, (_, _, oa, ob) in zip(windows, sched)]
+    assert PL.launch_count == n0  # nothing computed yet
+    datas = [o.data for o in outs]
+    assert PL.launch_count == n0 + 1  # one plan execute for every window
+    lfp = lf_das.LFProc(sp, verbose=False, write_files=False)
+    lfp.update_processing_parameter(output_sample_interval=dt, process_patch_size=P, edge_buff_size=B)
+    lfp.process_time_range(t1, t2)
+    x = dc.spool(sp).chunk(time=None)[0]
+    tx = x.sample_times_ns()
+    xd = np.asarray(x.data, np.float32)
+    for d, o, w, ref_lp, (_, _, oa, ob) in zip(datas, outs, windows, lfp.outputs, sched):
+        np.testing.assert_array_equal(o.coords["time"].astype(np.int64), tg[oa:ob])
+        assert _rel(d, ref_lp.data) < 1e-4  # the §3.1 equivalence
+        # the window's own semantics: sosfiltfilt of exactly its samples, then interp1d
+        _, s0, s1 = w._chunk_window
+        yf = oracle.sosfiltfilt(oracle.butter_sos(4, fc / 125.0), xd[:, s0:s1 + 1])
+        want = oracle.interpolate(yf, -1, tx[s0:s1 + 1], tg[oa:ob])
+        assert _rel(d, want) < 1e-4
+    # overlapping output grids cannot share one plan: one fused call each
+    n1 = PL.launch_count
+    outs2 = [windows[0].pass_filter(time=(None, fc)).interpolate(time=windows[0].coords["time"][1500:1510]),
+             windows[1].pass_filter(time=(None, fc)).interpolate(time=windows[1].coords["time"][0:10])]
+    for o in outs2:
+        assert o.data.shape == (300, 10)
+    assert PL.launch_count == n1 + 2

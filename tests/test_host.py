@@ -242,3 +242,38 @@ def test_units_and_coordinate_derived_time_step():
     half = [q.select(time=(None, q.coords["time"][19])), q.select(time=(q.coords["time"][20], None))]
     merged = dc.spool(half).chunk(time=None)
     assert len(merged) == 1 and merged[0].shape == q.shape
+
+
+def test_spool_chunk_windows_and_keep_partial():
+    """Spool.chunk(time=T, overlap=O): windows [start, start + T) stepping by
+    T - O from the merged patch's first sample; the last window past the
+    data is dropped unless keep_partial (then it ends at the last sample).
+    T = P dt, O = 2 B dt start exactly where LFProc's chunks start."""
+    import lfdas.dc as dc
+    sp = dc.get_example_spool()  # 3 x 2000 samples @ 250 Hz, contiguous: 24 s
+    P, B, dt = 40, 6, 0.2
+    for keep in (False, True):
+        ch = sp.chunk(time=P * dt, overlap=2 * B * dt, keep_partial=keep)
+        t0 = sp[0].coords["time"][0]
+        starts = [(c.coords["time"][0] - t0) / np.timedelta64(1, "ms") for c in ch]
+        ends = [(c.coords["time"][-1] - t0) / np.timedelta64(1, "ms") for c in ch]
+        assert starts == [0, 5600, 11200, 16800][: len(ch)]
+        assert ends[:3] == [7996, 13596, 19196]
+        assert len(ch) == (4 if keep else 3)
+        if keep:
+            assert ends[3] == 23996  # the partial last window ends at the last sample
+        for c in ch:
+            assert c.shape[0] == 300
+            grp, s0, s1 = c._chunk_window
+            assert s1 - s0 + 1 == c.shape[1]
+    # LFProc's schedule on the same spool starts its chunks at the same samples
+    tg = S.time_grid(sp[0].coords["time"][0], sp[-1].coords["time"][-1], dt)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    np.testing.assert_array_equal([tg[a] for a, _, _, _ in sched],
+                                  [c.coords["time"][0].astype(np.int64) for c in
+                                   sp.chunk(time=P * dt, overlap=2 * B * dt, keep_partial=True)])
+    with pytest.raises(ValueError, match="overlap"):
+        sp.chunk(time=1.0, overlap=1.0)
+    # a gap splits the merged patches: windows never straddle it
+    gapped = dc.get_example_spool(time_gap=2.0).chunk(time=4.0, overlap=1.0)
+    assert all((c.coords["time"][-1] - c.coords["time"][0]) < np.timedelta64(4, "s") for c in gapped)
