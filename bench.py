@@ -116,7 +116,8 @@ def build_plan(n_ch, n, fs, dt_out, P, B, off_ns=0):
     return LowpassPlan(sos, n_ch, n, lo, w, chunks), sched, sos, t0, dt_ns, tg
 
 
-K1_KERNELS = {"mfma_runs": "k_block_runs_mfma", "mfma": "k_block_functionals_mfma",
+K1_KERNELS = {"mfma_runs": "k_block_runs_mfma", "mfma_runs_tm": "k_block_runs_mfma_tm",
+              "mfma": "k_block_functionals_mfma",
               "mfma_fold": "k_block_functionals_mfma + k_fold_runs",
               "recurrence": "k_block_functionals_lds|gen",
               "recurrence_fold": "k_block_functionals_lds|gen + k_fold_runs"}

@@ -106,6 +106,9 @@ int lfd_set_timing(int enable);
  * separate fold kernel turns them into runs before the scan. */
 #define LFD_K1_RECURRENCE_FOLD 4
 #define LFD_K1_MFMA_FOLD 5
+/* (time, channel) rows (s_ch == 1, the real files' layout): fp64 MFMA over
+ * 32-channel row lines, in-register run folding (4th-order cascades). */
+#define LFD_K1_MFMA_RUNS_TM 6
 int lfd_lowpass_last_kernel(const lfd_lowpass_plan *plan);
 /* Testing hook: the plan's block taps Kx[n_comp][row_len] in natural layout,
  * F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p] (row_len = L + J).  With

@@ -554,6 +554,8 @@ struct lfd_lowpass_plan {
   std::vector<double> taps;      // natural layout [nc][L+J]
   lfd::TapGeom tg{};
   double *d_taps = nullptr;      // device layout (lfd_internal.h TapGeom)
+  lfd::TapGeom tg_tm{};          // (time, channel) rows: one table, row shift 0
+  double *d_taps_tm = nullptr;
   // run mode (lfd_internal.h RunConst): run table, K1 units, constants
   bool run_ok = false;       // run table + constants (4th-order cascades)
   bool run_mfma_ok = false;  // taps + 16 run buffers fit LDS: k_block_runs_mfma
@@ -730,6 +732,15 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     p->run_mfma_ok = !p->taps.empty() &&
         sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 8 * lfd::RUN_R * 5 * 16) <=
             (size_t)lfd::TAP_LDS_MAX;
+    // (time, channel) rows: k_block_runs_mfma_tm reads each block row from
+    // its first sample (no 16-B shift): one table, shift 0; its 512-thread
+    // workgroup holds 8 waves x 2 channel tiles of run buffers
+    if (!p->taps.empty()) {
+      const int row = (int)(p->taps.size() / p->tg.nc);
+      const int Lp_tm = (row + 63) / 64 * 64;
+      if (sizeof(double) * ((size_t)Lp_tm * p->tg.nc + 64 + 8 * 2 * lfd::RUN_R * 5 * 16) <= (size_t)lfd::TAP_LDS_MAX)
+        p->tg_tm = lfd::TapGeom{Lp_tm, p->tg.J, p->tg.nc, 1, 0};
+    }
     std::vector<int64_t> cuts = {0, p->bg.nb};
     for (const auto &G : p->chunks) {
       cuts.push_back(G.kb);
@@ -809,9 +820,8 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   if (e == hipSuccess)
     e = hipMemcpy(p->d_chunks, p->chunks.data(), sizeof(lfd::ChunkGeom) * n_chunks,
                   hipMemcpyHostToDevice);
-  if (e == hipSuccess && !p->taps.empty()) {
-    // device layout (lfd_internal.h TapGeom): one table per row shift v
-    const lfd::TapGeom &tg = p->tg;
+  // device layout (lfd_internal.h TapGeom): one table per row shift v
+  auto upload_taps = [&](const lfd::TapGeom &tg, double **dst) {
     const int row = (int)(p->taps.size() / tg.nc);
     const size_t tab = (size_t)tg.Lp * tg.nc;
     std::vector<double> dev(tab * tg.nvar, 0.0);
@@ -827,10 +837,13 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
                     p->taps[(size_t)cc * row + pos];
             }
     }
-    e = hipMalloc(&p->d_taps, dev.size() * sizeof(double));
-    if (e == hipSuccess)
-      e = hipMemcpy(p->d_taps, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice);
-  }
+    hipError_t e2 = hipMalloc(dst, dev.size() * sizeof(double));
+    if (e2 == hipSuccess)
+      e2 = hipMemcpy(*dst, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice);
+    return e2;
+  };
+  if (e == hipSuccess && !p->taps.empty()) e = upload_taps(p->tg, &p->d_taps);
+  if (e == hipSuccess && p->tg_tm.Lp > 0) e = upload_taps(p->tg_tm, &p->d_taps_tm);
   if (e == hipSuccess && p->run_ok) {
     e = hipMalloc(&p->d_run_ks, sizeof(int64_t) * p->run_ks.size());
     if (e == hipSuccess) e = hipMalloc(&p->d_run_len, sizeof(int) * p->run_len.size());
@@ -880,13 +893,18 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   p->timed = timed;
   if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
+  const bool rec = env_flag("LFD_K1_REC");
   const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
-                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !env_flag("LFD_K1_REC");
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !rec;
   const bool runs = p->run_ok && !env_flag("LFD_NO_RUNS");
   const bool mfma_runs = runs && mfma && p->run_mfma_ok;
+  // (time, channel) rows (the real files' layout): the time-major MFMA kernel
+  const bool mfma_tm = runs && !mfma && p->d_taps_tm && (s_ch == 1 || p->n_ch == 1) && s_t > 1 &&
+                       s_t >= p->n_ch && !rec;
   p->last_k1 = mfma_runs ? LFD_K1_MFMA_RUNS
-                         : runs ? (mfma ? LFD_K1_MFMA_FOLD : LFD_K1_RECURRENCE_FOLD)
-                                : (mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE);
+               : mfma_tm ? LFD_K1_MFMA_RUNS_TM
+               : runs    ? (mfma ? LFD_K1_MFMA_FOLD : LFD_K1_RECURRENCE_FOLD)
+                         : (mfma ? LFD_K1_MFMA : LFD_K1_RECURRENCE);
   if (runs) {
     const lfd::RunGeom rg{(int64_t)p->run_ks.size(), (int64_t)p->group_r0.size() - 1, p->n_sr,
                           p->d_run_ks, p->d_run_len, p->d_group_r0, p->d_rc};
@@ -895,6 +913,8 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
     double *SR = reinterpret_cast<double *>(ws + p->off_SR);
     if (mfma_runs) {
       LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
+    } else if (mfma_tm) {
+      LFD_HIP(lfd::launch_block_runs_mfma_tm(x, s_t, p->n_t, p->bg, p->d_taps_tm, p->tg_tm, rg, Y0, AG, st));
     } else {
       if (mfma)
         LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, F, st));
@@ -989,6 +1009,7 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   if (!p) return;
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);
+  if (p->d_taps_tm) (void)hipFree(p->d_taps_tm);
   for (void *d : {(void *)p->d_run_ks, (void *)p->d_run_len, (void *)p->d_group_r0, (void *)p->d_rc})
     if (d) (void)hipFree(d);
   for (auto &e : p->ev)

@@ -164,6 +164,11 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
 hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
                                   double *Y0, double *AG, hipStream_t st);
+// Run-mode MFMA K1 for (time, channel) storage (s_ch == 1, row stride s_t):
+// tap table with row shift 0 (tg.nvar == 1, tg.v0 == 0).
+hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
+                                     const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
+                                     double *AG, hipStream_t st);
 // Run epilogue applied to per-block functionals F (K1 kernels without run
 // mode): F -> Y0, AG (n_sec == 2).
 hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,

@@ -1047,21 +1047,49 @@ __global__ __launch_bounds__(256) void k_rolling_cols(
 }
 
 // Time-contiguous rows, step < window: one wave per (channel, segment of
-// outputs).  A wave step covers 256 consecutive positions (4 per lane,
-// float4 loads when the row and W allow): per position d = m(x[t]) -
-// m(x[t-W]) in float64, a lane-local prefix, a wave exclusive scan of the
-// lane totals (__shfl_up) and the carried window sum give Wsum at all 256
-// positions; outputs are the positions t = kS.  The segment's first window is
-// summed directly (a halo of W samples per segment: segments are >= 4W).
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_rolling_scan_tc(
+// outputs).  A wave step covers RS_P = 512 consecutive positions, each lane
+// RS_E = 8 CONSECUTIVE ones (two float4 loads of x[t] and two of the sample
+// leaving the window, x[t - W], an L1/L2 re-read).  Per lane: d = x[t] -
+// x[t-W] in float64 and a sequential running sum over its 8 positions; one
+// wave exclusive scan of the lane totals per step gives each lane its entry
+// window sum.  Outputs are the positions t = kS.  Steps inside the output
+// range whose window holds no null take a fast path (no masks, no range
+// tests: a null makes the lane total non-finite, which sends the step to
+// the general path).  The segment's first window is summed directly (a halo
+// of W samples per segment: segments are >= 4W).
+constexpr int RS_E = 8;             // positions per lane per step
+constexpr int RS_P = 64 * RS_E;     // positions per wave step
+// Null bookkeeping of the running sum: each sample contributes a packed code
+// (NaN: 1, +inf: 2^21, -inf: 2^42; finite: 0); a window's summed code holds
+// its NaN / +inf / -inf counts (W < 2^21).  numpy's mean over such a window:
+// NaN if it holds a NaN or both infinities, else the infinity it holds.
+__device__ __forceinline__ int64_t null_code(float v) {
+  return __builtin_isfinite(v) ? 0 : (v != v ? 1 : (v > 0.0f ? (int64_t)1 << 21 : (int64_t)1 << 42));
+}
+__device__ __forceinline__ float null_mean(int64_t code, float mean) {
+  const int64_t n_nan = code & ((1 << 21) - 1), n_pinf = (code >> 21) & ((1 << 21) - 1), n_ninf = code >> 42;
+  if (n_nan || (n_pinf && n_ninf)) return __builtin_nanf("");
+  if (n_pinf) return __builtin_inff();
+  if (n_ninf) return -__builtin_inff();
+  return mean;
+}
+
+// STAGE (A/B knob LFD_ROLL_STAGE): bit 0 = loads are coalesced float4 (lane
+// 4l + 256j) staged through a wave-private LDS tile into lane-consecutive
+// order; bit 1 = S == 1 outputs leave through LDS the same way (coalesced
+// float4 stores); else lanes load / store their 8 positions directly.
+constexpr int RS_ROW = RS_E + 4;    // padded LDS row (floats): conflict-free ds_read_b128
+template <bool VEC, int STAGE>
+__global__ __launch_bounds__(256, 3) void k_rolling_scan_tc(
     const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
     float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out) {
-  // positions are row-relative int32 (the launcher checks n_t < 2^31 - 512)
+  // positions are row-relative int32 (the launcher checks n_t < 2^31 - 1024)
+  __shared__ __attribute__((aligned(16))) float lds_all[(STAGE & 3) ? 4 : 1][2][(STAGE & 3) ? 64 * RS_ROW : 4];
+  const int lane = threadIdx.x & 63;
+  float *lx = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][0], *lo_ = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][1];
   const int n_out = (n_t + S - 1) / S;
   const int n_seg = (n_out + seg_out - 1) / seg_out;
   const int64_t n_units = (int64_t)n_seg * n_ch;
-  const int lane = threadIdx.x & 63;
   const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const float nanv = __builtin_nanf("");
   const int k_first = (W - 1 + S - 1) / S;
@@ -1080,135 +1108,199 @@ __global__ __launch_bounds__(256) void k_rolling_scan_tc(
     const int p0 = ka * S, p1 = (k1 - 1) * S;  // output positions [p0, p1]
     // Wsum(p0 - 1): window [p0 - W, p0 - 1] (x[-1] = 0 when p0 = W - 1)
     double carry = 0.0;
-    int ccnt = 0;
+    int64_t ccnt = 0;  // packed null counts of the window (null_code)
     {
       double acc = 0.0;
-      int cnt = 0;
+      int64_t cnt = 0;
       for (int m = p0 - W + lane; m < p0; m += 64) {
         if (m < 0) continue;
         const float v = row[m];
-        const bool f = __builtin_isfinite(v);
-        acc += f ? (double)v : 0.0;
-        cnt += !f;
+        acc += __builtin_isfinite(v) ? (double)v : 0.0;
+        cnt += null_code(v);
       }
       carry = wave_sum(acc);
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
       ccnt = cnt;
     }
-    // tiles of 256 positions from the 4-aligned position at or below p0; the
-    // next tile's loads are in flight while the current one is scanned (two
-    // static register buffers: moving prefetched registers would wait)
     const int tb0 = VEC ? (p0 & ~3) : p0;
-    const int step_mod = 256 % S;
-    int ph = (tb0 + 4 * lane) % S;  // phase of this lane's first position
     struct Tile {
-      float xi[4], xo[4];
+      float xi[RS_E], xo[RS_E];
     };
     auto load = [&](int tb, Tile &T) {
-      const int t = tb + 4 * lane;
-      const bool full = tb + 256 <= n_t && tb - W >= 0;
-      if (VEC && full) {
-        const f4v a = *reinterpret_cast<const f4v *>(row + t);
-        T.xi[0] = a.x, T.xi[1] = a.y, T.xi[2] = a.z, T.xi[3] = a.w;
-        if ((W & 3) == 0) {
-          const f4v b = *reinterpret_cast<const f4v *>(row + t - W);
-          T.xo[0] = b.x, T.xo[1] = b.y, T.xo[2] = b.z, T.xo[3] = b.w;
-        } else {
+      const int t = tb + RS_E * lane;
+      const bool full = tb + RS_P <= n_t && tb - W >= 0;
+      if ((STAGE & 1) && VEC && full) {
+        // coalesced: float4 j of lane l = positions 4l + 256j (unstaged here;
+        // process() moves them to lane-consecutive order through LDS)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) T.xo[e] = row[t + e - W];
+        for (int h = 0; h < 2; ++h) {
+          const int tc = tb + 4 * lane + 256 * h;
+          const f4v a = *reinterpret_cast<const f4v *>(row + tc);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
+          if ((W & 3) == 0) {
+            const f4v b = *reinterpret_cast<const f4v *>(row + tc - W);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = row[tc + e - W];
+          }
+        }
+      } else if (VEC && full) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f4v a = *reinterpret_cast<const f4v *>(row + t + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
+          if ((W & 3) == 0) {
+            const f4v b = *reinterpret_cast<const f4v *>(row + t + 4 * h - W);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = row[t + 4 * h + e - W];
+          }
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < RS_E; ++e) {
           const int ti = t + e;
           T.xi[e] = ti < n_t ? row[ti] : 0.0f;
           T.xo[e] = (ti - W >= 0 && ti < n_t) ? row[ti - W] : 0.0f;
         }
       }
     };
-    auto process = [&](int tb, const Tile &T) {
-      const int t = tb + 4 * lane;
-      double d[4];
-      int c[4];
-      bool anynf = false;
+    auto process = [&](int tb, const Tile &Tin) {
+      const int t = tb + RS_E * lane;  // this lane's first position
+      Tile T = Tin;
+      if ((STAGE & 1) && VEC && tb + RS_P <= n_t && tb - W >= 0) {
+        // coalesced -> lane-consecutive through LDS (padded rows of 12 floats)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ti = t + e;
-        const bool in = ti >= p0 && ti <= p1;
-        const bool fi = __builtin_isfinite(T.xi[e]), fo = __builtin_isfinite(T.xo[e]);
-        d[e] = in ? (fi ? (double)T.xi[e] : 0.0) - (fo ? (double)T.xo[e] : 0.0) : 0.0;
-        c[e] = in ? (int)!fi - (int)!fo : 0;
-        anynf |= in && (!fi || !fo);
+        for (int h = 0; h < 2; ++h) {
+          const int pos = 4 * lane + 256 * h;
+          const int off = (pos >> 3) * RS_ROW + (pos & 7);
+          *reinterpret_cast<f4v *>(lx + off) = f4v{Tin.xi[4 * h], Tin.xi[4 * h + 1], Tin.xi[4 * h + 2], Tin.xi[4 * h + 3]};
+          *reinterpret_cast<f4v *>(lo_ + off) = f4v{Tin.xo[4 * h], Tin.xo[4 * h + 1], Tin.xo[4 * h + 2], Tin.xo[4 * h + 3]};
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f4v a = *reinterpret_cast<const f4v *>(lx + lane * RS_ROW + 4 * h);
+          const f4v b = *reinterpret_cast<const f4v *>(lo_ + lane * RS_ROW + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            T.xi[4 * h + e] = a[e];
+            T.xo[4 * h + e] = b[e];
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      // lane-local inclusive prefix, then the wave's exclusive scan
-      d[1] += d[0];
-      d[2] += d[1];
-      d[3] += d[2];
-      double v = d[3];
+      double d[RS_E];
+#pragma unroll
+      for (int e = 0; e < RS_E; ++e) d[e] = (double)T.xi[e] - (double)T.xo[e];
+#pragma unroll
+      for (int e = 1; e < RS_E; ++e) d[e] += d[e - 1];
+      // general path: steps at the output range's edges, or whose window
+      // holds a null (a null makes some lane total non-finite)
+      const bool general = !(tb >= p0 && tb + RS_P - 1 <= p1 && ccnt == 0) ||
+                           __any(!__builtin_isfinite(d[RS_E - 1]));
+      if (general) {
+#pragma unroll
+        for (int e = 0; e < RS_E; ++e) {
+          const int ti = t + e;
+          const bool in = ti >= p0 && ti <= p1;
+          const float a = T.xi[e], b = T.xo[e];
+          d[e] = in ? (__builtin_isfinite(a) ? (double)a : 0.0) - (__builtin_isfinite(b) ? (double)b : 0.0) : 0.0;
+        }
+#pragma unroll
+        for (int e = 1; e < RS_E; ++e) d[e] += d[e - 1];
+      }
+      double v = d[RS_E - 1];
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const double w_ = __shfl_up(v, o, 64);
         if (lane >= o) v += w_;
       }
-      const double excl = carry + (v - d[3]);
+      const double excl = carry + (v - d[RS_E - 1]);
       const double tot = __shfl(v, 63, 64);
-      // non-finite counts only when this step or the carried window has one
-      int cc[4] = {0, 0, 0, 0};
-      if (__any(anynf) || ccnt != 0) {
-        c[1] += c[0];
-        c[2] += c[1];
-        c[3] += c[2];
-        int vc = c[3];
+      float o8[RS_E];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int w_ = __shfl_up(vc, o, 64);
-          if (lane >= o) vc += w_;
+      for (int e = 0; e < RS_E; ++e) o8[e] = (float)((excl + d[e]) * inv_w);
+      if (general) {
+        // windows holding nulls: the packed counts of NaN / +inf / -inf
+        // samples in the window give numpy's mean of the raw values
+        int64_t c[RS_E];
+        bool any_code = ccnt != 0;
+#pragma unroll
+        for (int e = 0; e < RS_E; ++e) {
+          const int ti = t + e;
+          c[e] = ti >= p0 && ti <= p1 ? null_code(T.xi[e]) - null_code(T.xo[e]) : 0;
+          any_code |= c[e] != 0;
         }
-        const int ex = ccnt + (vc - c[3]);
+        if (__any(any_code)) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) cc[e] = ex + c[e];
-        ccnt += __shfl(vc, 63, 64);
-      }
-      float o4[4];
-      bool is_out[4];
-      bool direct = false;
+          for (int e = 1; e < RS_E; ++e) c[e] += c[e - 1];
+          int64_t vc = c[RS_E - 1];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ti = t + e;
-        int pe = ph + e;
-        while (pe >= S) pe -= S;  // at most 3 subtractions (ph < S, e < 4)
-        is_out[e] = ti >= p0 && ti <= p1 && pe == 0;
-        o4[e] = (float)((excl + d[e]) * inv_w);
-        direct |= is_out[e] && cc[e] != 0;
-      }
-      if (__any(direct)) {  // windows holding a null: numpy's mean of the raw values
+          for (int o = 1; o < 64; o <<= 1) {
+            const int64_t w_ = __shfl_up(vc, o, 64);
+            if (lane >= o) vc += w_;
+          }
+          const int64_t ex = ccnt + (vc - c[RS_E - 1]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (is_out[e] && cc[e] != 0) o4[e] = window_direct(row, t + e, W, 1);
+          for (int e = 0; e < RS_E; ++e) o8[e] = null_mean(ex + c[e], o8[e]);
+          ccnt += __shfl(vc, 63, 64);
+        }
       }
-      if (S == 1 && vec_out && is_out[0] && is_out[3]) {
-        *reinterpret_cast<f4v *>(yo + t) = f4v{o4[0], o4[1], o4[2], o4[3]};
+      if (S == 1 && vec_out && !general && (STAGE & 2)) {
+        // lane-consecutive -> coalesced through LDS: float4 j of lane l =
+        // positions 4l + 256j
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          *reinterpret_cast<f4v *>(lx + lane * RS_ROW + 4 * h) = f4v{o8[4 * h], o8[4 * h + 1], o8[4 * h + 2], o8[4 * h + 3]};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int pos = 4 * lane + 256 * h;
+          *reinterpret_cast<f4v *>(yo + tb + pos) = *reinterpret_cast<const f4v *>(lx + (pos >> 3) * RS_ROW + (pos & 7));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (S == 1 && vec_out && !general) {
+        *reinterpret_cast<f4v *>(yo + t) = f4v{o8[0], o8[1], o8[2], o8[3]};
+        *reinterpret_cast<f4v *>(yo + t + 4) = f4v{o8[4], o8[5], o8[6], o8[7]};
       } else {
+        // outputs: positions t + e with (t + e) % S == 0
+        int ph = t % S;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (is_out[e]) yo[(int64_t)((t + e) / S) * ys_t] = o4[e];
+        for (int e = 0; e < RS_E; ++e) {
+          const int ti = t + e;
+          if (ti >= p0 && ti <= p1 && ph == 0) yo[(int64_t)(ti / S) * ys_t] = o8[e];
+          ph = ph + 1 == S ? 0 : ph + 1;
+        }
       }
       carry += tot;
-      ph += step_mod;
-      ph = ph >= S ? ph - S : ph;
     };
     Tile A, B;
     int tb = tb0;
     load(tb, A);
     while (true) {
-      if (tb + 256 <= p1) load(tb + 256, B);
+      if (tb + RS_P <= p1) load(tb + RS_P, B);
       process(tb, A);
-      tb += 256;
+      tb += RS_P;
       if (tb > p1) break;
-      if (tb + 256 <= p1) load(tb + 256, A);
+      if (tb + RS_P <= p1) load(tb + RS_P, A);
       process(tb, B);
-      tb += 256;
+      tb += RS_P;
       if (tb > p1) break;
     }
   }
@@ -1658,6 +1750,287 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
   for (int64_t k = kb; k < k1; ++k) guarded_block(k);
 }
 
+// ---------------------------------------------------------------------------
+// k_block_runs_mfma_tm — run-mode K1 for (time, channel) storage (the real
+// files' layout, low_pass_dascore.ipynb cell 14 data[:, ch]: s_ch = 1, rows
+// of s_t floats).  A wave owns 32 channels = one 128-B line of every sample
+// row, i.e. two MFMA column tiles (channels 0-15, 16-31).  Per MFMA step
+// (16-sample group j, step e) the four samples 16j + e + {0, 4, 8, 12} of
+// the block row are loaded with two dword loads, P (rows +0, +4) and Q (+8,
+// +12): lane l reads channel l & 31 of row 4 (l >> 5), so every load
+// instruction reads two whole lines.  v_permlane32_swap + v_permlane16_swap
+// then leave lane 16k + c holding row k of channel c (P: tile 0) and of
+// channel 16 + c (Q: tile 1) — the B operand layout of
+// v_mfma_f64_16x16x4_f64 with the channel-major kernel's sample order, so
+// the same tap table (row shift 0) and the same run epilogue apply, once per
+// tile.  512-thread workgroups: taps + 8 waves x 2 run buffers in LDS.
+// ---------------------------------------------------------------------------
+
+struct TmIter {
+  float p[4][4], q[4][4];  // [16-sample group j][step e]
+};
+
+// SWAP: lane l reads channel l & 31 of rows +4 (l >> 5) (P) and +8 + 4 (l >> 5)
+// (Q); else lane (q, col) reads channel col (P) and 16 + col (Q) of row +4q
+// (two half lines of the same rows back to back; A/B knob LFD_TM_SWAP=0).
+// Interior loads: the row pointer is wave-uniform (SGPR base) and the lane's
+// part a 32-bit element offset, so a load needs no per-lane 64-bit address
+// arithmetic (global_load ... saddr).
+template <bool SWAP>
+__device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c0, int64_t s_t, int64_t row0,
+                                          uint32_t offp, uint32_t offq, TmIter &b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t ro = uniform64(c0 + (row0 + 16 * j + e) * s_t);  // element offset of the row
+      const char *rp = reinterpret_cast<const char *>(x + ro);
+      const char *rq = SWAP ? reinterpret_cast<const char *>(x + ro + 8 * s_t) : rp;
+      b.p[j][e] = *reinterpret_cast<const float *>(rp + offp);
+      b.q[j][e] = *reinterpret_cast<const float *>(rq + offq);
+    }
+}
+
+template <bool GUARD, bool SWAP>
+__device__ __forceinline__ void tm_load(const float *__restrict__ xc, const float *__restrict__ xq, int64_t s_t,
+                                        int64_t n_t, int64_t row0, TmIter &b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t rp = row0 + 16 * j + e, rq = SWAP ? rp + 8 : rp;
+      if (GUARD) {
+        const int64_t cp = rp < 0 ? 0 : (rp >= n_t ? n_t - 1 : rp);
+        const int64_t cq = rq < 0 ? 0 : (rq >= n_t ? n_t - 1 : rq);
+        const float vp = xc[cp * s_t], vq = xq[cq * s_t];
+        b.p[j][e] = (rp >= 0 && rp < n_t) ? vp : 0.0f;
+        b.q[j][e] = (rq >= 0 && rq < n_t) ? vq : 0.0f;
+      } else {
+        b.p[j][e] = xc[rp * s_t];
+        b.q[j][e] = xq[rq * s_t];
+      }
+    }
+}
+
+// 2 x 16 MFMAs of one 64-sample iteration (offset o0 = 64 it); out-of-block
+// samples (row offsets outside [lo, hi)) finite-masked when `mask`
+template <bool SWAP>
+__device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmIter &b, int o0, int q, bool mask,
+                                        int lo, int hi, d4v &acc0, d4v &acc1) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double2 b01 = *reinterpret_cast<const double2 *>(kt + j * kstride);
+    const double2 b23 = *reinterpret_cast<const double2 *>(kt + j * kstride + 2);
+    const double a[4] = {b01.x, b01.y, b23.x, b23.y};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v0 = b.p[j][e], v1 = b.q[j][e];
+      if (SWAP) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
+        const auto s2 = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
+        v0 = __uint_as_float(s2[0]);
+        v1 = __uint_as_float(s2[1]);
+      }
+      if (mask) {
+        const int o = o0 + 16 * j + 4 * q + e;
+        if (o < lo || o >= hi) {
+          v0 = finite_or_zero(v0);
+          v1 = finite_or_zero(v1);
+        }
+      }
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v1, acc1, 0, 0, 0);
+    }
+  }
+}
+
+template <int TM_PF, int NT, bool SWAP>
+__global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
+    const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
+    TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
+  extern __shared__ double Ks[];
+  const int tab = tg.Lp * tg.nc;  // one table: row shift 0
+  for (int i = 2 * threadIdx.x; i < tab; i += 2 * blockDim.x)
+    *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
+  double *cst = Ks + tab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4]
+  for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  double *wbase = Ks + tab + RUN_CST + wave * 2 * RUN_WB;  // tile t's buffer: wbase + t * RUN_WB
+  const int64_t n_c32 = (g.n_ch + 31) / 32;
+  const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (unit >= n_c32 * rg.n_groups) return;
+  const int64_t c32 = unit % n_c32, grp = unit / n_c32;
+  int r = __builtin_amdgcn_readfirstlane(rg.group_r0[grp]);
+  const int r_end = __builtin_amdgcn_readfirstlane(rg.group_r0[grp + 1]);
+  const int ru0 = r;
+  const int my_len = lane < r_end - ru0 ? rg.run_len[ru0 + lane] : 0;
+  const int64_t my_ks = lane < r_end - ru0 ? rg.run_ks[ru0 + lane] : 0;
+  auto run_len_of = [&](int rr) { return __builtin_amdgcn_readlane(my_len, rr - ru0); };
+  auto run_ks_of = [&](int rr) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_ks, rr - ru0);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)my_ks >> 32), rr - ru0);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  const int64_t k0 = run_ks_of(r);
+  const int64_t k1 = run_ks_of(r_end - 1) + run_len_of(r_end - 1);
+  const int col = lane & 15, q = lane >> 4;
+  const bool tile1 = c32 * 32 + 16 < g.n_ch;  // tile 1 holds a real channel (else its stores would
+                                               // leave the 16-channel padding of Y0 / AG)
+  // this lane's load channel and row offset
+  const int lc = SWAP ? (lane & 31) : col;
+  const int64_t lch = min(c32 * 32 + lc, g.n_ch - 1);
+  const float *xc = x + lch;
+  const int rsel = SWAP ? 4 * (lane >> 5) : 4 * q;
+  // (channels past n_ch, in a ragged last group, read channel n_ch - 1)
+  // Q loads: the same lane channel (SWAP) or tile 1's (16 + col), clamped
+  // like P so no load leaves the array
+  const int64_t lchq = SWAP ? lch : min(c32 * 32 + 16 + col, g.n_ch - 1);
+  const float *xq = x + lchq;
+  const int64_t c0 = uniform64(c32 * 32);  // interior loads: uniform row base + lane offset
+  const uint32_t offp = (uint32_t)(4 * (lch - c32 * 32 + rsel * s_t)),  // bytes
+      offq = (uint32_t)(4 * (lchq - c32 * 32 + rsel * s_t));
+
+  const bool colv = col < tg.nc;
+  const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
+  const int nit = tg.Lp / 64;
+  const int kstride = 16 * tg.nc;
+  const int64_t s0 = g.base - tg.J;
+  const int L = g.L;
+  const int lo = tg.J, hi = tg.J + L;  // the block's own samples in its row
+  const double *PhiF = cst, *Mm = cst + 16, *PhiR = cst + 32, *G0 = cst + 48, *H0 = cst + 52;
+
+  int64_t rks = k0;
+  int rlen = run_len_of(r);
+  double S0[2] = {0.0, 0.0};  // run prefix state, component q of channel col, per tile
+  auto block_done = [&](const d4v &a, int t, int64_t k) {
+    // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
+    const int p = (int)(k - rks);
+    double sv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sv[j] = __shfl(S0[t], col + 16 * j, 64);
+    double v = a[1], pg = a[2], sn = a[0];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v = fma(Mm[q * 4 + j], sv[j], v);
+      pg = fma(G0[j], sv[j], pg);
+      sn = fma(PhiF[q * 4 + j], sv[j], sn);
+    }
+    S0[t] = sn;
+    double *wb = wbase + t * RUN_WB;
+    wb[(p * 5 + 1 + q) * 16 + col] = v;
+    if (q == 0) wb[(p * 5) * 16 + col] = pg;
+  };
+  auto run_done = [&]() {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t == 1 && !tile1) break;
+      const double *wb = wbase + t * RUN_WB;
+      const int64_t cg = 2 * c32 + t;
+      double T[4] = {0.0, 0.0, 0.0, 0.0};
+      double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
+      for (int pp = rlen - 1; pp >= 0; --pp) {
+        double y0 = wb[(pp * 5) * 16 + col];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y0 = fma(H0[j], T[j], y0);
+        if ((pp & 3) == q) y0o[pp * 16] = y0;
+        double nt[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          double acc = wb[(pp * 5 + 1 + i) * 16 + col];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc = fma(PhiR[i * 4 + j], T[j], acc);
+          nt[i] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T[i] = nt[i];
+      }
+      double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + col;
+      ag[q * 16] = S0[t];
+      ag[(4 + q) * 16] = q == 0 ? T[0] : (q == 1 ? T[1] : (q == 2 ? T[2] : T[3]));
+    }
+    __builtin_amdgcn_wave_barrier();
+    S0[0] = S0[1] = 0.0;
+    ++r;
+    if (r < r_end) {
+      rks = run_ks_of(r);
+      rlen = run_len_of(r);
+    }
+  };
+  auto finish_block = [&](const d4v &acc0, const d4v &acc1, int64_t k) {
+    block_done(acc0, 0, k);
+    block_done(acc1, 1, k);
+    if (k - rks + 1 == rlen) run_done();
+  };
+  auto guarded_block = [&](int64_t k) {
+    const int64_t s = s0 + k * L;
+    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int it = 0; it < nit; ++it) {
+      TmIter b;
+      tm_load<true, SWAP>(xc, xq, s_t, n_t, s + 64 * it + rsel, b);
+      tm_iter<SWAP>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0, acc1);
+    }
+    finish_block(acc0, acc1, k);
+  };
+
+  int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
+  int64_t kb = n_t - tg.Lp - s0 >= 0 ? (n_t - tg.Lp - s0) / L + 1 : 0;
+  ka = uniform64(ka < k0 ? k0 : (ka > k1 ? k1 : ka));
+  kb = uniform64(kb > k1 ? k1 : (kb < ka ? ka : kb));
+  for (int64_t k = k0; k < ka; ++k) guarded_block(k);
+  if (ka < kb) {
+    // interior: flattened (block, iteration) stream, TM_PF iterations of
+    // loads in flight (ring unrolled so buffer indices are static)
+    int64_t k = ka, s = s0 + ka * L;
+    int it = 0;
+    int64_t kp = ka, sp = s;
+    int itp = 0;
+    auto produce = [&]() {
+      if (kp == kb - 1 && itp == nit - 1) return;  // past the end: re-load the last one
+      if (++itp == nit) {
+        itp = 0;
+        ++kp;
+        sp += L;
+      }
+    };
+    TmIter buf[TM_PF + 1];
+#pragma unroll
+    for (int d = 0; d < TM_PF; ++d) {
+      tm_load_u<SWAP>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[d]);
+      produce();
+    }
+    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    bool fin = false;
+    while (!fin) {
+#pragma unroll
+      for (int u = 0; u <= TM_PF; ++u) {
+        constexpr int NB = TM_PF + 1;
+        const int lb = (u + TM_PF) % NB;
+        tm_load_u<SWAP>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[lb]);
+        produce();
+        // a run's first and last iteration need the finite mask (chunk
+        // boundaries are run boundaries)
+        const bool mask = (it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen);
+        tm_iter<SWAP>(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
+        if (++it == nit) {
+          finish_block(acc0, acc1, k);
+          acc0 = d4v{0.0, 0.0, 0.0, 0.0};
+          acc1 = d4v{0.0, 0.0, 0.0, 0.0};
+          it = 0;
+          ++k;
+          s += L;
+          if (k >= kb) {
+            fin = true;
+            break;
+          }
+        }
+      }
+    }
+  }
+  for (int64_t k = kb; k < k1; ++k) guarded_block(k);
+}
+
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 inline bool getenv_flag(const char *name) {
@@ -1683,6 +2056,43 @@ hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t, const
 }
 
 }  // namespace
+
+hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
+                                     const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
+                                     double *AG, hipStream_t st) {
+  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || tg.nvar != 1 || tg.v0 != 0 || rg.n_groups < 1)
+    return hipErrorInvalidValue;
+  const size_t tab = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST);
+  // measured on cfg3 stored time-major (tools/tm_bench.py): no-swap loads at
+  // 512 threads / depth 2 14.28 ms, 768 / 1 14.46; permlane loads 14.74-14.89
+  int nt = 512, pf = 2;
+  if (const char *v = std::getenv("LFD_TM_NT")) nt = std::atoi(v);
+  if (const char *v = std::getenv("LFD_TM_PF")) pf = std::atoi(v);
+  const size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * 2 * RUN_WB;
+  if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
+  auto go = [&](auto kern, int NT) -> hipError_t {
+    static bool attr[2] = {false, false};  // per instantiation below
+    (void)attr;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       TAP_LDS_MAX);
+    if (e != hipSuccess) return e;
+    const int W = NT / 64;
+    const int64_t units = ((g.n_ch + 31) / 32) * rg.n_groups;
+    kern<<<(unsigned)((units + W - 1) / W), NT, lds, st>>>(x, s_t, n_t, g, taps, tg, rg, Y0, AG);
+    return hipGetLastError();
+  };
+  bool swap = false;
+  if (const char *v = std::getenv("LFD_TM_SWAP")) swap = std::atoi(v) != 0;
+  if (swap) {
+    if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, true>, 768);
+    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, true>, 512);
+    if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, true>, 512);
+  } else {
+    if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, false>, 768);
+    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false>, 512);
+  }
+  return hipErrorInvalidValue;  // no instantiation for this A/B knob combination
+}
 
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g, const BlockConst &kc,
@@ -2001,15 +2411,21 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                hipStream_t st) {
   const int64_t n_out = (n_t + S - 1) / S;
   const int64_t cap = 256 * 32;  // workgroups of the grid-stride launches
-  if (s_t == 1 && S >= W) {
-    // windows do not overlap: each is summed directly by one wave
+  // step < window: the running-sum scan reads each sample twice (x[t] and,
+  // from cache, x[t - W]) and scans every position; summing each window
+  // directly reads it W/S times from L2/L1 (W/S = 4: 5.25 ms vs 3.81 ms on
+  // cfg2), so the scan takes every W > 2S (A/B knob LFD_ROLL_DIRECT_MAX)
+  int64_t direct_max = 2;
+  if (const char *v = std::getenv("LFD_ROLL_DIRECT_MAX")) direct_max = std::atoll(v);
+  if (s_t == 1 && W <= direct_max * S) {
+    // windows overlap little or not at all: each is summed directly by one wave
     const int64_t waves = n_ch * n_out;
     int64_t blocks = (waves + 3) / 4;
     if (blocks > cap) blocks = cap;
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     k_rolling_tc<<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y,
                                                    ys_ch, ys_t, vec);
-  } else if (s_t == 1 && n_t < (int64_t)INT32_MAX - 512 && W < INT32_MAX / 2) {
+  } else if (s_t == 1 && n_t < (int64_t)INT32_MAX - 1024 && W < ((int64_t)1 << 21)) {
     // overlapping windows: running sum over segments of >= max(32768, 4W)
     // positions (halo W per segment), fewer when that leaves the chip idle
     int64_t seg_pos = std::max<int64_t>(32768, 4 * W);
@@ -2021,12 +2437,25 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     if (blocks > cap) blocks = cap;
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
     const bool vec_out = vec && ys_t == 1 && ys_ch % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-    if (vec)
-      k_rolling_scan_tc<true><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch,
-                                                                ys_t, (int)seg_out, vec_out);
+    // stage 2 (lanes load their 8 positions directly, outputs leave through
+    // LDS as coalesced float4 stores) measured best on cfg2 at S = 1: 4.77 ms
+    // vs 5.93 (0), 5.99 (1), 5.54 (3)
+    int stage = 2;
+    if (const char *v = std::getenv("LFD_ROLL_STAGE")) stage = std::atoi(v) & 3;
+#define LFD_ROLL(V, ST)                                                                                    \
+  k_rolling_scan_tc<V, ST><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, \
+                                                             ys_t, (int)seg_out, V && vec_out)
+    if (!vec)
+      LFD_ROLL(false, 0);
+    else if (stage == 0)
+      LFD_ROLL(true, 0);
+    else if (stage == 1)
+      LFD_ROLL(true, 1);
+    else if (stage == 2)
+      LFD_ROLL(true, 2);
     else
-      k_rolling_scan_tc<false><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch,
-                                                                 ys_t, (int)seg_out, false);
+      LFD_ROLL(true, 3);
+#undef LFD_ROLL
   } else {
     const int64_t seg_out = S >= W ? 64 : std::max<int64_t>(1, std::max<int64_t>(4096, 4 * W) / S);
     const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);

@@ -125,12 +125,13 @@ class LowpassPlan:
 
     def last_kernel(self) -> str:
         """Block-functional kernel of the last execute: "mfma_runs" (MFMA +
-        run folding), "mfma" or "recurrence"; "recurrence_fold" / "mfma_fold"
-        when a separate fold kernel turns their per-block functionals into runs
-        (4th-order cascades)."""
+        run folding), "mfma_runs_tm" (the same for (time, channel) rows),
+        "mfma" or "recurrence"; "recurrence_fold" / "mfma_fold" when a separate
+        fold kernel turns their per-block functionals into runs (4th-order
+        cascades)."""
         k = self._lib.lfd_lowpass_last_kernel(self._h)
         return {1: "recurrence", 2: "mfma", 3: "mfma_runs", 4: "recurrence_fold",
-                5: "mfma_fold"}.get(k, "none")
+                5: "mfma_fold", 6: "mfma_runs_tm"}.get(k, "none")
 
     def runs(self):
         """(run_ks, run_len, RunConst record) or None without run mode — testing hook."""

@@ -77,10 +77,7 @@ def test_lfproc_parity(cfg, dc, layout, off_ns):
     # both fold into runs (in registers where the MFMA kernel's LDS fits the
     # run buffers, else by the separate fold kernel: L = 2000, recurrence)
     # (off-sample grids stay on the block plan: the blended output functional)
-    if layout == "tc":
-        assert _run.last_kernel == "mfma_runs"
-    else:
-        assert _run.last_kernel == "recurrence_fold"
+    assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
 def _plan_cfg(fs, dt_out, P, B, n_ch, n):
@@ -361,8 +358,8 @@ def test_nonfinite_samples_poison_their_chunk_only(where, layout):
 ])
 def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
     """(time, channel) storage viewed as (channel, time) (s_ch = 1, s_t =
-    row width): recurrence K1 + run fold agrees with the per-block scan and
-    with the oracle, nulls included."""
+    row width): the time-major MFMA run kernel and the recurrence K1 + run
+    fold agree with the per-block scan and with the oracle, nulls included."""
     import torch
     fs, dt_out, P, B, n_ch, n, width = cfg
     rng = np.random.default_rng(9)
@@ -373,19 +370,25 @@ def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
     assert xd.stride() == (1, width)
     ws = plan.alloc_workspace()
     out = {}
-    for mode in ("default", "blocks"):
+    for mode in ("default", "recfold", "blocks"):
+        if mode == "recfold":
+            monkeypatch.setenv("LFD_K1_REC", "1")
         if mode == "blocks":
             monkeypatch.setenv("LFD_NO_RUNS", "1")
         yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
         plan.execute(xd, yd, ws)
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
-    assert out["default"][1] == "recurrence_fold"
+    assert out["default"][1] == "mfma_runs_tm"
+    assert out["recfold"][1] == "recurrence_fold"
     assert out["blocks"][1] == "recurrence"
-    a, b = out["default"][0], out["blocks"][0]
-    assert np.array_equal(np.isnan(a), np.isnan(b))
+    b = out["blocks"][0]
     m = ~np.isnan(b)
-    assert _relrms(a[m], b[m]) < 1e-6
+    for mode in ("default", "recfold"):
+        a = out[mode][0]
+        assert np.array_equal(np.isnan(a), np.isnan(b)), mode
+        assert _relrms(a[m], b[m]) < 1e-6, mode
+    a = out["default"][0]
     # oracle on the same channels
     x = np.ascontiguousarray(xt[:, :n_ch].T)
     dt_ns = int(round(1e9 / fs))
