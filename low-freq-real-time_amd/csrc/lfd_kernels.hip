@@ -1776,7 +1776,7 @@ struct TmIter {
 // Interior loads: the row pointer is wave-uniform (SGPR base) and the lane's
 // part a 32-bit element offset, so a load needs no per-lane 64-bit address
 // arithmetic (global_load ... saddr).
-template <bool SWAP>
+template <bool SWAP, int NTILE = 2>
 __device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c0, int64_t s_t, int64_t row0,
                                           uint32_t offp, uint32_t offq, TmIter &b) {
 #pragma unroll
@@ -1787,11 +1787,11 @@ __device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c
       const char *rp = reinterpret_cast<const char *>(x + ro);
       const char *rq = SWAP ? reinterpret_cast<const char *>(x + ro + 8 * s_t) : rp;
       b.p[j][e] = *reinterpret_cast<const float *>(rp + offp);
-      b.q[j][e] = *reinterpret_cast<const float *>(rq + offq);
+      if (NTILE == 2) b.q[j][e] = *reinterpret_cast<const float *>(rq + offq);
     }
 }
 
-template <bool GUARD, bool SWAP>
+template <bool GUARD, bool SWAP, int NTILE = 2>
 __device__ __forceinline__ void tm_load(const float *__restrict__ xc, const float *__restrict__ xq, int64_t s_t,
                                         int64_t n_t, int64_t row0, TmIter &b) {
 #pragma unroll
@@ -1802,19 +1802,21 @@ __device__ __forceinline__ void tm_load(const float *__restrict__ xc, const floa
       if (GUARD) {
         const int64_t cp = rp < 0 ? 0 : (rp >= n_t ? n_t - 1 : rp);
         const int64_t cq = rq < 0 ? 0 : (rq >= n_t ? n_t - 1 : rq);
-        const float vp = xc[cp * s_t], vq = xq[cq * s_t];
+        const float vp = xc[cp * s_t], vq = NTILE == 2 ? xq[cq * s_t] : 0.0f;
         b.p[j][e] = (rp >= 0 && rp < n_t) ? vp : 0.0f;
         b.q[j][e] = (rq >= 0 && rq < n_t) ? vq : 0.0f;
       } else {
         b.p[j][e] = xc[rp * s_t];
-        b.q[j][e] = xq[rq * s_t];
+        if (NTILE == 2) b.q[j][e] = xq[rq * s_t];
       }
     }
 }
 
 // 2 x 16 MFMAs of one 64-sample iteration (offset o0 = 64 it); out-of-block
 // samples (row offsets outside [lo, hi)) finite-masked when `mask`
-template <bool SWAP>
+// NTILE == 2: acc0 / acc1 are tiles 0 / 1; NTILE == 1: two chains of tile 0
+// (even / odd steps), summed at the block end
+template <bool SWAP, int NTILE = 2>
 __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmIter &b, int o0, int q, bool mask,
                                         int lo, int hi, d4v &acc0, d4v &acc1) {
 #pragma unroll
@@ -1838,14 +1840,20 @@ __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmI
           v1 = finite_or_zero(v1);
         }
       }
-      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v1, acc1, 0, 0, 0);
+      if (NTILE == 2) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v1, acc1, 0, 0, 0);
+      } else if (e & 1) {
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc1, 0, 0, 0);
+      } else {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
+      }
     }
   }
 }
 
-template <int TM_PF, int NT, bool SWAP>
-__global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
+template <int TM_PF, int NT, bool SWAP, int NTILE = 2>
+__global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
   extern __shared__ double Ks[];
@@ -1856,8 +1864,9 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
   for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  double *wbase = Ks + tab + RUN_CST + wave * 2 * RUN_WB;  // tile t's buffer: wbase + t * RUN_WB
-  const int64_t n_c32 = (g.n_ch + 31) / 32;
+  double *wbase = Ks + tab + RUN_CST + wave * NTILE * RUN_WB;  // tile t's buffer: wbase + t * RUN_WB
+  constexpr int CW = 16 * NTILE;  // channels per wave
+  const int64_t n_c32 = (g.n_ch + CW - 1) / CW;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_c32 * rg.n_groups) return;
   const int64_t c32 = unit % n_c32, grp = unit / n_c32;
@@ -1875,21 +1884,21 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
   const int64_t k0 = run_ks_of(r);
   const int64_t k1 = run_ks_of(r_end - 1) + run_len_of(r_end - 1);
   const int col = lane & 15, q = lane >> 4;
-  const bool tile1 = c32 * 32 + 16 < g.n_ch;  // tile 1 holds a real channel (else its stores would
+  const bool tile1 = NTILE == 2 && c32 * 32 + 16 < g.n_ch;  // tile 1 holds a real channel (else its stores would
                                                // leave the 16-channel padding of Y0 / AG)
   // this lane's load channel and row offset
   const int lc = SWAP ? (lane & 31) : col;
-  const int64_t lch = min(c32 * 32 + lc, g.n_ch - 1);
+  const int64_t lch = min(c32 * CW + lc, g.n_ch - 1);
   const float *xc = x + lch;
   const int rsel = SWAP ? 4 * (lane >> 5) : 4 * q;
   // (channels past n_ch, in a ragged last group, read channel n_ch - 1)
   // Q loads: the same lane channel (SWAP) or tile 1's (16 + col), clamped
   // like P so no load leaves the array
-  const int64_t lchq = SWAP ? lch : min(c32 * 32 + 16 + col, g.n_ch - 1);
+  const int64_t lchq = SWAP ? lch : min(c32 * CW + 16 + col, g.n_ch - 1);
   const float *xq = x + lchq;
-  const int64_t c0 = uniform64(c32 * 32);  // interior loads: uniform row base + lane offset
-  const uint32_t offp = (uint32_t)(4 * (lch - c32 * 32 + rsel * s_t)),  // bytes
-      offq = (uint32_t)(4 * (lchq - c32 * 32 + rsel * s_t));
+  const int64_t c0 = uniform64(c32 * CW);  // interior loads: uniform row base + lane offset
+  const uint32_t offp = (uint32_t)(4 * (lch - c32 * CW + rsel * s_t)),  // bytes
+      offq = (uint32_t)(4 * (lchq - c32 * CW + rsel * s_t));
 
   const bool colv = col < tg.nc;
   const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
@@ -1927,7 +1936,7 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
     for (int t = 0; t < 2; ++t) {
       if (t == 1 && !tile1) break;
       const double *wb = wbase + t * RUN_WB;
-      const int64_t cg = 2 * c32 + t;
+      const int64_t cg = NTILE * c32 + t;
       double T[4] = {0.0, 0.0, 0.0, 0.0};
       double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
       for (int pp = rlen - 1; pp >= 0; --pp) {
@@ -1959,8 +1968,12 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
     }
   };
   auto finish_block = [&](const d4v &acc0, const d4v &acc1, int64_t k) {
-    block_done(acc0, 0, k);
-    block_done(acc1, 1, k);
+    if (NTILE == 2) {
+      block_done(acc0, 0, k);
+      block_done(acc1, 1, k);
+    } else {
+      block_done(acc0 + acc1, 0, k);
+    }
     if (k - rks + 1 == rlen) run_done();
   };
   auto guarded_block = [&](int64_t k) {
@@ -1968,8 +1981,9 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     for (int it = 0; it < nit; ++it) {
       TmIter b;
-      tm_load<true, SWAP>(xc, xq, s_t, n_t, s + 64 * it + rsel, b);
-      tm_iter<SWAP>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0, acc1);
+      tm_load<true, SWAP, NTILE>(xc, xq, s_t, n_t, s + 64 * it + rsel, b);
+      tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0,
+                           acc1);
     }
     finish_block(acc0, acc1, k);
   };
@@ -1997,7 +2011,7 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
     TmIter buf[TM_PF + 1];
 #pragma unroll
     for (int d = 0; d < TM_PF; ++d) {
-      tm_load_u<SWAP>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[d]);
+      tm_load_u<SWAP, NTILE>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[d]);
       produce();
     }
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
@@ -2007,12 +2021,12 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma_tm(
       for (int u = 0; u <= TM_PF; ++u) {
         constexpr int NB = TM_PF + 1;
         const int lb = (u + TM_PF) % NB;
-        tm_load_u<SWAP>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[lb]);
+        tm_load_u<SWAP, NTILE>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[lb]);
         produce();
         // a run's first and last iteration need the finite mask (chunk
         // boundaries are run boundaries)
         const bool mask = (it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen);
-        tm_iter<SWAP>(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
+        tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
         if (++it == nit) {
           finish_block(acc0, acc1, k);
           acc0 = d4v{0.0, 0.0, 0.0, 0.0};
@@ -2068,7 +2082,9 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   int nt = 512, pf = 2;
   if (const char *v = std::getenv("LFD_TM_NT")) nt = std::atoi(v);
   if (const char *v = std::getenv("LFD_TM_PF")) pf = std::atoi(v);
-  const size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * 2 * RUN_WB;
+  int ntile = 2;
+  if (const char *v = std::getenv("LFD_TM_NTILE")) ntile = std::atoi(v) == 1 ? 1 : 2;
+  const size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * ntile * RUN_WB;
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   auto go = [&](auto kern, int NT) -> hipError_t {
     static bool attr[2] = {false, false};  // per instantiation below
@@ -2077,12 +2093,16 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
                                        TAP_LDS_MAX);
     if (e != hipSuccess) return e;
     const int W = NT / 64;
-    const int64_t units = ((g.n_ch + 31) / 32) * rg.n_groups;
+    const int64_t units = ((g.n_ch + 16 * ntile - 1) / (16 * ntile)) * rg.n_groups;
     kern<<<(unsigned)((units + W - 1) / W), NT, lds, st>>>(x, s_t, n_t, g, taps, tg, rg, Y0, AG);
     return hipGetLastError();
   };
   bool swap = false;
   if (const char *v = std::getenv("LFD_TM_SWAP")) swap = std::atoi(v) != 0;
+  if (ntile == 1) {  // one 16-channel tile per wave: half-line loads, 16 waves/CU
+    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 1>, 512);
+    return hipErrorInvalidValue;
+  }
   if (swap) {
     if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, true>, 768);
     if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, true>, 512);
