@@ -13,6 +13,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -255,20 +257,11 @@ void out_weights(const RModel &m, R ow, R *e) {
   }
 }
 
-// Fill the block-functional and scan constants for block length L and output
-// weight ow (the grid's constant fractional sample position).
-int block_constants(const Cascade &cs, int L, R ow, lfd::BlockConst &kc, lfd::ScanConst &sc,
-                    bool &fir32) {
-  RModel m;
-  if (int e = make_rmodel(cs, m)) return e;
-  const int n = 2 * m.ns, J = m.J;
-  if (L < J + 1 + (ow != 0 ? 1 : 0)) return fail(LFD_EUNSUPPORTED, "block shorter than the FIR span");
-  std::memset(&kc, 0, sizeof(kc));
-  std::memset(&sc, 0, sizeof(sc));
-  lfd::RCoef rc{};
+// Device coefficients of realization R; fir32 = no negative FIR tap.
+void make_rcoef(const RModel &m, lfd::RCoef &rc, bool &fir32) {
   R csum = 0;
   fir32 = true;
-  for (int j = 0; j <= J; ++j) {
+  for (int j = 0; j <= m.J; ++j) {
     rc.c64[j] = (double)m.c[j];
     rc.c32[j] = (float)m.c[j];
     csum += m.c[j];
@@ -283,6 +276,72 @@ int block_constants(const Cascade &cs, int L, R ow, lfd::BlockConst &kc, lfd::Sc
     rc.nra[s] = (double)(-m.a1[s] / m.a2[s]);
     rc.dcg[s] = (double)(1.0L / ((1.0L + m.a1[s]) + m.a2[s]));
   }
+}
+
+// Full-rate constants (lfd_internal.h FRConst): SciPy's TDF-II cascade
+// (_sosfilt, scipy/signal/_signaltools.py:4706) simulated in extended
+// precision.
+R tdf2_step(const Cascade &c, R *z, R v) {
+  for (int s = 0; s < c.ns; ++s) {
+    const R yv = c.b0[s] * v + z[2 * s];
+    z[2 * s] = c.b1[s] * v - c.a1[s] * yv + z[2 * s + 1];
+    z[2 * s + 1] = c.b2[s] * v - c.a2[s] * yv;
+    v = yv;
+  }
+  return v;
+}
+
+void fullrate_constants(const Cascade &cs, lfd::FRConst &fc) {
+  const int n = 2 * cs.ns;
+  std::memset(&fc, 0, sizeof(fc));
+  for (int s = 0; s < cs.ns; ++s) {
+    fc.cf.b0[s] = cs.b0[s];
+    fc.cf.b1[s] = cs.b1[s];
+    fc.cf.b2[s] = cs.b2[s];
+    fc.cf.a1[s] = cs.a1[s];
+    fc.cf.a2[s] = cs.a2[s];
+  }
+  sosfilt_zi(cs, fc.zi.v);
+  Mat P(n);
+  for (int c = 0; c < n; ++c) {
+    R z[MAX_N] = {0};
+    z[c] = 1;
+    for (int t = 0; t < lfd::FR_LS; ++t) (void)tdf2_step(cs, z, 0);
+    for (int r = 0; r < n; ++r) P.a[r][c] = z[r];
+  }
+  for (int i = 0; i < 6; ++i) {
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) fc.PhiP[i][r * MAX_N + c] = (double)P.a[r][c];
+    P = P * P;
+  }
+  for (int r = 0; r < n; ++r)  // P = PhiP[5]^2: FR_L samples
+    for (int c = 0; c < n; ++c) fc.PhiL[r * MAX_N + c] = (double)P.a[r][c];
+  std::vector<R> yv(lfd::FR_L);
+  for (int c = 0; c < n; ++c) {
+    R z[MAX_N] = {0};
+    z[c] = 1;
+    for (int i = 0; i < lfd::FR_L; ++i) {
+      yv[i] = tdf2_step(cs, z, 0);
+      if (i < lfd::FR_LS) fc.H[i][c] = (double)yv[i];
+    }
+    R t[MAX_N] = {0};
+    for (int i = lfd::FR_L - 1; i >= 0; --i) (void)tdf2_step(cs, t, yv[i]);
+    for (int r = 0; r < n; ++r) fc.M[r * MAX_N + c] = (double)t[r];
+  }
+}
+
+// Fill the block-functional and scan constants for block length L and output
+// weight ow (the grid's constant fractional sample position).
+int block_constants(const Cascade &cs, int L, R ow, lfd::BlockConst &kc, lfd::ScanConst &sc,
+                    bool &fir32) {
+  RModel m;
+  if (int e = make_rmodel(cs, m)) return e;
+  const int n = 2 * m.ns, J = m.J;
+  if (L < J + 1 + (ow != 0 ? 1 : 0)) return fail(LFD_EUNSUPPORTED, "block shorter than the FIR span");
+  std::memset(&kc, 0, sizeof(kc));
+  std::memset(&sc, 0, sizeof(sc));
+  lfd::RCoef rc{};
+  make_rcoef(m, rc, fir32);
   kc.r = rc;
   sc.r = rc;
   // reverse state-space in T coordinates (T(m) = A T(m+1) + B y)
@@ -1017,9 +1076,85 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   delete p;
 }
 
+}  // extern "C"
+
+namespace {
+// ---------------------------------------------------------------------------
+// Full-rate path (lfd_sosfiltfilt_f32): k_fullrate_wave functionals over big
+// blocks of FR_L samples -> k_fullrate_scan per channel (edges, states at
+// every block start, the tail's outputs) -> k_fullrate_wave outputs.  The
+// tail [nb * FR_L, n_t) keeps at least one sample (the reverse pass starts
+// from y_f[-1], which the scan computes).
+// ---------------------------------------------------------------------------
+int64_t fullrate_blocks(int64_t n_t) {  // the tail keeps >= 1 sample
+  return n_t > 1 ? (n_t - 1) / lfd::FR_L : 0;
+}
+
+struct FrLayout {
+  size_t off_F, off_SF, off_ST, off_TP, bytes;
+};
+FrLayout fullrate_layout(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64_t nb) {
+  const size_t n = 2 * n_sec;
+  FrLayout l{};
+  l.off_F = 0;
+  l.off_SF = align256(sizeof(double) * 2 * n * nb * n_ch);
+  l.off_ST = l.off_SF + align256(sizeof(double) * n * (nb + 1) * n_ch);
+  l.off_TP = l.off_ST + align256(sizeof(double) * n * (nb + 1) * n_ch);
+  l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - nb * lfd::FR_L + padlen) * n_ch);
+  return l;
+}
+
+// Per-(device, cascade) device constants, built on first use (the per-call
+// path then allocates nothing and never synchronises).
+struct FrEntry {
+  int dev = -1, n_sec = 0;
+  double sos[6 * MAX_SEC] = {0};
+  lfd::FRConst *d_fc = nullptr;
+};
+std::mutex g_fr_mu;
+std::vector<std::unique_ptr<FrEntry>> g_fr;
+
+int fullrate_entry(const double *sos, int n_sec, const Cascade &c, const FrEntry **out) {
+  int dev = 0;
+  LFD_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_fr_mu);
+  for (const auto &e : g_fr)
+    if (e->dev == dev && e->n_sec == n_sec && std::memcmp(e->sos, sos, sizeof(double) * 6 * n_sec) == 0) {
+      *out = e.get();
+      return LFD_OK;
+    }
+  auto e = std::make_unique<FrEntry>();
+  e->dev = dev;
+  e->n_sec = n_sec;
+  std::memcpy(e->sos, sos, sizeof(double) * 6 * n_sec);
+  auto fc = std::make_unique<lfd::FRConst>();
+  fullrate_constants(c, *fc);
+  LFD_HIP(hipMalloc(&e->d_fc, sizeof(lfd::FRConst)));
+  const hipError_t he = hipMemcpy(e->d_fc, fc.get(), sizeof(lfd::FRConst), hipMemcpyHostToDevice);
+  if (he != hipSuccess) {
+    (void)hipFree(e->d_fc);
+    return fail(LFD_EHIP, std::string("full-rate constants: ") + hipGetErrorString(he));
+  }
+  if (g_fr.size() >= 16) {  // bounded: drop the oldest (hipFree waits for the device)
+    (void)hipFree(g_fr.front()->d_fc);
+    g_fr.erase(g_fr.begin());
+  }
+  g_fr.push_back(std::move(e));
+  *out = g_fr.back().get();
+  return LFD_OK;
+}
+}  // namespace
+
+extern "C" {
+
 size_t lfd_sosfiltfilt_workspace_bytes(int64_t n_ch, int64_t n_t, int padlen, int n_sec) {
   if (padlen < 0) padlen = 3 * (2 * n_sec + 1);
-  return align256(sizeof(double) * (size_t)(n_t + 2 * (int64_t)padlen) * (size_t)n_ch);
+  size_t b = align256(sizeof(double) * (size_t)(n_t + 2 * (int64_t)padlen) * (size_t)n_ch);
+  if (n_sec >= 1 && n_sec <= MAX_SEC && n_ch >= 1) {
+    const int64_t nb = fullrate_blocks(n_t);
+    if (nb > 0) b = std::max(b, fullrate_layout(n_ch, n_t, padlen, n_sec, nb).bytes);
+  }
+  return b;
 }
 
 int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
@@ -1042,11 +1177,32 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     cf.a1[s] = c.a1[s];
     cf.a2[s] = c.a2[s];
   }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // blocked path (k_fullrate_wave -> k_fullrate_scan -> k_fullrate_wave) when
+  // the array holds a big block; LFD_FULLRATE_SERIAL=1 (A/B knob) keeps the
+  // one-thread-per-channel kernel
+  const int64_t nb = fullrate_blocks(n_t);
+  if (nb > 0 && !env_flag("LFD_FULLRATE_SERIAL")) {
+    const FrEntry *fe = nullptr;
+    if (int e = fullrate_entry(sos, n_sec, c, &fe)) return e;
+    const FrLayout lo = fullrate_layout(n_ch, n_t, padlen, n_sec, nb);
+    char *ws = static_cast<char *>(workspace);
+    double *F = reinterpret_cast<double *>(ws + lo.off_F);
+    double *SF = reinterpret_cast<double *>(ws + lo.off_SF);
+    double *ST = reinterpret_cast<double *>(ws + lo.off_ST);
+    double *TP = reinterpret_cast<double *>(ws + lo.off_TP);
+    LFD_HIP(lfd::launch_fullrate_blocks(n_sec, false, x, s_ch, s_t, n_ch, nb, fe->d_fc, nullptr, nullptr, F,
+                                        nullptr, 0, 0, st));
+    LFD_HIP(lfd::launch_fullrate_scan(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F, SF, ST, TP, y,
+                                      ys_ch, ys_t, st));
+    LFD_HIP(lfd::launch_fullrate_blocks(n_sec, true, x, s_ch, s_t, n_ch, nb, fe->d_fc, SF, ST, nullptr, y,
+                                        ys_ch, ys_t, st));
+    return LFD_OK;
+  }
   lfd::ZiVec zi{};
   sosfilt_zi(c, zi.v);
   LFD_HIP(lfd::launch_sosfiltfilt(n_sec, x, n_ch, n_t, s_ch, s_t, cf, zi, padlen,
-                                  static_cast<double *>(workspace), y, ys_ch, ys_t,
-                                  reinterpret_cast<hipStream_t>(stream)));
+                                  static_cast<double *>(workspace), y, ys_ch, ys_t, st));
   return LFD_OK;
 }
 

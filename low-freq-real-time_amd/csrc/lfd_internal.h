@@ -156,7 +156,44 @@ struct RunGeom {
   const RunConst *rc;
 };
 
+// Full-rate zero-phase filter (lfd_sosfiltfilt_f32), in SciPy's own
+// coordinates: the TDF-II state z of every section (SosCoef; dimension
+// N = 2 n_sec).  Big blocks of FR_L = 64 x FR_LS samples; a wave owns one
+// (channel, big block) and each lane one FR_LS-sample sub-block.  Inside the
+// wave the sub-block states are combined by log-step scans over the lanes
+// with the zero-input transition over FR_LS * 2^i samples (PhiP[i]; the
+// reverse pass runs the same cascade on the reversed signal, so it shares
+// it).  H[i][n]: forward output i samples into a sub-block per unit entering
+// state e_n.  Between the two wave passes k_fullrate_scan walks the big
+// blocks per channel:  S_f(k+1) = PhiL S_f(k) + e_f(k),
+// T(k) = PhiL T(k+1) + e_r(k) + M S_f(k)  (T(k): reverse state after sample
+// k * FR_L).
+constexpr int FR_LS = 32;
+constexpr int FR_L = 64 * FR_LS;
+struct FRConst {
+  SosCoef cf;
+  ZiVec zi;                       // sosfilt_zi (unit step steady state)
+  double PhiP[6][MAX_N * MAX_N];  // row-major, stride MAX_N
+  double PhiL[MAX_N * MAX_N];     // over FR_L samples
+  double M[MAX_N * MAX_N];        // reverse exit state over a big block per forward state entering it
+  double H[FR_LS][MAX_N];
+};
+// Layouts (channel fastest, so the scan's per-channel threads coalesce):
+//   F [k][2N][ch] (e_f then e_r), SF / ST [k][N][ch] for k in [0, nb].
+
 // Launchers (lfd_kernels.hip).  All return hipError_t of the launch.
+// Full-rate wave kernels: out == false writes the big blocks' functionals F;
+// out == true reads the scan's SF / ST and writes y[ch, 0 : nb * FR_L].
+hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s_ch, int64_t s_t,
+                                  int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
+                                  const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
+                                  hipStream_t st);
+// Per-channel walk over the big blocks + both edges (odd extension, zi) and
+// the outputs of the tail [nb * FR_L, n_t).  TP: (n_t - nb * FR_L + padlen) x n_ch.
+hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch,
+                                int64_t n_t, int64_t nb, int padlen, const FRConst *fc, const double *F,
+                                double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
+                                hipStream_t st);
 // MFMA block functionals: s_t == 1, s_ch % 4 == 0, 16-B aligned x.
 hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n_t,
                                          const BlockGeom &g, const double *taps,

@@ -828,6 +828,229 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 }
 
 // ---------------------------------------------------------------------------
+// Full-rate zero-phase filter (lfd_internal.h FRConst): SciPy's TDF-II
+// cascade, blocked.  k_fullrate_wave: one wave = one (channel, big block of
+// FR_L samples); lane j owns the FR_LS-sample sub-block a + j*FR_LS.  Per
+// lane, in registers:
+//   1. TDF-II forward over the sub-block from zero state -> y0, exit A_j;
+//   2. wave scan S_{j+1} = PhiP S_j + A_j (log-step over the lanes), S_0 =
+//      the state entering the big block (SF; 0 for the functionals);
+//   3. y_f = y0 + H S_j;
+//   4. TDF-II over the reversed y_f from zero state -> Z_j, wave scan
+//      T_j = PhiP T_{j+1} + Z_j from the right (T_64 = ST(k+1); 0 for the
+//      functionals);
+//   5. (out) the reverse pass again from T_{j+1}, emitting the outputs.
+// Functional mode writes e_f = S_64 and e_r = T_0.  Every recurrence runs in
+// its own direction (stable for any pole radius) and in SciPy's coordinates.
+// x comes through LDS (row loads; a 4-float pad per 32 keeps the lanes'
+// float4 reads conflict-free) and y leaves through LDS as row stores.
+// ---------------------------------------------------------------------------
+template <int NS, bool OUT>
+__global__ __launch_bounds__(64, 2) void k_fullrate_wave(
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t nb,
+    const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
+    double *__restrict__ F, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+  constexpr int N = 2 * NS, LS = FR_LS, L = FR_L;
+  static_assert(LS == 32, "tile reads assume 32-sample sub-blocks");
+  constexpr int TLDS = L + 4 * (L / 32);
+  constexpr int OSTR = LS + 1;  // output row stride (doubles)
+  constexpr int NLDS = 64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2;
+  __shared__ __attribute__((aligned(16))) double lds[NLDS];
+  float *tile = reinterpret_cast<float *>(lds);
+  const int lane = threadIdx.x;
+  const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
+  const int64_t a = k * L;
+  {
+    const float *row = x + ch * s_ch + a * s_t;
+#pragma unroll 8
+    for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = row[u * s_t];
+  }
+  __syncthreads();
+  FwdRec<NS> fr;
+  fr.load(fc->cf);
+  // ---- 1. zero-state forward
+  double yf[LS], A[N];
+  {
+    float xs[LS];
+    const float *tr = tile + 36 * lane;
+#pragma unroll
+    for (int g = 0; g < LS / 4; ++g) {
+      const float4 v = *reinterpret_cast<const float4 *>(tr + 4 * g);
+      xs[4 * g + 0] = v.x;
+      xs[4 * g + 1] = v.y;
+      xs[4 * g + 2] = v.z;
+      xs[4 * g + 3] = v.w;
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n) A[n] = 0.0;
+#pragma unroll
+    for (int i = 0; i < LS; ++i) yf[i] = fr.step(A, (double)xs[i]);
+  }
+  auto matvec_add = [&](const double *P, const double (&o)[N], double (&v)[N]) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double acc = v[r];
+#pragma unroll
+      for (int c = 0; c < N; ++c) acc = fma(P[r * MAX_N + c], o[c], acc);
+      v[r] = acc;
+    }
+  };
+  // ---- 2. forward wave scan
+  double Sin[N], vf[N], Sj[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    Sin[n] = OUT ? SF[(k * N + n) * n_ch + ch] : 0.0;
+    vf[n] = A[n];
+  }
+  if (OUT && lane == 0) matvec_add(fc->PhiP[0], Sin, vf);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int d = 1 << i;
+    double o[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) o[n] = __shfl_up(vf[n], d);
+    if (lane >= d) matvec_add(fc->PhiP[i], o, vf);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const double u = __shfl_up(vf[n], 1);
+    Sj[n] = lane == 0 ? Sin[n] : u;
+  }
+  // ---- 3. true forward output
+#pragma unroll
+  for (int i = 0; i < LS; ++i)
+#pragma unroll
+    for (int n = 0; n < N; ++n) yf[i] = fma(fc->H[i][n], Sj[n], yf[i]);
+  // ---- 4. zero-state reverse + backward wave scan
+  double vb[N], Tin[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) vb[n] = 0.0;
+#pragma unroll
+  for (int i = LS - 1; i >= 0; --i) (void)fr.step(vb, yf[i]);
+#pragma unroll
+  for (int n = 0; n < N; ++n) Tin[n] = OUT ? ST[((k + 1) * N + n) * n_ch + ch] : 0.0;
+  if (OUT && lane == 63) matvec_add(fc->PhiP[0], Tin, vb);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int d = 1 << i;
+    double o[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) o[n] = __shfl_down(vb[n], d);
+    if (lane + d < 64) matvec_add(fc->PhiP[i], o, vb);
+  }
+  if constexpr (!OUT) {
+    if (lane == 63) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) F[(k * 2 * N + n) * n_ch + ch] = vf[n];
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) F[(k * 2 * N + N + n) * n_ch + ch] = vb[n];
+    }
+    return;
+  }
+  // ---- 5. output pass from T_{j+1}
+  double T[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const double u = __shfl_down(vb[n], 1);
+    T[n] = lane == 63 ? Tin[n] : u;
+  }
+  double *ob = lds;
+#pragma unroll
+  for (int i = LS - 1; i >= 0; --i) ob[lane * OSTR + i] = fr.step(T, yf[i]);
+  __syncthreads();
+  double *yr = y + ch * ys_ch + a * ys_t;
+#pragma unroll 8
+  for (int o = lane; o < L; o += 64) yr[o * ys_t] = ob[(o / LS) * OSTR + (o % LS)];
+}
+
+// k_fullrate_scan: one thread per channel.  SciPy's left edge (odd extension,
+// zi * ext[0]) -> S_f at every big block start -> the tail + right pad
+// forward (TP) -> reverse from zi * y_f[-1] over pad + tail, writing the
+// tail's outputs -> T at every big block start, backward.
+template <int NS>
+__global__ __launch_bounds__(256) void k_fullrate_scan(
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t nb, int padlen,
+    const FRConst *__restrict__ fc, const double *__restrict__ F, double *__restrict__ SF,
+    double *__restrict__ ST, double *__restrict__ TP, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+  constexpr int N = 2 * NS;
+  const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= n_ch) return;
+  FwdRec<NS> fr;
+  fr.load(fc->cf);
+  const float *xc = x + ch * s_ch;
+  const int E = padlen;
+  const int64_t n_ext = n_t + 2 * (int64_t)E;
+  const float x0 = xc[0], xn = xc[(n_t - 1) * s_t];
+  auto ext = [&](int64_t t) -> double {  // scipy odd extension, float32 like numpy
+    if (t < E) return (double)(2.0f * x0 - xc[(E - t) * s_t]);
+    if (t < E + n_t) return (double)xc[(t - E) * s_t];
+    return (double)(2.0f * xn - xc[(n_t - 2 - (t - E - n_t)) * s_t]);
+  };
+  double z[N];
+  {
+    const double e0 = ext(0);
+#pragma unroll
+    for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * e0;
+  }
+  for (int64_t t = 0; t < E; ++t) (void)fr.step(z, ext(t));
+  auto matvec = [&](const double *P, const double (&v)[N], double (&o)[N]) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double acc = o[r];
+#pragma unroll
+      for (int c = 0; c < N; ++c) acc = fma(P[r * MAX_N + c], v[c], acc);
+      o[r] = acc;
+    }
+  };
+  // forward over the big blocks
+  for (int64_t k = 0; k < nb; ++k) {
+    double nz[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      SF[(k * N + n) * n_ch + ch] = z[n];
+      nz[n] = F[(k * 2 * N + n) * n_ch + ch];
+    }
+    matvec(fc->PhiL, z, nz);
+#pragma unroll
+    for (int n = 0; n < N; ++n) z[n] = nz[n];
+  }
+  // tail + right pad, forward
+  const int64_t t_tail = E + nb * FR_L;
+  double yl = 0.0;
+  for (int64_t t = t_tail; t < n_ext; ++t) {
+    yl = fr.step(z, ext(t));
+    TP[(t - t_tail) * n_ch + ch] = yl;
+  }
+  // reverse over pad + tail
+#pragma unroll
+  for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * yl;
+  for (int64_t t = n_ext - 1; t >= t_tail; --t) {
+    const double v = fr.step(z, TP[(t - t_tail) * n_ch + ch]);
+    if (t < E + n_t) y[ch * ys_ch + (t - E) * ys_t] = v;
+  }
+  // reverse over the big blocks
+#pragma unroll
+  for (int n = 0; n < N; ++n) ST[(nb * N + n) * n_ch + ch] = z[n];
+  for (int64_t k = nb - 1; k >= 0; --k) {
+    double sf[N], nz[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      sf[n] = SF[(k * N + n) * n_ch + ch];
+      nz[n] = F[(k * 2 * N + N + n) * n_ch + ch];
+    }
+    matvec(fc->PhiL, z, nz);
+    matvec(fc->M, sf, nz);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      z[n] = nz[n];
+      ST[(k * N + n) * n_ch + ch] = z[n];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Full-rate sosfiltfilt: one thread per channel; forward outputs staged in a
 // float64 workspace laid out [t][ch] (coalesced across channels).
 // ---------------------------------------------------------------------------
@@ -2393,6 +2616,50 @@ hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch
     default: return hipErrorInvalidValue;
   }
 #undef LFD_SCAN
+  return hipGetLastError();
+}
+
+hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s_ch, int64_t s_t,
+                                  int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
+                                  const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
+                                  hipStream_t st) {
+  const int64_t n_wg = n_ch * nb;
+  if (n_wg < 1 || n_wg > INT32_MAX) return hipErrorInvalidValue;
+#define LFD_FR(NS, OUT)                                                                                \
+  k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
+                                                         ys_t)
+#define LFD_FR2(NS)   \
+  if (out)            \
+    LFD_FR(NS, true); \
+  else                \
+    LFD_FR(NS, false)
+  switch (n_sec) {
+    case 1: LFD_FR2(1); break;
+    case 2: LFD_FR2(2); break;
+    case 3: LFD_FR2(3); break;
+    case 4: LFD_FR2(4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LFD_FR2
+#undef LFD_FR
+  return hipGetLastError();
+}
+
+hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch,
+                                int64_t n_t, int64_t nb, int padlen, const FRConst *fc, const double *F,
+                                double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
+                                hipStream_t st) {
+  const unsigned g = nblk(n_ch, 64);
+#define LFD_FRS(NS) \
+  k_fullrate_scan<NS><<<g, 64, 0, st>>>(x, s_ch, s_t, n_ch, n_t, nb, padlen, fc, F, SF, ST, TP, y, ys_ch, ys_t)
+  switch (n_sec) {
+    case 1: LFD_FRS(1); break;
+    case 2: LFD_FRS(2); break;
+    case 3: LFD_FRS(3); break;
+    case 4: LFD_FRS(4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LFD_FRS
   return hipGetLastError();
 }
 

@@ -289,6 +289,56 @@ def test_full_rate_filtfilt_parity():
     assert _relrms(y, oracle.sosfiltfilt(sos, x)) < 1e-10
 
 
+@pytest.mark.parametrize("case", [
+    # (fs, lo, hi, n_t, padlen): band-pass with heavily damped poles
+    # (|p| = 0.48), a low-pass with poles at |p| = 0.9988, 2nd/6th-order
+    # cascades, padlen 0 / long, tails of 1..2048 samples (big blocks of 2048)
+    (250.0, 0.2, 30.0, 20000, None),
+    (500.0, None, 1.0, 9000, None),
+    (1000.0, 1.0, 10.0, 2 * 2048 + 1, None),
+    (1000.0, 1.0, 10.0, 2 * 2048, None),
+    (1000.0, 1.0, 10.0, 3 * 2048 + 5, 0),
+    (250.0, 2.0, None, 6000, 700),
+])
+def test_full_rate_blocked_parity(case):
+    """lfd_sosfiltfilt_f32's blocked path (k_fullrate_wave functionals ->
+    k_fullrate_scan -> k_fullrate_wave outputs) against SciPy's sosfiltfilt
+    restatement: relRMS < 1e-10 per channel."""
+    import torch
+    from lfdas.plan import sosfiltfilt_device
+    fs, lo, hi, n_t, padlen = case
+    sos = oracle.dascore_pass_filter_sos(fs, lo, hi)
+    rng = np.random.default_rng(n_t)
+    x = (rng.standard_normal((5, n_t)) + 3).astype(np.float32)
+    pl = -1 if padlen is None else padlen
+    y = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos, pl).cpu().numpy()
+    ref = oracle.sosfiltfilt(sos, x, padlen=padlen)
+    for c in range(x.shape[0]):
+        assert _relrms(y[c], ref[c]) < 1e-10, c
+    for order in (2, 6):  # other cascade lengths (n_sec = 1, 3)
+        sos2 = oracle.butter_sos(order, 0.05)
+        y2 = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos2, pl).cpu().numpy()
+        assert _relrms(y2, oracle.sosfiltfilt(sos2, x, padlen=padlen)) < 1e-10
+
+
+def test_full_rate_blocked_strides_and_nan():
+    """Strided input (a column view of a (time, channel) array) and a channel
+    holding a NaN: the NaN channel is all-NaN like SciPy's, the others are
+    unaffected."""
+    import torch
+    from lfdas.plan import sosfiltfilt_device
+    sos = oracle.dascore_pass_filter_sos(500.0, 0.5, 20.0)
+    rng = np.random.default_rng(77)
+    xt = rng.standard_normal((7000, 6)).astype(np.float32)
+    xt[3000, 2] = np.nan
+    xd = torch.from_numpy(xt).cuda().t()  # (channel, time) view, s_t = 6
+    y = sosfiltfilt_device(xd, sos).cpu().numpy()
+    ref = oracle.sosfiltfilt(sos, xt.T)
+    assert np.isnan(y[2]).all() and np.isnan(ref[2]).all()
+    m = [0, 1, 3, 4, 5]
+    assert _relrms(y[m], ref[m]) < 1e-10
+
+
 def test_execute_is_graph_capturable():
     """lfd_lowpass_execute allocates nothing and never synchronises, so a
     whole chunked low-pass (K1 + scan) can be captured once as a HIP graph and
