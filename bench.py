@@ -389,6 +389,89 @@ def bench_rolling(dev, W, S_, reps=10):
                          "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_sample": 4 + 4 / S_}}
 
 
+def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=5):
+    """Full-rate zero-phase band-pass (DASCore ``pass_filter(time=band)``
+    .data -> scipy sosfiltfilt): 2,000 ch x 10 min @ 1 kHz, 8th-order
+    Butterworth band-pass (4 sections), float32 in, float64 out (SciPy's
+    dtype).  Algorithmic bytes 4 + 8 per channel-sample.  The dominant
+    kernel is the output pass k_fullrate_wave<4, true> (x read + y written
+    over the big blocks, 12 B per sample)."""
+    import os as _os
+
+    import torch
+    import oracle
+    from lfdas.plan import load, set_timing, sosfiltfilt_device, sosfiltfilt_last_timing_ms
+    sos = oracle.dascore_pass_filter_sos(fs, band[0], band[1])
+    x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
+    synth_fill(x, fs, 77)
+    y = torch.empty((n_ch, n), dtype=torch.float64, device=dev)
+    wsb = load().lfd_sosfiltfilt_workspace_bytes(n_ch, n, -1, sos.shape[0])
+    ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        sosfiltfilt_device(x, sos, y=y, ws=ws)
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        sosfiltfilt_device(x, sos, y=y, ws=ws)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    set_timing(True)
+    kt = []
+    for _ in range(reps):
+        sosfiltfilt_device(x, sos, y=y, ws=ws)
+        kt.append(sosfiltfilt_last_timing_ms())
+    set_timing(False)
+    kt = np.mean(np.array(kt), axis=0)
+    L = 2048
+    nb = (n - 1) // L
+    gbs_out = n_ch * nb * L * 12 / (kt[2] * 1e-3) / 1e9
+    gbs_all = n_ch * n * 12 / (ms * 1e-3) / 1e9
+    # parity spot check outside the timed region (3 channels vs the oracle)
+    rows = [0, n_ch // 2, n_ch - 1]
+    xs = x[rows].cpu().numpy()
+    rel = float(np.sqrt(np.sum((y[rows].cpu().numpy() - oracle.sosfiltfilt(sos, xs)) ** 2)
+                        / np.sum(oracle.sosfiltfilt(sos, xs) ** 2)))
+    # the previous one-thread-per-channel kernel on a tenth of the samples
+    _os.environ["LFD_FULLRATE_SERIAL"] = "1"
+    try:
+        xs10 = x[:, : n // 10]
+        ys10 = y[:, : n // 10]
+        sosfiltfilt_device(xs10, sos, y=ys10, ws=ws)
+        torch.cuda.synchronize(dev)
+        e0.record()
+        sosfiltfilt_device(xs10, sos, y=ys10, ws=ws)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        serial_ms = e0.elapsed_time(e1)
+    finally:
+        del _os.environ["LFD_FULLRATE_SERIAL"]
+    # CPU: SciPy's sosfiltfilt itself on 24 channels (single core)
+    from scipy.signal import sosfiltfilt as sp_sosfiltfilt
+    xc = x[:24].cpu().numpy()
+    ta = time.perf_counter()
+    sp_sosfiltfilt(sos, xc, axis=-1)
+    cpu_s = time.perf_counter() - ta
+    del x, y, ws
+    torch.cuda.empty_cache()
+    return {"value": n_ch * n / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms,
+            "config": f"{n_ch:,} ch x {n:,} @ {fs:g} Hz fp32 -> f64, Butterworth band-pass {band} Hz "
+                      f"(corners=4, {sos.shape[0]} sections), zero-phase, full rate",
+            "kernels_ms": {"k_fullrate_wave<4,false> (functionals)": kt[0], "k_fullrate_scan<4>": kt[1],
+                           "k_fullrate_wave<4,true> (output)": kt[2]},
+            "roofline": {"bound": "hbm", "kernel": "k_fullrate_wave<4,true>", "achieved": gbs_out,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs_out / HBM_PEAK_GBS,
+                         "alg_bytes_per_sample": 12, "samples_per_launch": n_ch * nb * L},
+            "pipeline_hbm_frac": gbs_all / HBM_PEAK_GBS,
+            "relrms_vs_oracle_3ch": rel,
+            "serial_kernel_ms_tenth": serial_ms,
+            "serial_kernel_value": n_ch * (n // 10) / (serial_ms * 1e-3),
+            "cpu_baseline": {"value": 24 * n / cpu_s, "unit": "channel-samples/s", "cores": 1,
+                             "kind": "reference-lib", "sample": f"scipy.signal.sosfiltfilt, 24 ch x {n:,}"}}
+
+
 def _cpu_worker(a, barrier=None, q=None):
     """One CPU-baseline process: the LFProc chunks of ``n_c`` channels x the
     full hour (own data, made before the start barrier)."""
@@ -579,6 +662,8 @@ def main():
             dev, 10_000, 1000.0, 3600.0, 10.0, 120, 6,
             label="10,000 ch x 1 h @ 1 kHz (144 GB), dt = 10 s (the batch notebook's d_t), P = 120, B = 6: "
                   "R = 10,000 as 20 sub-blocks of 500")
+    if ws == 1 and not args.no_extra:
+        secondary["fullrate_bandpass"] = bench_fullrate(dev)
     if not args.no_rolling and ws == 1:
         secondary["rolling_mean_cfg2"] = bench_rolling(dev, 1000, 1000)
         secondary["rolling_mean_cfg2_step1"] = bench_rolling(dev, 1000, 1, reps=5)

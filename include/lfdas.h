@@ -150,6 +150,11 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t,
                         int64_t s_ch, int64_t s_t, const double *sos,
                         int n_sec, int padlen, double *y, int64_t ys_ch,
                         int64_t ys_t, void *workspace, void *stream);
+/* With lfd_set_timing(1): the last blocked lfd_sosfiltfilt_f32's kernel times
+ * (ms; waits for them): big-block functionals, per-channel scan, output pass.
+ * LFD_EINVAL when that call was untimed or took the serial kernel. */
+int lfd_sosfiltfilt_last_timing(float *ms_functionals, float *ms_scan,
+                                float *ms_output);
 
 /* Linear interpolation of a device float64 array along time at positions
  * lo[j] + w[j] (DASCore Patch.interpolate → interp1d, _interpolate.py:457). */

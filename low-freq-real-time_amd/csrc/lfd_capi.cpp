@@ -327,7 +327,16 @@ void fullrate_constants(const Cascade &cs, lfd::FRConst &fc) {
     R t[MAX_N] = {0};
     for (int i = lfd::FR_L - 1; i >= 0; --i) (void)tdf2_step(cs, t, yv[i]);
     for (int r = 0; r < n; ++r) fc.M[r * MAX_N + c] = (double)t[r];
+    R u[MAX_N] = {0};
+    for (int i = lfd::FR_LS - 1; i >= 0; --i) fc.Rh[i][c] = (double)tdf2_step(cs, u, yv[i]);
+    for (int r = 0; r < n; ++r) fc.M32[r * MAX_N + c] = (double)u[r];
   }
+  for (int mt = 0; mt < 2; ++mt)
+    for (int ks = 0; ks < 4; ++ks)
+      for (int l = 0; l < 64; ++l) {
+        const int i = 16 * mt + (l & 15), kk = 4 * ks + (l >> 4);
+        fc.QA[mt][ks][l] = kk < n ? fc.Rh[i][kk] : (kk < 2 * n ? fc.H[lfd::FR_LS - 1 - i][kk - n] : 0.0);
+      }
 }
 
 // Fill the block-functional and scan constants for block length L and output
@@ -1113,6 +1122,10 @@ struct FrEntry {
 };
 std::mutex g_fr_mu;
 std::vector<std::unique_ptr<FrEntry>> g_fr;
+// lfd_set_timing(1): events around the three launches of the last blocked call
+hipEvent_t g_fr_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+int g_fr_ev_dev = -1;
+bool g_fr_timed = false;
 
 int fullrate_entry(const double *sos, int n_sec, const Cascade &c, const FrEntry **out) {
   int dev = 0;
@@ -1191,18 +1204,50 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     double *SF = reinterpret_cast<double *>(ws + lo.off_SF);
     double *ST = reinterpret_cast<double *>(ws + lo.off_ST);
     double *TP = reinterpret_cast<double *>(ws + lo.off_TP);
+    const bool timed = lfd::timing_enabled();
+    if (timed) {
+      std::lock_guard<std::mutex> lk(g_fr_mu);
+      int dev = 0;
+      LFD_HIP(hipGetDevice(&dev));
+      if (g_fr_ev_dev != dev) {
+        for (auto &ev : g_fr_ev)
+          if (ev) (void)hipEventDestroy(ev);
+        for (auto &ev : g_fr_ev) LFD_HIP(hipEventCreate(&ev));
+        g_fr_ev_dev = dev;
+      }
+      g_fr_timed = true;
+    } else {
+      g_fr_timed = false;
+    }
+    if (timed) LFD_HIP(hipEventRecord(g_fr_ev[0], st));
     LFD_HIP(lfd::launch_fullrate_blocks(n_sec, false, x, s_ch, s_t, n_ch, nb, fe->d_fc, nullptr, nullptr, F,
                                         nullptr, 0, 0, st));
+    if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
     LFD_HIP(lfd::launch_fullrate_scan(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F, SF, ST, TP, y,
                                       ys_ch, ys_t, st));
+    if (timed) LFD_HIP(hipEventRecord(g_fr_ev[2], st));
     LFD_HIP(lfd::launch_fullrate_blocks(n_sec, true, x, s_ch, s_t, n_ch, nb, fe->d_fc, SF, ST, nullptr, y,
                                         ys_ch, ys_t, st));
+    if (timed) LFD_HIP(hipEventRecord(g_fr_ev[3], st));
     return LFD_OK;
   }
   lfd::ZiVec zi{};
   sosfilt_zi(c, zi.v);
   LFD_HIP(lfd::launch_sosfiltfilt(n_sec, x, n_ch, n_t, s_ch, s_t, cf, zi, padlen,
                                   static_cast<double *>(workspace), y, ys_ch, ys_t, st));
+  return LFD_OK;
+}
+
+int lfd_sosfiltfilt_last_timing(float *ms_functionals, float *ms_scan, float *ms_output) {
+  if (!g_fr_timed) return fail(LFD_EINVAL, "timing was not enabled for the last blocked full-rate call");
+  LFD_HIP(hipEventSynchronize(g_fr_ev[3]));
+  float a = 0, b = 0, c = 0;
+  LFD_HIP(hipEventElapsedTime(&a, g_fr_ev[0], g_fr_ev[1]));
+  LFD_HIP(hipEventElapsedTime(&b, g_fr_ev[1], g_fr_ev[2]));
+  LFD_HIP(hipEventElapsedTime(&c, g_fr_ev[2], g_fr_ev[3]));
+  if (ms_functionals) *ms_functionals = a;
+  if (ms_scan) *ms_scan = b;
+  if (ms_output) *ms_output = c;
   return LFD_OK;
 }
 

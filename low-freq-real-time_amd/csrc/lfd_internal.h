@@ -163,8 +163,7 @@ struct RunGeom {
 // wave the sub-block states are combined by log-step scans over the lanes
 // with the zero-input transition over FR_LS * 2^i samples (PhiP[i]; the
 // reverse pass runs the same cascade on the reversed signal, so it shares
-// it).  H[i][n]: forward output i samples into a sub-block per unit entering
-// state e_n.  Between the two wave passes k_fullrate_scan walks the big
+// it).  Between the two wave passes k_fullrate_scan walks the big
 // blocks per channel:  S_f(k+1) = PhiL S_f(k) + e_f(k),
 // T(k) = PhiL T(k+1) + e_r(k) + M S_f(k)  (T(k): reverse state after sample
 // k * FR_L).
@@ -176,7 +175,13 @@ struct FRConst {
   double PhiP[6][MAX_N * MAX_N];  // row-major, stride MAX_N
   double PhiL[MAX_N * MAX_N];     // over FR_L samples
   double M[MAX_N * MAX_N];        // reverse exit state over a big block per forward state entering it
-  double H[FR_LS][MAX_N];
+  double M32[MAX_N * MAX_N];      // the same over one sub-block
+  double H[FR_LS][MAX_N];         // zero-input output i steps after unit state e_n
+  double Rh[FR_LS][MAX_N];        // zero-state reverse output at i of H's forward output
+  // output table Q[i][kk] = (Rh[i][kk] | H[31 - i][kk - N]) as the A operand of
+  // v_mfma_f64_16x16x4 per 16-row tile mt and k-step ks:
+  // QA[mt][ks][l] = Q[16 mt + (l & 15)][4 ks + (l >> 4)]
+  double QA[2][4][64];
 };
 // Layouts (channel fastest, so the scan's per-channel threads coalesce):
 //   F [k][2N][ch] (e_f then e_r), SF / ST [k][N][ch] for k in [0, nb].

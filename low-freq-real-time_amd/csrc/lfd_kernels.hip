@@ -833,28 +833,33 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 // FR_L samples); lane j owns the FR_LS-sample sub-block a + j*FR_LS.  Per
 // lane, in registers:
 //   1. TDF-II forward over the sub-block from zero state -> y0, exit A_j;
-//   2. wave scan S_{j+1} = PhiP S_j + A_j (log-step over the lanes), S_0 =
+//   2. TDF-II over the reversed y0 from zero state -> r0 (outputs), exit Z0_j;
+//   3. wave scan S_{j+1} = PhiP S_j + A_j (log-step over the lanes), S_0 =
 //      the state entering the big block (SF; 0 for the functionals);
-//   3. y_f = y0 + H S_j;
-//   4. TDF-II over the reversed y_f from zero state -> Z_j, wave scan
-//      T_j = PhiP T_{j+1} + Z_j from the right (T_64 = ST(k+1); 0 for the
-//      functionals);
-//   5. (out) the reverse pass again from T_{j+1}, emitting the outputs.
+//   4. Z_j = Z0_j + M32 S_j, wave scan T_j = PhiP T_{j+1} + Z_j from the
+//      right (T_64 = ST(k+1); 0 for the functionals);
+//   5. (out) y[i] = r0[i] + Rh[i] S_j + H[31 - i] T_{j+1}  (linearity: the
+//      forward state's and the reverse state's responses; fp64 MFMA).
 // Functional mode writes e_f = S_64 and e_r = T_0.  Every recurrence runs in
 // its own direction (stable for any pole radius) and in SciPy's coordinates.
 // x comes through LDS (row loads; a 4-float pad per 32 keeps the lanes'
 // float4 reads conflict-free) and y leaves through LDS as row stores.
 // ---------------------------------------------------------------------------
+typedef double fr_d4v __attribute__((ext_vector_type(4)));
+#ifndef FR_WAVES
+#define FR_WAVES 4  // waves per SIMD the register budget targets (<= 128 VGPRs)
+#endif
+
 template <int NS, bool OUT>
-__global__ __launch_bounds__(64, 2) void k_fullrate_wave(
+__global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t nb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
     double *__restrict__ F, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L;
   static_assert(LS == 32, "tile reads assume 32-sample sub-blocks");
   constexpr int TLDS = L + 4 * (L / 32);
-  constexpr int OSTR = LS + 1;  // output row stride (doubles)
-  constexpr int NLDS = 64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2;
+  constexpr int OSTR = 17;  // output stage row stride (doubles): 16 samples + 1
+  constexpr int NLDS = !OUT ? TLDS / 2 : (64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2);
   __shared__ __attribute__((aligned(16))) double lds[NLDS];
   float *tile = reinterpret_cast<float *>(lds);
   const int lane = threadIdx.x;
@@ -868,8 +873,8 @@ __global__ __launch_bounds__(64, 2) void k_fullrate_wave(
   __syncthreads();
   FwdRec<NS> fr;
   fr.load(fc->cf);
-  // ---- 1. zero-state forward
-  double yf[LS], A[N];
+  // ---- 1, 2. zero-state forward, then zero-state reverse over its output
+  double r0[LS], A[N], Z[N];
   {
     float xs[LS];
     const float *tr = tile + 36 * lane;
@@ -882,61 +887,61 @@ __global__ __launch_bounds__(64, 2) void k_fullrate_wave(
       xs[4 * g + 3] = v.w;
     }
 #pragma unroll
-    for (int n = 0; n < N; ++n) A[n] = 0.0;
+    for (int n = 0; n < N; ++n) A[n] = Z[n] = 0.0;
 #pragma unroll
-    for (int i = 0; i < LS; ++i) yf[i] = fr.step(A, (double)xs[i]);
+    for (int i = 0; i < LS; ++i) r0[i] = fr.step(A, (double)xs[i]);
+#pragma unroll
+    for (int i = LS - 1; i >= 0; --i) r0[i] = fr.step(Z, r0[i]);
   }
-  auto matvec_add = [&](const double *P, const double (&o)[N], double (&v)[N]) {
+  // the zero-input transition of a cascade is block lower-triangular (a
+  // section's state never feeds an earlier section): PhiP skips those blocks
+  auto matvec_add = [&](const double *P, const double (&o)[N], double (&v)[N], bool tri) {
 #pragma unroll
     for (int r = 0; r < N; ++r) {
       double acc = v[r];
 #pragma unroll
-      for (int c = 0; c < N; ++c) acc = fma(P[r * MAX_N + c], o[c], acc);
+      for (int c = 0; c < N; ++c)
+        if (!tri || c / 2 <= r / 2) acc = fma(P[r * MAX_N + c], o[c], acc);
       v[r] = acc;
     }
   };
-  // ---- 2. forward wave scan
+  // ---- 3. forward wave scan
   double Sin[N], vf[N], Sj[N];
 #pragma unroll
   for (int n = 0; n < N; ++n) {
     Sin[n] = OUT ? SF[(k * N + n) * n_ch + ch] : 0.0;
     vf[n] = A[n];
   }
-  if (OUT && lane == 0) matvec_add(fc->PhiP[0], Sin, vf);
+  if (OUT && lane == 0) matvec_add(fc->PhiP[0], Sin, vf, true);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int d = 1 << i;
     double o[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) o[n] = __shfl_up(vf[n], d);
-    if (lane >= d) matvec_add(fc->PhiP[i], o, vf);
+    if (lane >= d) matvec_add(fc->PhiP[i], o, vf, true);
   }
 #pragma unroll
   for (int n = 0; n < N; ++n) {
     const double u = __shfl_up(vf[n], 1);
     Sj[n] = lane == 0 ? Sin[n] : u;
   }
-  // ---- 3. true forward output
-#pragma unroll
-  for (int i = 0; i < LS; ++i)
-#pragma unroll
-    for (int n = 0; n < N; ++n) yf[i] = fma(fc->H[i][n], Sj[n], yf[i]);
-  // ---- 4. zero-state reverse + backward wave scan
+  // ---- 4. reverse exit with the true forward state, backward wave scan
   double vb[N], Tin[N];
 #pragma unroll
-  for (int n = 0; n < N; ++n) vb[n] = 0.0;
-#pragma unroll
-  for (int i = LS - 1; i >= 0; --i) (void)fr.step(vb, yf[i]);
-#pragma unroll
-  for (int n = 0; n < N; ++n) Tin[n] = OUT ? ST[((k + 1) * N + n) * n_ch + ch] : 0.0;
-  if (OUT && lane == 63) matvec_add(fc->PhiP[0], Tin, vb);
+  for (int n = 0; n < N; ++n) {
+    vb[n] = Z[n];
+    Tin[n] = OUT ? ST[((k + 1) * N + n) * n_ch + ch] : 0.0;
+  }
+  matvec_add(fc->M32, Sj, vb, false);
+  if (OUT && lane == 63) matvec_add(fc->PhiP[0], Tin, vb, true);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int d = 1 << i;
     double o[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) o[n] = __shfl_down(vb[n], d);
-    if (lane + d < 64) matvec_add(fc->PhiP[i], o, vb);
+    if (lane + d < 64) matvec_add(fc->PhiP[i], o, vb, true);
   }
   if constexpr (!OUT) {
     if (lane == 63) {
@@ -949,20 +954,73 @@ __global__ __launch_bounds__(64, 2) void k_fullrate_wave(
     }
     return;
   }
-  // ---- 5. output pass from T_{j+1}
+  // ---- 5. outputs y_j = r0_j + Q w_j, w_j = (S_j, T_{j+1}), Q[i] = (Rh[i],
+  // H[31 - i]): the 32 x 2N by 2N x 64 product runs on the fp64 matrix cores
+  // (v_mfma_f64_16x16x4: A = Q from FRConst::QA, B = w staged through LDS,
+  // C = r0 read back in the accumulator layout)
   double T[N];
 #pragma unroll
   for (int n = 0; n < N; ++n) {
     const double u = __shfl_down(vb[n], 1);
     T[n] = lane == 63 ? Tin[n] : u;
   }
-  double *ob = lds;
+  constexpr int K = 2 * N, KS = K / 4;
+  double *W = lds;  // [64][K]
 #pragma unroll
-  for (int i = LS - 1; i >= 0; --i) ob[lane * OSTR + i] = fr.step(T, yf[i]);
+  for (int n = 0; n < N; ++n) {
+    W[lane * K + n] = Sj[n];
+    W[lane * K + N + n] = T[n];
+  }
   __syncthreads();
+  const int col = lane & 15, q = lane >> 4;
+  double bop[KS][4], aop[2][KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bop[ks][nt] = W[(16 * nt + col) * K + 4 * ks + q];
+    aop[0][ks] = fc->QA[0][ks][lane];
+    aop[1][ks] = fc->QA[1][ks][lane];
+  }
+  __syncthreads();
+  // two passes of 16 samples (one MFMA row tile each) through a 64 x 16 LDS
+  // stage: rows of 128 B leave as 16-B stores
+  double *ob = lds;
   double *yr = y + ch * ys_ch + a * ys_t;
-#pragma unroll 8
-  for (int o = lane; o < L; o += 64) yr[o * ys_t] = ob[(o / LS) * OSTR + (o % LS)];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ob[lane * OSTR + i] = r0[16 * mt + i];
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      double *o = ob + (16 * nt + col) * OSTR + q;
+      fr_d4v acc = {o[0], o[4], o[8], o[12]};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[mt][ks], bop[ks][nt], acc, 0, 0, 0);
+      o[0] = acc[0];
+      o[4] = acc[1];
+      o[8] = acc[2];
+      o[12] = acc[3];
+    }
+    __syncthreads();
+    if (ys_t == 1 && (reinterpret_cast<uintptr_t>(yr) & 15) == 0) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
+        double2 v;
+        v.x = ob[r * OSTR + c2];
+        v.y = ob[r * OSTR + c2 + 1];
+        *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = v;
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 4 + (lane >> 4), c = lane & 15;
+        yr[(r * LS + 16 * mt + c) * ys_t] = ob[r * OSTR + c];
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // k_fullrate_scan: one thread per channel.  SciPy's left edge (odd extension,
@@ -970,18 +1028,24 @@ __global__ __launch_bounds__(64, 2) void k_fullrate_wave(
 // forward (TP) -> reverse from zi * y_f[-1] over pad + tail, writing the
 // tail's outputs -> T at every big block start, backward.
 template <int NS>
-__global__ __launch_bounds__(256) void k_fullrate_scan(
+__global__ __launch_bounds__(64) void k_fullrate_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t nb, int padlen,
     const FRConst *__restrict__ fc, const double *__restrict__ F, double *__restrict__ SF,
     double *__restrict__ ST, double *__restrict__ TP, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = 2 * NS;
+  // PhiL and M (read every step) live in LDS: too many for SGPRs
+  __shared__ double cPL[N * N], cMM[N * N];
+  for (int i = threadIdx.x; i < N * N; i += blockDim.x) {
+    cPL[i] = fc->PhiL[(i / N) * MAX_N + i % N];
+    cMM[i] = fc->M[(i / N) * MAX_N + i % N];
+  }
+  __syncthreads();
   const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= n_ch) return;
   FwdRec<NS> fr;
   fr.load(fc->cf);
   const float *xc = x + ch * s_ch;
   const int E = padlen;
-  const int64_t n_ext = n_t + 2 * (int64_t)E;
   const float x0 = xc[0], xn = xc[(n_t - 1) * s_t];
   auto ext = [&](int64_t t) -> double {  // scipy odd extension, float32 like numpy
     if (t < E) return (double)(2.0f * x0 - xc[(E - t) * s_t]);
@@ -995,58 +1059,123 @@ __global__ __launch_bounds__(256) void k_fullrate_scan(
     for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * e0;
   }
   for (int64_t t = 0; t < E; ++t) (void)fr.step(z, ext(t));
-  auto matvec = [&](const double *P, const double (&v)[N], double (&o)[N]) {
+  // The walks below are latency-bound (one thread per channel): full batches
+  // of Q blocks / B samples load before they are applied, the next batch's
+  // loads in flight; the remainders run one step at a time.
+  constexpr int Q = 4, B = 8;
+  const double *PL = cPL, *MM = cMM;
+  auto mv = [&](const double *P, const double (&v)[N], double (&o)[N], bool tri) {
+    asm volatile("" ::: "memory");  // re-read P from LDS (hoisted, 2 x N*N doubles spill)
 #pragma unroll
     for (int r = 0; r < N; ++r) {
       double acc = o[r];
 #pragma unroll
-      for (int c = 0; c < N; ++c) acc = fma(P[r * MAX_N + c], v[c], acc);
+      for (int c = 0; c < N; ++c)
+        if (!tri || c / 2 <= r / 2) acc = fma(P[r * N + c], v[c], acc);
       o[r] = acc;
     }
   };
-  // forward over the big blocks
-  for (int64_t k = 0; k < nb; ++k) {
-    double nz[N];
+  auto fwd_block = [&](int64_t k, double (&f)[N]) {
 #pragma unroll
-    for (int n = 0; n < N; ++n) {
-      SF[(k * N + n) * n_ch + ch] = z[n];
-      nz[n] = F[(k * 2 * N + n) * n_ch + ch];
-    }
-    matvec(fc->PhiL, z, nz);
+    for (int n = 0; n < N; ++n) SF[(k * N + n) * n_ch + ch] = z[n];
+    mv(PL, z, f, true);
 #pragma unroll
-    for (int n = 0; n < N; ++n) z[n] = nz[n];
+    for (int n = 0; n < N; ++n) z[n] = f[n];
+  };
+  // ---- forward over the big blocks
+  const int64_t nbq = nb / Q * Q;
+  for (int64_t k0 = 0; k0 < nbq; k0 += Q) {
+    double fq[Q][N];
+#pragma unroll
+    for (int u = 0; u < Q; ++u)
+#pragma unroll
+      for (int n = 0; n < N; ++n) fq[u][n] = F[((k0 + u) * 2 * N + n) * n_ch + ch];
+#pragma unroll
+    for (int u = 0; u < Q; ++u) fwd_block(k0 + u, fq[u]);
   }
-  // tail + right pad, forward
-  const int64_t t_tail = E + nb * FR_L;
+  for (int64_t k = nbq; k < nb; ++k) {
+    double f[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) f[n] = F[(k * 2 * N + n) * n_ch + ch];
+    fwd_block(k, f);
+  }
+  // ---- tail samples [nb * FR_L, n_t), forward
+  const int64_t t_tail = nb * FR_L;  // sample index (ext index + E)
+  double *tp = TP + ch;
   double yl = 0.0;
-  for (int64_t t = t_tail; t < n_ext; ++t) {
-    yl = fr.step(z, ext(t));
-    TP[(t - t_tail) * n_ch + ch] = yl;
+  {
+    const int64_t nt = n_t - t_tail, ntb = nt / B * B;
+    const float *xt = xc + t_tail * s_t;
+    for (int64_t i0 = 0; i0 < ntb; i0 += B) {
+      float xv[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) xv[u] = xt[(i0 + u) * s_t];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        yl = fr.step(z, (double)xv[u]);
+        tp[(i0 + u) * n_ch] = yl;
+      }
+    }
+    for (int64_t i = ntb; i < nt; ++i) {
+      yl = fr.step(z, (double)xt[i * s_t]);
+      tp[i * n_ch] = yl;
+    }
+    // right pad (odd extension)
+    for (int64_t i = 0; i < E; ++i) {
+      yl = fr.step(z, (double)(2.0f * xn - xc[(n_t - 2 - i) * s_t]));
+      tp[(nt + i) * n_ch] = yl;
+    }
   }
-  // reverse over pad + tail
+  // ---- reverse over pad + tail
 #pragma unroll
   for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * yl;
-  for (int64_t t = n_ext - 1; t >= t_tail; --t) {
-    const double v = fr.step(z, TP[(t - t_tail) * n_ch + ch]);
-    if (t < E + n_t) y[ch * ys_ch + (t - E) * ys_t] = v;
+  {
+    const int64_t nt = n_t - t_tail, ntp = nt + E;
+    for (int64_t i = ntp - 1; i >= nt; --i) (void)fr.step(z, tp[i * n_ch]);
+    double *yt = y + ch * ys_ch + t_tail * ys_t;
+    const int64_t r = nt % B;  // the tail's last r samples one at a time, then full batches
+    for (int64_t i = nt - 1; i >= nt - r; --i) yt[i * ys_t] = fr.step(z, tp[i * n_ch]);
+    for (int64_t i1 = nt - r - 1; i1 >= 0; i1 -= B) {
+      double tv[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) tv[u] = tp[(i1 - u) * n_ch];
+#pragma unroll
+      for (int u = 0; u < B; ++u) yt[(i1 - u) * ys_t] = fr.step(z, tv[u]);
+    }
   }
-  // reverse over the big blocks
+  // ---- reverse over the big blocks
 #pragma unroll
   for (int n = 0; n < N; ++n) ST[(nb * N + n) * n_ch + ch] = z[n];
-  for (int64_t k = nb - 1; k >= 0; --k) {
-    double sf[N], nz[N];
+  auto bwd_block = [&](int64_t k, double (&f)[N], const double (&sf)[N]) {
+    mv(PL, z, f, true);
+    mv(MM, sf, f, false);
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      sf[n] = SF[(k * N + n) * n_ch + ch];
-      nz[n] = F[(k * 2 * N + N + n) * n_ch + ch];
-    }
-    matvec(fc->PhiL, z, nz);
-    matvec(fc->M, sf, nz);
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-      z[n] = nz[n];
+      z[n] = f[n];
       ST[(k * N + n) * n_ch + ch] = z[n];
     }
+  };
+  const int64_t rb = nb % Q;
+  for (int64_t k = nb - 1; k >= nb - rb; --k) {
+    double f[N], sf[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      f[n] = F[(k * 2 * N + N + n) * n_ch + ch];
+      sf[n] = SF[(k * N + n) * n_ch + ch];
+    }
+    bwd_block(k, f, sf);
+  }
+  for (int64_t k1 = nb - rb - 1; k1 >= 0; k1 -= Q) {
+    double fq[Q][N], sq[Q][N];
+#pragma unroll
+    for (int u = 0; u < Q; ++u)
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        fq[u][n] = F[((k1 - u) * 2 * N + N + n) * n_ch + ch];
+        sq[u][n] = SF[((k1 - u) * N + n) * n_ch + ch];
+      }
+#pragma unroll
+    for (int u = 0; u < Q; ++u) bwd_block(k1 - u, fq[u], sq[u]);
   }
 }
 

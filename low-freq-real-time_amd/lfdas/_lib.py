@@ -128,6 +128,7 @@ def load():
         "lfd_sosfiltfilt_workspace_bytes": ([i64, i64, i32, i32], sz),
         "lfd_sosfiltfilt_f32": ([vp, i64, i64, i64, i64, vp, i32, i32, vp, i64,
                                  i64, vp, vp], i32),
+        "lfd_sosfiltfilt_last_timing": ([P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float)], i32),
         "lfd_interp_linear_f64": ([vp, i64, i64, i64, i64, vp, vp, i64, vp, i64,
                                    i64, vp], i32),
         "lfd_rolling_mean_f32": ([vp, i64, i64, i64, i64, i64, i64, vp, i64, i64,
@@ -164,7 +165,7 @@ EXPORTED = (
     "lfd_lowpass_last_timing", "lfd_lowpass_plan_destroy",
     "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_debug_runs",
     "lfd_sos_filtfilt_resample_f32",
-    "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32",
+    "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32", "lfd_sosfiltfilt_last_timing",
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32",
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",

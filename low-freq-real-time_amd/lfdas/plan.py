@@ -180,22 +180,33 @@ def device_count() -> int:
     return int(n.value)
 
 
-def sosfiltfilt_device(x, sos, padlen: int = -1, stream=None):
+def sosfiltfilt_device(x, sos, padlen: int = -1, stream=None, y=None, ws=None):
     """Full-rate zero-phase filter on device → float64 tensor (n_ch, n_t)
-    (``lfd_sosfiltfilt_f32``; DASCore ``pass_filter`` alone)."""
+    (``lfd_sosfiltfilt_f32``; DASCore ``pass_filter`` alone).  ``y`` / ``ws``:
+    preallocated output and workspace (``lfd_sosfiltfilt_workspace_bytes``)."""
     import torch
     _require_cuda(x, "x", torch.float32)
     lib = load()
     sos = np.ascontiguousarray(sos, dtype=np.float64)
     n_ch, n_t = x.shape
-    wsb = lib.lfd_sosfiltfilt_workspace_bytes(n_ch, n_t, int(padlen), sos.shape[0])
-    ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=x.device)
-    y = torch.empty((n_ch, n_t), dtype=torch.float64, device=x.device)
+    if ws is None:
+        wsb = lib.lfd_sosfiltfilt_workspace_bytes(n_ch, n_t, int(padlen), sos.shape[0])
+        ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=x.device)
+    if y is None:
+        y = torch.empty((n_ch, n_t), dtype=torch.float64, device=x.device)
     _count()
     check(lib.lfd_sosfiltfilt_f32(_ptr(x), n_ch, n_t, x.stride(0), x.stride(1), sos.ctypes.data,
                                   sos.shape[0], int(padlen), _ptr(y), y.stride(0), y.stride(1),
                                   _ptr(ws), _stream_ptr(stream)))
     return y
+
+
+def sosfiltfilt_last_timing_ms():
+    """(functionals, scan, output pass) kernel times of the last blocked
+    ``sosfiltfilt_device`` call made with ``set_timing(True)``."""
+    a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+    check(load().lfd_sosfiltfilt_last_timing(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+    return float(a.value), float(b.value), float(c.value)
 
 
 def interp_device(yfull, lo, w, stream=None):
