@@ -331,6 +331,21 @@ void fullrate_constants(const Cascade &cs, lfd::FRConst &fc) {
     for (int i = lfd::FR_LS - 1; i >= 0; --i) fc.Rh[i][c] = (double)tdf2_step(cs, u, yv[i]);
     for (int r = 0; r < n; ++r) fc.M32[r * MAX_N + c] = (double)u[r];
   }
+  {
+    R kaz[16][lfd::FR_LS] = {{0}};
+    for (int p = 0; p < lfd::FR_LS; ++p) {
+      R z[MAX_N] = {0}, yo[lfd::FR_LS];
+      for (int i = 0; i < lfd::FR_LS; ++i) yo[i] = tdf2_step(cs, z, i == p ? 1.0L : 0.0L);
+      R t[MAX_N] = {0};
+      for (int i = lfd::FR_LS - 1; i >= 0; --i) (void)tdf2_step(cs, t, yo[i]);
+      for (int c = 0; c < n; ++c) {
+        kaz[c][p] = z[c];
+        kaz[n + c][p] = t[c];
+      }
+    }
+    for (int ks = 0; ks < lfd::FR_LS / 4; ++ks)
+      for (int l = 0; l < 64; ++l) fc.KAZ[ks][l] = (double)kaz[l & 15][4 * ks + (l >> 4)];
+  }
   for (int mt = 0; mt < 2; ++mt)
     for (int ks = 0; ks < 4; ++ks)
       for (int l = 0; l < 64; ++l) {

@@ -182,6 +182,10 @@ struct FRConst {
   // v_mfma_f64_16x16x4 per 16-row tile mt and k-step ks:
   // QA[mt][ks][l] = Q[16 mt + (l & 15)][4 ks + (l >> 4)]
   double QA[2][4][64];
+  // functional taps: row c < N the forward exit state A, N <= c < 2N the
+  // zero-state reverse exit Z0 of a sub-block per unit sample p (rows >= 2N
+  // zero), as the A operand per k-step: KAZ[ks][l] = Kaz[l & 15][4 ks + (l >> 4)]
+  double KAZ[FR_LS / 4][64];
 };
 // Layouts (channel fastest, so the scan's per-channel threads coalesce):
 //   F [k][2N][ch] (e_f then e_r), SF / ST [k][N][ch] for k in [0, nb].

@@ -858,11 +858,14 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L;
   static_assert(LS == 32, "tile reads assume 32-sample sub-blocks");
   constexpr int TLDS = L + 4 * (L / 32);
-  constexpr int OSTR = 17;  // output stage row stride (doubles): 16 samples + 1
-  constexpr int NLDS = !OUT ? TLDS / 2 : (64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2);
+  // LDS row strides of 18 doubles (36 dwords = 4 x odd): the MFMA-layout
+  // accesses (16 rows x 4 adjacent doubles per instruction) hit distinct banks
+  constexpr int OSTR = 18;
+  constexpr int NLDS = 64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2;
   __shared__ __attribute__((aligned(16))) double lds[NLDS];
   float *tile = reinterpret_cast<float *>(lds);
   const int lane = threadIdx.x;
+  const int col = lane & 15, q = lane >> 4;
   const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
   const int64_t a = k * L;
   {
@@ -873,9 +876,9 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   __syncthreads();
   FwdRec<NS> fr;
   fr.load(fc->cf);
-  // ---- 1, 2. zero-state forward, then zero-state reverse over its output
-  double r0[LS], A[N], Z[N];
-  {
+  double r0[OUT ? LS : 1], A[N], Z[N];
+  if constexpr (OUT) {
+    // ---- 1, 2. zero-state forward, then zero-state reverse over its output
     float xs[LS];
     const float *tr = tile + 36 * lane;
 #pragma unroll
@@ -892,6 +895,33 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     for (int i = 0; i < LS; ++i) r0[i] = fr.step(A, (double)xs[i]);
 #pragma unroll
     for (int i = LS - 1; i >= 0; --i) r0[i] = fr.step(Z, r0[i]);
+  } else {
+    // ---- 1, 2 (functionals): only the exit states are needed, and they are
+    // linear in the sub-block's samples: (A_j, Z0_j) = KAZ x_j, a 16 x 32 by
+    // 32 x 64 product on the fp64 matrix cores (B = samples from the tile)
+    fr_d4v acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
+    const float *tb = tile + 36 * col + q;
+#pragma unroll
+    for (int ks = 0; ks < LS / 4; ++ks) {
+      const double av = fc->KAZ[ks][lane];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[36 * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
+    }
+    __syncthreads();
+    double *az = lds;  // [sub-block][functional], stride OSTR
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) az[(16 * nt + col) * OSTR + q + 4 * r] = acc[nt][r];
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      A[n] = az[lane * OSTR + n];
+      Z[n] = az[lane * OSTR + N + n];
+    }
   }
   // the zero-input transition of a cascade is block lower-triangular (a
   // section's state never feeds an earlier section): PhiP skips those blocks
@@ -965,19 +995,18 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     T[n] = lane == 63 ? Tin[n] : u;
   }
   constexpr int K = 2 * N, KS = K / 4;
-  double *W = lds;  // [64][K]
+  double *W = lds;  // [64][K], stride OSTR
 #pragma unroll
   for (int n = 0; n < N; ++n) {
-    W[lane * K + n] = Sj[n];
-    W[lane * K + N + n] = T[n];
+    W[lane * OSTR + n] = Sj[n];
+    W[lane * OSTR + N + n] = T[n];
   }
   __syncthreads();
-  const int col = lane & 15, q = lane >> 4;
   double bop[KS][4], aop[2][KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bop[ks][nt] = W[(16 * nt + col) * K + 4 * ks + q];
+    for (int nt = 0; nt < 4; ++nt) bop[ks][nt] = W[(16 * nt + col) * OSTR + 4 * ks + q];
     aop[0][ks] = fc->QA[0][ks][lane];
     aop[1][ks] = fc->QA[1][ks][lane];
   }
@@ -1007,10 +1036,8 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
-        double2 v;
-        v.x = ob[r * OSTR + c2];
-        v.y = ob[r * OSTR + c2 + 1];
-        *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = v;
+        *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) =
+            *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
       }
     } else {
 #pragma unroll
