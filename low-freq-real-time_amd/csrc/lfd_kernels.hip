@@ -539,7 +539,21 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     for (int j = 0; j < J; ++j) h[j] = e0;
     for (int i = 0; i < E && !(g_scan_diag & 1); ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
   }
-  for (int64_t t = G.s0; t < G.head_end && !(g_scan_diag & 1); ++t) R.fwd(S, h, (double)xc[t * s_t]);
+  // head / tail / reverse walks: 8 samples' loads issued together (a per-step
+  // load left every step waiting on memory latency: the off-sample grids'
+  // heads and tails are up to L - 1 samples)
+  constexpr int SB = 8;
+  if (!(g_scan_diag & 1)) {
+    int64_t t = G.s0;
+    for (; t + SB <= G.head_end; t += SB) {
+      float xv[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) xv[u] = xc[(t + u) * s_t];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) R.fwd(S, h, (double)xv[u]);
+    }
+    for (; t < G.head_end; ++t) R.fwd(S, h, (double)xc[t * s_t]);
+  }
 
   // ---- FIR-history correction of block kb: K1 used the raw samples before
   // head_end (0 before the channel start); this chunk saw pad / head values.
@@ -643,9 +657,23 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   double *tp = TP + tid;
   int64_t ntp = 0;
   double ylast = 0.0;
-  for (int64_t t = G.tail_begin; t <= G.s1 && !(g_scan_diag & 4); ++t) {
-    ylast = R.fwd(S, h, (double)xc[t * s_t]);
-    tp[(ntp++) * n_thr] = ylast;
+  if (!(g_scan_diag & 4)) {
+    int64_t t = G.tail_begin;
+    for (; t + SB <= G.s1 + 1; t += SB) {
+      float xv[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) xv[u] = xc[(t + u) * s_t];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        ylast = R.fwd(S, h, (double)xv[u]);
+        tp[(ntp + u) * n_thr] = ylast;
+      }
+      ntp += SB;
+    }
+    for (; t <= G.s1; ++t) {
+      ylast = R.fwd(S, h, (double)xc[t * s_t]);
+      tp[(ntp++) * n_thr] = ylast;
+    }
   }
   const float xr = xc[G.s1 * s_t];
   for (int i = 0; i < E && !(g_scan_diag & 4); ++i) {
@@ -661,8 +689,8 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     for (int j = 0; j < J; ++j) qw[j] = qss;
   }
   double y_next = 0.0;  // zero-phase output one sample after the tail output
-  for (int64_t i = ntp - 1; i >= 0; --i) {
-    const double q = R.rev(T, tp[i * n_thr]);
+  auto rev_step = [&](int64_t i, double v) {
+    const double q = R.rev(T, v);
     if (G.tail_out_j >= 0 && (G.tail_begin + i == G.tail_out_pos || G.tail_begin + i == G.tail_out_pos + 1)) {
       double acc = q;  // c[0] = 1
 #pragma unroll
@@ -676,6 +704,17 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
     for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
     qw[0] = q;
+  };
+  {
+    int64_t i = ntp - 1;
+    for (; i + 1 >= SB; i -= SB) {
+      double tv[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) tv[u] = tp[(i - u) * n_thr];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) rev_step(i - u, tv[u]);
+    }
+    for (; i >= 0; --i) rev_step(i, tp[i * n_thr]);
   }
 
   // ---- backward scan, outputs at block starts
