@@ -741,6 +741,14 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     G.kout0 = G.kout1 = G.kb;
     G.jout0 = 0;
     G.kstep = kstep;
+    // head skip (run mode): the samples of block kb-1 before s0 and its J
+    // samples of FIR history all lie in the left pad
+    {
+      const int64_t nh = G.head_end - G.s0, lo = G.head_end - L, J = 2 * n_sec;
+      const int64_t ncorr = G.s0 - lo + J;
+      G.hskip = (nh >= J && lo >= 0 && ncorr <= padlen && ncorr <= lfd::HSKIP_MAX &&
+                 !(std::getenv("LFD_NO_HSKIP") && std::atoi(std::getenv("LFD_NO_HSKIP")))) ? 1 : 0;
+    }
     bool any_block = false;
     for (int64_t j = ch.g0; j < ch.g1; ++j) {
       const int64_t pos = grid_lo[j];
@@ -762,7 +770,7 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
         G.tail_out_j = j;
       }
     }
-    kmin = std::min(kmin, G.kb);
+    kmin = std::min(kmin, G.hskip ? G.kb - 1 : G.kb);
     kmax = std::max(kmax, G.ke);
     const int64_t nhead = G.head_end - G.s0, ntail = G.s1 + 1 - G.tail_begin;
     p->tp_len = std::max(p->tp_len, nhead + ntail + padlen);
@@ -790,9 +798,9 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     delete p;
     return e;
   }
+  std::vector<long double> Kx;
+  int nc = 0, row = 0;
   if (2 * n + 1 <= 16) {
-    std::vector<long double> Kx;
-    int nc = 0, row = 0;
     if (int e = block_taps(c, L, (R)w0, Kx, nc, row)) {
       delete p;
       return e;
@@ -826,6 +834,7 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     }
     std::vector<int64_t> cuts = {0, p->bg.nb};
     for (const auto &G : p->chunks) {
+      if (G.hskip) cuts.push_back(G.kb - 1);  // block kb-1 alone: E_f = e_f(kb-1)
       cuts.push_back(G.kb);
       if (G.kb + 1 < G.ke) cuts.push_back(G.kb + 1);
       cuts.push_back(G.ke);
@@ -873,6 +882,9 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     }
     p->n_sr = sr;
     run_constants(p->sc, p->rc);
+    for (int i = 0; i < 4; ++i)
+      for (int q = 0; q < lfd::HSKIP_MAX; ++q)
+        p->rc.KfH[i][q] = (nc > i && q < row) ? (double)Kx[(size_t)i * row + q] : 0.0;
     p->run_ok = true;
   }
   // channel-group-major layouts (lfd_internal.h f_index / sf_index): channels

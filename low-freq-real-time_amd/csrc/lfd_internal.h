@@ -89,6 +89,11 @@ struct ChunkGeom {
   int64_t r0, r1;        // run-mode: runs [r0, r1) tile blocks [kb, ke) (run r0 = [kb])
   int64_t sr_off;        // run-mode: offset (in runs) of this chunk in the S_in scratch
   int64_t kstep;         // blocks per output-grid interval (sub-blocks: L = R / kstep)
+  // run mode, head skip: the head [s0, head_end) is block kb-1 (a one-block
+  // run, r0 - 1) minus its first samples; the scan enters block kb from
+  // PhiF S + E_f(kb-1) + the head taps on (pad - raw) samples instead of
+  // walking the head (off-sample grids: head = L - 1 samples)
+  int64_t hskip;
 };
 
 struct BlockGeom {
@@ -147,7 +152,11 @@ struct RunConst {
   double B[RUN_R][4];               // H0 PhiR^d
   // K1 epilogue: PhiF, M, PhiR (row-major 4x4), G0, H0
   double PhiF[16], M[16], PhiR[16], G0[4], H0[4];
+  // scan head skip: e_f taps of a block row's first HSKIP_MAX samples
+  // (Kx[c][p], c < 4: lfd_capi.cpp block_taps)
+  double KfH[4][32];
 };
+constexpr int HSKIP_MAX = 32;
 struct RunGeom {
   int64_t n_runs, n_groups, n_sr;
   const int64_t *run_ks;    // first block of run r

@@ -532,18 +532,62 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // ---- left edge: odd extension (float32 like numpy), steady state of ext[0]
   double S[N], h[J];
   const float xl = xc[G.s0 * s_t];
+  // head skip (run mode, ChunkGeom::hskip): the head is block kb-1 without
+  // its samples [lo, s0), so the state entering block kb is
+  //   PhiF S(lo) + E_f(kb-1) + sum_p KfH[.][p] (pad - raw)(lo - J + p)
+  // with S(lo) the state after the pad's samples before lo: K1 already summed
+  // the head.  A null in [lo, s0) (outside this chunk) poisons e_f(kb-1), so
+  // such a (chunk, channel) walks its head instead.
+  const int64_t lo_h = G.head_end - g.L;
+  bool hs = false;
+  if constexpr (RUNS) {
+    if (G.hskip && E > 0 && !(g_scan_diag & 1)) {
+      hs = true;
+      for (int64_t t = lo_h; t < G.s0; ++t) hs = hs && __builtin_isfinite(xc[t * s_t]);
+    }
+  }
   {
+    const int n_pad = hs ? E - (int)(G.s0 - lo_h) : E;
     const double e0 = E > 0 ? (double)(2.0f * xl - xc[(G.s0 + E) * s_t]) : (double)xl;
     R.steady(S, e0, true);
 #pragma unroll
     for (int j = 0; j < J; ++j) h[j] = e0;
-    for (int i = 0; i < E && !(g_scan_diag & 1); ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
+    for (int i = 0; i < n_pad && !(g_scan_diag & 1); ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
+  }
+  if constexpr (RUNS) {
+    if (hs) {
+      static_assert(N == RUN_N, "run mode is 4th order");
+      const RunConst &rc = rcs[0];
+      const double *agh = F + ((((ch >> 4) * rg.n_runs) + (G.r0 - 1)) * 8) * 16 + (ch & 15);
+      double ns[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double acc = agh[i * 16];
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = fma(rc.PhiFp[1][i * 4 + j], S[j], acc);
+        ns[i] = acc;
+      }
+      const int ncorr = (int)(G.s0 - lo_h) + J;
+      for (int pq = 0; pq < ncorr; ++pq) {
+        const int64_t pos = lo_h - J + pq;
+        const double u = (double)(2.0f * xl - xc[(2 * G.s0 - pos) * s_t]);
+        const float xv = pos < 0 ? 0.0f : xc[pos * s_t];
+        const double raw = pos < lo_h ? (double)finite_or_zero(xv) : (double)xv;
+        const double d = u - raw;
+#pragma unroll
+        for (int i = 0; i < N; ++i) ns[i] = fma(rc.KfH[i][pq], d, ns[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) S[i] = ns[i];
+#pragma unroll
+      for (int j = 0; j < J; ++j) h[j] = (double)xc[(G.head_end - 1 - j) * s_t];
+    }
   }
   // head / tail / reverse walks: 8 samples' loads issued together (a per-step
   // load left every step waiting on memory latency: the off-sample grids'
   // heads and tails are up to L - 1 samples)
   constexpr int SB = 8;
-  if (!(g_scan_diag & 1)) {
+  if (!(g_scan_diag & 1) && !hs) {
     int64_t t = G.s0;
     for (; t + SB <= G.head_end; t += SB) {
       float xv[SB];
@@ -1497,7 +1541,7 @@ __device__ __forceinline__ float null_mean(int64_t code, float mean) {
 // order; bit 1 = S == 1 outputs leave through LDS the same way (coalesced
 // float4 stores); else lanes load / store their 8 positions directly.
 constexpr int RS_ROW = RS_E + 4;    // padded LDS row (floats): conflict-free ds_read_b128
-template <bool VEC, int STAGE>
+template <bool VEC, int STAGE, int NPF = 1>
 __global__ __launch_bounds__(256, 3) void k_rolling_scan_tc(
     const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
     float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out) {
@@ -1527,7 +1571,7 @@ __global__ __launch_bounds__(256, 3) void k_rolling_scan_tc(
     // Wsum(p0 - 1): window [p0 - W, p0 - 1] (x[-1] = 0 when p0 = W - 1)
     double carry = 0.0;
     int64_t ccnt = 0;  // packed null counts of the window (null_code)
-    {
+    auto halo = [&]() {
       double acc = 0.0;
       int64_t cnt = 0;
       for (int m = p0 - W + lane; m < p0; m += 64) {
@@ -1540,7 +1584,7 @@ __global__ __launch_bounds__(256, 3) void k_rolling_scan_tc(
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
       ccnt = cnt;
-    }
+    };
     const int tb0 = VEC ? (p0 & ~3) : p0;
     struct Tile {
       float xi[RS_E], xo[RS_E];
@@ -1708,18 +1752,26 @@ __global__ __launch_bounds__(256, 3) void k_rolling_scan_tc(
       }
       carry += tot;
     };
-    Tile A, B;
+    // ring of NPF + 1 tiles: NPF steps of loads in flight behind the step
+    // being processed (indices static: the ring is unrolled)
+    Tile R[NPF + 1];
     int tb = tb0;
-    load(tb, A);
-    while (true) {
-      if (tb + RS_P <= p1) load(tb + RS_P, B);
-      process(tb, A);
-      tb += RS_P;
-      if (tb > p1) break;
-      if (tb + RS_P <= p1) load(tb + RS_P, A);
-      process(tb, B);
-      tb += RS_P;
-      if (tb > p1) break;
+#pragma unroll
+    for (int d = 0; d < NPF; ++d)
+      if (tb + d * RS_P <= p1) load(tb + d * RS_P, R[d]);
+    halo();  // the first window's sum (its loads queue behind the ring's)
+    bool fin = false;
+    while (!fin) {
+#pragma unroll
+      for (int u = 0; u <= NPF; ++u) {
+        if (tb + NPF * RS_P <= p1) load(tb + NPF * RS_P, R[(u + NPF) % (NPF + 1)]);
+        process(tb, R[u]);
+        tb += RS_P;
+        if (tb > p1) {
+          fin = true;
+          break;
+        }
+      }
     }
   }
 }
@@ -2194,7 +2246,10 @@ struct TmIter {
 // Interior loads: the row pointer is wave-uniform (SGPR base) and the lane's
 // part a 32-bit element offset, so a load needs no per-lane 64-bit address
 // arithmetic (global_load ... saddr).
-template <bool SWAP, int NTILE = 2>
+// X2: lane (q, col) reads channels 2 col, 2 col + 1 of row +4q with one
+// 8-B load (tile 0 = even channels, tile 1 = odd): every load instruction
+// reads 4 whole 128-B lines, half as many instructions as two dword loads
+template <bool SWAP, int NTILE = 2, bool X2 = false>
 __device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c0, int64_t s_t, int64_t row0,
                                           uint32_t offp, uint32_t offq, TmIter &b) {
 #pragma unroll
@@ -2204,8 +2259,14 @@ __device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c
       const int64_t ro = uniform64(c0 + (row0 + 16 * j + e) * s_t);  // element offset of the row
       const char *rp = reinterpret_cast<const char *>(x + ro);
       const char *rq = SWAP ? reinterpret_cast<const char *>(x + ro + 8 * s_t) : rp;
-      b.p[j][e] = *reinterpret_cast<const float *>(rp + offp);
-      if (NTILE == 2) b.q[j][e] = *reinterpret_cast<const float *>(rq + offq);
+      if (X2) {
+        const float2 v = *reinterpret_cast<const float2 *>(rp + offp);
+        b.p[j][e] = v.x;
+        b.q[j][e] = v.y;
+      } else {
+        b.p[j][e] = *reinterpret_cast<const float *>(rp + offp);
+        if (NTILE == 2) b.q[j][e] = *reinterpret_cast<const float *>(rq + offq);
+      }
     }
 }
 
@@ -2270,7 +2331,7 @@ __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmI
   }
 }
 
-template <int TM_PF, int NT, bool SWAP, int NTILE = 2>
+template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false>
 __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
@@ -2305,14 +2366,16 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
   const bool tile1 = NTILE == 2 && c32 * 32 + 16 < g.n_ch;  // tile 1 holds a real channel (else its stores would
                                                // leave the 16-channel padding of Y0 / AG)
   // this lane's load channel and row offset
-  const int lc = SWAP ? (lane & 31) : col;
-  const int64_t lch = min(c32 * CW + lc, g.n_ch - 1);
+  // (X2: channel pairs 2 col, 2 col + 1; n_ch is even, a pair past n_ch
+  // reads the last pair)
+  const int lc = SWAP ? (lane & 31) : (X2 ? 2 * col : col);
+  const int64_t lch = X2 ? min(c32 * CW + lc, g.n_ch - 2) : min(c32 * CW + lc, g.n_ch - 1);
   const float *xc = x + lch;
   const int rsel = SWAP ? 4 * (lane >> 5) : 4 * q;
   // (channels past n_ch, in a ragged last group, read channel n_ch - 1)
   // Q loads: the same lane channel (SWAP) or tile 1's (16 + col), clamped
   // like P so no load leaves the array
-  const int64_t lchq = SWAP ? lch : min(c32 * CW + 16 + col, g.n_ch - 1);
+  const int64_t lchq = SWAP ? lch : (X2 ? lch + 1 : min(c32 * CW + 16 + col, g.n_ch - 1));
   const float *xq = x + lchq;
   const int64_t c0 = uniform64(c32 * CW);  // interior loads: uniform row base + lane offset
   const uint32_t offp = (uint32_t)(4 * (lch - c32 * CW + rsel * s_t)),  // bytes
@@ -2352,16 +2415,20 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (t == 1 && !tile1) break;
+      if (!X2 && t == 1 && !tile1) break;
       const double *wb = wbase + t * RUN_WB;
-      const int64_t cg = NTILE * c32 + t;
+      // tile t, lane col: channel 16 (2 c32 + t) + col, or (X2) 32 c32 + 2 col + t
+      const int64_t chn = X2 ? c32 * 32 + 2 * col + t : (NTILE * c32 + t) * 16 + col;
+      const int64_t cg = chn >> 4;
+      const int cc = (int)(chn & 15);
+      const bool st_ok = !X2 || cg * 16 < g.n_ch;  // (X2) inside the 16-channel padding
       double T[4] = {0.0, 0.0, 0.0, 0.0};
-      double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
+      double *y0o = Y0 + (cg * g.nb + rks) * 16 + cc;
       for (int pp = rlen - 1; pp >= 0; --pp) {
         double y0 = wb[(pp * 5) * 16 + col];
 #pragma unroll
         for (int j = 0; j < 4; ++j) y0 = fma(H0[j], T[j], y0);
-        if ((pp & 3) == q) y0o[pp * 16] = y0;
+        if ((pp & 3) == q && st_ok) y0o[pp * 16] = y0;
         double nt[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -2373,9 +2440,11 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
 #pragma unroll
         for (int i = 0; i < 4; ++i) T[i] = nt[i];
       }
-      double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + col;
-      ag[q * 16] = S0[t];
-      ag[(4 + q) * 16] = q == 0 ? T[0] : (q == 1 ? T[1] : (q == 2 ? T[2] : T[3]));
+      if (st_ok) {
+        double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + cc;
+        ag[q * 16] = S0[t];
+        ag[(4 + q) * 16] = q == 0 ? T[0] : (q == 1 ? T[1] : (q == 2 ? T[2] : T[3]));
+      }
     }
     __builtin_amdgcn_wave_barrier();
     S0[0] = S0[1] = 0.0;
@@ -2429,7 +2498,7 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     TmIter buf[TM_PF + 1];
 #pragma unroll
     for (int d = 0; d < TM_PF; ++d) {
-      tm_load_u<SWAP, NTILE>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[d]);
+      tm_load_u<SWAP, NTILE, X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[d]);
       produce();
     }
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
@@ -2439,7 +2508,7 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
       for (int u = 0; u <= TM_PF; ++u) {
         constexpr int NB = TM_PF + 1;
         const int lb = (u + TM_PF) % NB;
-        tm_load_u<SWAP, NTILE>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[lb]);
+        tm_load_u<SWAP, NTILE, X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[lb]);
         produce();
         // a run's first and last iteration need the finite mask (chunk
         // boundaries are run boundaries)
@@ -2517,6 +2586,16 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   };
   bool swap = false;
   if (const char *v = std::getenv("LFD_TM_SWAP")) swap = std::atoi(v) != 0;
+  // channel-pair loads: need 8-B aligned pairs (even n_ch and row stride)
+  const bool x2_ok = g.n_ch % 2 == 0 && s_t % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
+  bool x2 = x2_ok;
+  if (const char *v = std::getenv("LFD_TM_X2")) x2 = x2_ok && std::atoi(v) != 0;
+  if (x2 && !swap && ntile == 2) {
+    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, 512);
+    if (nt == 512 && pf == 3) return go(&k_block_runs_mfma_tm<3, 512, false, 2, true>, 512);
+    if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true>, 512);
+    return hipErrorInvalidValue;
+  }
   if (ntile == 1) {  // one 16-channel tile per wave: half-line loads, 16 waves/CU
     if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 1>, 512);
     return hipErrorInvalidValue;
@@ -2911,6 +2990,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // overlapping windows: running sum over segments of >= max(32768, 4W)
     // positions (halo W per segment), fewer when that leaves the chip idle
     int64_t seg_pos = std::max<int64_t>(32768, 4 * W);
+    if (const char *v = std::getenv("LFD_ROLL_SEG")) seg_pos = std::max<int64_t>(4 * W, std::atoll(v));
     while (seg_pos > std::max<int64_t>(4096, 4 * W) && n_ch * ((n_t + seg_pos - 1) / seg_pos) < 16384)
       seg_pos /= 2;
     const int64_t seg_out = std::max<int64_t>(1, seg_pos / S);
@@ -2924,19 +3004,25 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // vs 5.93 (0), 5.99 (1), 5.54 (3)
     int stage = 2;
     if (const char *v = std::getenv("LFD_ROLL_STAGE")) stage = std::atoi(v) & 3;
-#define LFD_ROLL(V, ST)                                                                                    \
-  k_rolling_scan_tc<V, ST><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, \
+    int npf = 1;
+    if (const char *v = std::getenv("LFD_ROLL_PF")) npf = std::atoi(v);
+#define LFD_ROLL(V, ST, PF_)                                                                                    \
+  k_rolling_scan_tc<V, ST, PF_><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, \
                                                              ys_t, (int)seg_out, V && vec_out)
     if (!vec)
-      LFD_ROLL(false, 0);
+      LFD_ROLL(false, 0, 1);
+    else if (stage == 2 && npf == 2)
+      LFD_ROLL(true, 2, 2);
+    else if (stage == 2 && npf == 3)
+      LFD_ROLL(true, 2, 3);
     else if (stage == 0)
-      LFD_ROLL(true, 0);
+      LFD_ROLL(true, 0, 1);
     else if (stage == 1)
-      LFD_ROLL(true, 1);
+      LFD_ROLL(true, 1, 1);
     else if (stage == 2)
-      LFD_ROLL(true, 2);
+      LFD_ROLL(true, 2, 1);
     else
-      LFD_ROLL(true, 3);
+      LFD_ROLL(true, 3, 1);
 #undef LFD_ROLL
   } else {
     const int64_t seg_out = S >= W ? 64 : std::max<int64_t>(1, std::max<int64_t>(4096, 4 * W) / S);

@@ -38,12 +38,13 @@ SCAN_CONST_DTYPE = np.dtype([("r", _RCOEF), ("PhiF", "f8", (MAX_N, MAX_N)),
                              ("Kc", "f8", (2 * MAX_N + 1, MAX_J)), ("ow", "f8")], align=True)
 CHUNK_GEOM_DTYPE = np.dtype([(n, "i8") for n in (
     "s0", "s1", "kb", "ke", "head_end", "tail_begin", "kout0", "kout1", "jout0",
-    "sf_off", "tail_out_pos", "tail_out_j", "r0", "r1", "sr_off", "kstep")])
+    "sf_off", "tail_out_pos", "tail_out_j", "r0", "r1", "sr_off", "kstep", "hskip")])
 RUN_R = 8  # lfd::RUN_R
 RUN_CONST_DTYPE = np.dtype([("PhiFp", "f8", (RUN_R + 1, 16)), ("PhiRp", "f8", (RUN_R + 1, 16)),
                             ("C", "f8", (RUN_R + 1, 16)), ("A", "f8", (RUN_R + 1, RUN_R, 4)),
                             ("B", "f8", (RUN_R, 4)), ("PhiF", "f8", 16), ("M", "f8", 16),
-                            ("PhiR", "f8", 16), ("G0", "f8", 4), ("H0", "f8", 4)])
+                            ("PhiR", "f8", 16), ("G0", "f8", 4), ("H0", "f8", 4),
+                            ("KfH", "f8", (4, 32))])
 
 
 class LFDLibraryError(RuntimeError):

@@ -138,11 +138,29 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
         e0 = (2 * xl - x[:, s0 + E]).astype(np.float32).astype(np.float64)
         Sf, _ = steady(e0, True)
         h = np.stack([e0] * J, 0)
-        for i in range(E):
-            fwd(Sf, h, (2 * xl - x[:, s0 + E - i]).astype(np.float32).astype(np.float64))
-        for t in range(s0, int(Gc["head_end"])):
-            fwd(Sf, h, x[:, t].astype(np.float64))
         he = int(Gc["head_end"])
+        hs = k1 == "runs" and int(Gc["hskip"]) != 0 and E > 0
+        lo_h = he - L
+        n_pad = E - (s0 - lo_h) if hs else E
+        for i in range(n_pad):
+            fwd(Sf, h, (2 * xl - x[:, s0 + E - i]).astype(np.float32).astype(np.float64))
+        if hs:
+            # head skip: K1's one-block run kb-1 summed the head; correct the
+            # row samples before s0 (pad instead of raw) with the e_f taps
+            rh = int(Gc["r0"]) - 1
+            assert run_ks[rh] == kb - 1 and run_len[rh] == 1
+            Sf = rc["PhiFp"][1].reshape(4, 4) @ Sf + AG[rh, :4]
+            for pq in range(s0 - lo_h + J):
+                pos = lo_h - J + pq
+                u = (2 * xl - x[:, 2 * s0 - pos]).astype(np.float32).astype(np.float64)
+                rv = x[:, pos].astype(np.float64) if pos >= 0 else np.zeros(n_ch)
+                if pos < lo_h:
+                    rv = np.where(np.isfinite(rv), rv, 0.0)
+                Sf = Sf + np.outer(rc["KfH"][:, pq], u - rv)
+            h = np.stack([x[:, he - 1 - j] for j in range(J)], 0).astype(np.float64)
+        else:
+            for t in range(s0, he):
+                fwd(Sf, h, x[:, t].astype(np.float64))
         raw = np.stack([x[:, he - 1 - j] if he - 1 - j >= 0 else np.zeros(n_ch) for j in range(J)], 0)
         dh = h - raw.astype(np.float64)
         dw = np.stack([sum(c64[jj] * dh[jj - m - 1] for jj in range(m + 1, J + 1)) for m in range(J)], 0)

@@ -405,6 +405,7 @@ def test_nonfinite_samples_poison_their_chunk_only(where, layout):
     (250.0, 0.2, 40, 6, 37, 6000, 37),      # L = 50
     (500.0, 1.0, 600, 7, 33, 750_001, 40),  # L = 500, channel subset of a wider (time, ch) array
     (1000.0, 0.5, 40, 4, 18, 100_003, 18),  # odd n_t
+    (250.0, 0.2, 40, 6, 70, 6000, 72),      # even channels (channel-pair loads), ragged last wave
 ])
 def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
     """(time, channel) storage viewed as (channel, time) (s_ch = 1, s_t =
@@ -420,7 +421,9 @@ def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
     assert xd.stride() == (1, width)
     ws = plan.alloc_workspace()
     out = {}
-    for mode in ("default", "recfold", "blocks"):
+    for mode in ("default", "nox2", "recfold", "blocks"):
+        if mode == "nox2":  # one dword load per channel instead of channel pairs
+            monkeypatch.setenv("LFD_TM_X2", "0")
         if mode == "recfold":
             monkeypatch.setenv("LFD_K1_REC", "1")
         if mode == "blocks":
@@ -430,6 +433,9 @@ def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
     assert out["default"][1] == "mfma_runs_tm"
+    assert out["nox2"][1] == "mfma_runs_tm"
+    # both load shapes feed the same MFMA sequence per channel: bit-identical
+    assert np.array_equal(out["default"][0], out["nox2"][0], equal_nan=True)
     assert out["recfold"][1] == "recurrence_fold"
     assert out["blocks"][1] == "recurrence"
     b = out["blocks"][0]

@@ -8,12 +8,17 @@ import bench  # noqa: E402
 import torch  # noqa: E402
 
 dev = torch.device("cuda", 0)
-for nt, pf, sw, ntl in [("512", "2", "0", "2"), ("512", "2", "0", "1"), ("512", "2", "0", "2"), ("512", "2", "0", "1")]:
-    os.environ["LFD_TM_NT"], os.environ["LFD_TM_PF"], os.environ["LFD_TM_SWAP"] = nt, pf, sw
-    os.environ["LFD_TM_NTILE"] = ntl
-    r = bench.bench_lowpass_line(dev, 10_000, 500.0, 3600.0, 1.0, 600, 7, time_major=True, label="tm")
-    print("TM", nt, pf, sw, ntl, r["k1"], round(r["roofline"]["kernel_ms"], 3), round(r["roofline"]["frac"], 3),
-          round(r["ms_per_step"], 3), flush=True)
+specs = sys.argv[1:] or ["LFD_TM_X2=1", "LFD_TM_X2=0", "LFD_TM_X2=1 LFD_TM_PF=3", "LFD_TM_X2=1 LFD_TM_PF=1"]
+for rep in range(2):
+    for spec in specs:
+        for k in ("LFD_TM_NT", "LFD_TM_PF", "LFD_TM_SWAP", "LFD_TM_NTILE", "LFD_TM_X2"):
+            os.environ.pop(k, None)
+        for kv in spec.split():
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
+        r = bench.bench_lowpass_line(dev, 10_000, 500.0, 3600.0, 1.0, 600, 7, time_major=True, label="tm")
+        print("TM", spec, r["k1"], round(r["roofline"]["kernel_ms"], 3), round(r["roofline"]["frac"], 3),
+              round(r["ms_per_step"], 3), flush=True)
 for st in ():
     os.environ["LFD_ROLL_STAGE"] = st
     for W, S_ in [(1000, 1), (1000, 250)]:
