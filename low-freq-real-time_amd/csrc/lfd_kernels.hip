@@ -1541,8 +1541,8 @@ __device__ __forceinline__ float null_mean(int64_t code, float mean) {
 // order; bit 1 = S == 1 outputs leave through LDS the same way (coalesced
 // float4 stores); else lanes load / store their 8 positions directly.
 constexpr int RS_ROW = RS_E + 4;    // padded LDS row (floats): conflict-free ds_read_b128
-template <bool VEC, int STAGE, int NPF = 1>
-__global__ __launch_bounds__(256, 3) void k_rolling_scan_tc(
+template <bool VEC, int STAGE, int NPF = 1, int MINW = 3>
+__global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
     float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out) {
   // positions are row-relative int32 (the launcher checks n_t < 2^31 - 1024)
@@ -1844,6 +1844,39 @@ __device__ __forceinline__ void mf_iter(const double *kt, int kstride, bool colv
   }
 }
 
+// The same 16 MFMA steps on v_mfma_f64_4x4x4_4b: 4 blocks of 4x4x4, block b
+// = lanes with (l >> 2) & 3 == b.  Its operands share the 16x16x4 layout's
+// lane mapping (measured, tools/check_mfma4x4.hip): A[i][k] at lane 16k + 4b
+// + i, B[k][j] at lane 16k + 4b + j, D[i][j] at lane 16i + 4b + j.  So with
+// B = this lane's sample (k = q, channel 4b + j = col) unchanged, MFMA m
+// with A = taps of functional 4m + (l & 3) leaves functional 4m + q of
+// channel col on the lane — acc0/acc1's row q + 4m.  Three of them cover the
+// 9 functionals (12 rows; 16x16x4 computes 16): 3 x 18.5 vs 86.6 cycles per
+// step at 4 waves / SIMD (tools/ubench_mfma64b.hip).  kt[m]: the lane's tap
+// column for functional 4m + (l & 3) (clamped to nc - 1).
+__device__ __forceinline__ void mf_iter4(const double *const (&kt)[3], int kstride, const f4v (&cur)[4],
+                                         double (&acc)[2][3]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double a[3][4];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const double2 b01 = *reinterpret_cast<const double2 *>(kt[m] + j * kstride);
+      const double2 b23 = *reinterpret_cast<const double2 *>(kt[m] + j * kstride + 2);
+      a[m][0] = b01.x;
+      a[m][1] = b01.y;
+      a[m][2] = b23.x;
+      a[m][3] = b23.y;
+    }
+    const float xv[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+        acc[e & 1][m] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[m][e], (double)xv[e], acc[e & 1][m], 0, 0, 0);
+  }
+}
+
 // lane holds D[c = q + 4r][ch]: 16 consecutive channels per (block, c)
 __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, double *F, int64_t k,
                                          int nc, int q, int64_t ch, const BlockGeom &g) {
@@ -2012,8 +2045,11 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 // MODE 0: production.  Diagnostics (timing only, results invalid;
 // LFD_RUN_MODE): 1 = VALU sum instead of the MFMAs, 4 = MFMAs but the run
 // epilogue reduced to one store per block.
-template <int PF, int MODE = 0, int NT = 1024>
-__global__ __launch_bounds__(NT) void k_block_runs_mfma(
+// MINW: minimum waves per SIMD the register allocation must allow (0: the
+// compiler's choice; 144 VGPRs at PF 2 / 512 threads = 3 waves per SIMD,
+// fewer than the 4 that two workgroups' LDS allow)
+template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0>
+__global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
     double *__restrict__ AG) {
@@ -2067,18 +2103,23 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
   const float *xr = x + (ch < g.n_ch ? ch : g.n_ch - 1) * s_ch;
   const bool colv = col < tg.nc;
   const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
+  // (M4) tap columns of functionals 4m + (lane & 3)
+  const double *kl4[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) kl4[m] = Ks + (q * tg.nc + min(4 * m + (lane & 3), tg.nc - 1)) * 4;
   const int nit = tg.Lp / 64;
   const int kstride = 16 * tg.nc;
   const int64_t s0 = g.base - tg.J;
   const int L = g.L;
   auto table = [&](int64_t s) { return tg.nvar == 1 ? kl : kl + (int)(s & 3) * tab; };
+  auto tshift = [&](int64_t s) { return tg.nvar == 1 ? 0 : (int)(s & 3) * tab; };
   const double *PhiF = cst, *Mm = cst + 16, *PhiR = cst + 32, *G0 = cst + 48, *H0 = cst + 52;
 
   int64_t rks = k0;
   int rlen = run_len_of(r);
   double S0 = 0.0;  // run prefix state, component q of channel col
-  auto block_done = [&](const d4v &acc0, const d4v &acc1, int64_t k) {
-    const d4v a = acc0 + acc1;  // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
+  auto block_done = [&](const d4v &a, int64_t k) {
+    // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
     const int p = (int)(k - rks);
     double sv[4];
 #pragma unroll
@@ -2130,16 +2171,27 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
     const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
+    const int vsh = tg.nvar == 1 ? 0 : v * tab;
     const int64_t a = s - v + 4 * q;
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    double acc4[2][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     for (int it = 0; it < nit; ++it) {
       f4v cur[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
       if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
-      mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+      if (M4) {
+        const double *const kt4[3] = {kl4[0] + vsh + (4 * it) * kstride, kl4[1] + vsh + (4 * it) * kstride,
+                                      kl4[2] + vsh + (4 * it) * kstride};
+        mf_iter4(kt4, kstride, cur, acc4);
+      } else {
+        mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+      }
     }
-    block_done(acc0, acc1, k);
+    if (M4)
+      block_done(d4v{acc4[0][0] + acc4[1][0], acc4[0][1] + acc4[1][1], acc4[0][2] + acc4[1][2], 0.0}, k);
+    else
+      block_done(acc0 + acc1, k);
   };
 
   int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
@@ -2172,7 +2224,9 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
       produce();
     }
     const double *kt = table(s);
+    int ksh = tshift(s);
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    double acc4[2][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     bool fin = false;
     while (!fin) {
 #pragma unroll
@@ -2194,17 +2248,26 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
             const int v = (int)(s & 3);
             mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
           }
-          mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+          if (M4) {
+            const double *const kt4[3] = {kl4[0] + ksh + (4 * it) * kstride, kl4[1] + ksh + (4 * it) * kstride,
+                                          kl4[2] + ksh + (4 * it) * kstride};
+            mf_iter4(kt4, kstride, buf[u], acc4);
+          } else {
+            mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+          }
         }
         if (++it == nit) {
+          const d4v a = M4 ? d4v{acc4[0][0] + acc4[1][0], acc4[0][1] + acc4[1][1], acc4[0][2] + acc4[1][2], 0.0}
+                           : acc0 + acc1;
           if (MODE == 4) {
-            const d4v a = acc0 + acc1;
             Y0[(cg * g.nb + k) * 16 + col] = a[q & 3];
           } else {
-            block_done(acc0, acc1, k);
+            block_done(a, k);
           }
           acc0 = d4v{0.0, 0.0, 0.0, 0.0};
           acc1 = d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int m = 0; m < 3; ++m) acc4[0][m] = acc4[1][m] = 0.0;
           it = 0;
           ++k;
           s += L;
@@ -2213,6 +2276,7 @@ __global__ __launch_bounds__(NT) void k_block_runs_mfma(
             break;
           }
           kt = table(s);
+          ksh = tshift(s);
         }
       }
     }
@@ -2682,7 +2746,7 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   return hipGetLastError();
 }
 
-template <int PF, int MODE, int NT>
+template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
@@ -2692,12 +2756,13 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, M4, MINW>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_block_runs_mfma<PF, MODE, NT><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
+  k_block_runs_mfma<PF, MODE, NT, M4, MINW><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0,
+                                                                             AG);
   return hipGetLastError();
 }
 
@@ -2710,7 +2775,12 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   // independently, unlike one 1024-thread group per CU: 12.3-12.7 ms vs
   // 12.65-13.0 on cfg3 (A/B, tools/ab_env.sh). Prefetch depth 2: 0.6 % faster
   // than depth 1 in 15 of 15 in-process pairs on two boxes (tools/probe_k1cfg.py)
-  int mode = 0, pf = 2, nt = 512;
+  // Registers for 4 waves per SIMD (MINW 4: 16 waves per CU, as many as two
+  // workgroups' LDS allow) at prefetch depth 1: 12.77 ms vs 13.09-13.12 for
+  // depth 2 at the compiler's 144 VGPRs (3 waves per SIMD), in-process A/B on
+  // one allocation, 2 processes x 20 launches (tools/ab_plan.py); depth 2
+  // under the cap spills 18 VGPRs and is slower (13.25)
+  int mode = 0, pf = 1, nt = 512;
   {
     static int band_set = 0;
     const char *v = std::getenv("LFD_K1_BAND");
@@ -2727,6 +2797,24 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   if (const char *v = std::getenv("LFD_RUN_MODE")) mode = std::atoi(v);
   if (const char *v = std::getenv("LFD_RUN_PF")) pf = std::atoi(v);
   if (const char *v = std::getenv("LFD_RUN_NT")) nt = std::atoi(v);
+  // three v_mfma_f64_4x4x4_4b per step instead of one 16x16x4 (mf_iter4)
+  bool m4 = false;
+  if (const char *v = std::getenv("LFD_RUN_M4")) m4 = std::atoi(v) != 0;
+  int minw = 4;  // LFD_RUN_MINW=0: the compiler's register allocation
+  if (const char *v = std::getenv("LFD_RUN_MINW")) minw = std::atoi(v);
+  if (minw == 4 && mode == 0 && nt == 512) {
+    if (m4 && pf == 2) return run_k1<2, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (m4 && pf == 1) return run_k1<1, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (!m4 && pf == 2) return run_k1<2, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (!m4 && pf == 1) return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    return hipErrorInvalidValue;
+  }
+  if (m4 && mode == 0) {
+    if (pf == 2 && nt == 512) return run_k1<2, 0, 512, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (pf == 1 && nt == 512) return run_k1<1, 0, 512, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (pf == 3 && nt == 512) return run_k1<3, 0, 512, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    return hipErrorInvalidValue;
+  }
   if (mode == 1) return run_k1<1, 1, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (mode == 4 && nt == 320) return run_k1<1, 4, 320>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
   if (mode == 4 && nt == 512) return run_k1<1, 4, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
@@ -3004,13 +3092,20 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // vs 5.93 (0), 5.99 (1), 5.54 (3)
     int stage = 2;
     if (const char *v = std::getenv("LFD_ROLL_STAGE")) stage = std::atoi(v) & 3;
-    int npf = 1;
+    int npf = 1, minw = 3;
     if (const char *v = std::getenv("LFD_ROLL_PF")) npf = std::atoi(v);
+    if (const char *v = std::getenv("LFD_ROLL_MINW")) minw = std::atoi(v);
 #define LFD_ROLL(V, ST, PF_)                                                                                    \
   k_rolling_scan_tc<V, ST, PF_><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, \
                                                              ys_t, (int)seg_out, V && vec_out)
     if (!vec)
       LFD_ROLL(false, 0, 1);
+    else if (stage == 2 && npf == 1 && minw == 4)
+      k_rolling_scan_tc<true, 2, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
+                                                                      ys_ch, ys_t, (int)seg_out, vec_out);
+    else if (stage == 2 && npf == 2 && minw == 4)
+      k_rolling_scan_tc<true, 2, 2, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
+                                                                      ys_ch, ys_t, (int)seg_out, vec_out);
     else if (stage == 2 && npf == 2)
       LFD_ROLL(true, 2, 2);
     else if (stage == 2 && npf == 3)

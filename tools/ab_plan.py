@@ -69,7 +69,10 @@ for rep in range(a.reps):
             ref = y.clone()
         elif rep == 0:
             same = bool(torch.equal(torch.nan_to_num(y, 7.0), torch.nan_to_num(ref, 7.0)))
-            print(f"[{s}] {plan.last_kernel()} bit-identical to [{specs[0]}]: {same}", flush=True)
+            m = ~torch.isnan(ref)
+            d = (y[m].double() - ref[m].double())
+            rel = float(torch.sqrt(torch.sum(d * d) / torch.sum(ref[m].double() ** 2)))
+            print(f"[{s}] {plan.last_kernel()} bit-identical to [{specs[0]}]: {same}  relRMS {rel:.2e}", flush=True)
         for _ in range(a.steps):
             plan.execute(x, y, wsb, st)
             k1, sc = plan.last_timing_ms()
@@ -77,5 +80,5 @@ for rep in range(a.reps):
             res[s][1].append(sc)
 for s in specs:
     k1, sc = np.array(res[s][0]), np.array(res[s][1])
-    print(f"[{s:36s}] K1 mean {k1.mean():.3f} min {k1.min():.3f} max {k1.max():.3f} ms  "
+    print(f"[{s:36s}] K1 median {np.median(k1):.3f} mean {k1.mean():.3f} min {k1.min():.3f} max {k1.max():.3f} ms  "
           f"frac {alg / (k1.mean() * 1e-3) / 8e12:.3f}  scan {sc.mean():.3f} ms", flush=True)

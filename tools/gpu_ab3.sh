@@ -6,5 +6,5 @@ timeout -k 10 200 python tools/ab_plan.py --off-ns 1900000 --reps 2 "" > gpurun_
 cat gpurun_out/ab_off.log
 LFD_NO_HSKIP=1 timeout -k 10 200 python tools/ab_plan.py --off-ns 1900000 --reps 2 "" > gpurun_out/ab_off0.log 2>&1 || { tail -20 gpurun_out/ab_off0.log; exit 1; }
 cat gpurun_out/ab_off0.log
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/ubench_mfma64b tools/ubench_mfma64b.hip > gpurun_out/hipcc.log 2>&1
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -Wno-unused-result -o /tmp/ubench_mfma64b tools/ubench_mfma64b.hip > gpurun_out/hipcc.log 2>&1
 timeout -k 5 60 /tmp/ubench_mfma64b > gpurun_out/ub64b.txt 2>&1; cat gpurun_out/ub64b.txt

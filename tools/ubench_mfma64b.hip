@@ -22,10 +22,10 @@ __global__ __launch_bounds__(256) void k16(double *out, int iters, double seed) 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int r = AMODE == 1 && row >= 9 ? 8 : row;
-    a[i] = __builtin_sin(seed * (r + 1) + 0.37 * i + (lane >> 4));
+    a[i] = sin(seed * (r + 1) + 0.37 * i + (lane >> 4));
     if (AMODE == 2 && row >= 9) a[i] = 0.0;
     if (AMODE == 3) a[i] = 0.0;
-    b[i] = __builtin_cos(seed * (lane + 3) + 0.71 * i);
+    b[i] = cos(seed * (lane + 3) + 0.71 * i);
   }
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
@@ -43,8 +43,8 @@ __global__ __launch_bounds__(256) void k4(double *out, int iters, double seed) {
   double a[8], b[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    a[i] = __builtin_sin(seed * (lane + 1) + 0.37 * i);
-    b[i] = __builtin_cos(seed * (lane + 3) + 0.71 * i);
+    a[i] = sin(seed * (lane + 1) + 0.37 * i);
+    b[i] = cos(seed * (lane + 3) + 0.71 * i);
   }
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
