@@ -175,6 +175,21 @@ int lfd_rolling_mean_f32(const float *x, int64_t n_ch, int64_t n_t,
                          void *stream);
 
 /* ------------------------------------------------------------------------
+ * FIR decimation: DASCore Patch.decimate(time=q, filter_type='fir')
+ *   (dascore/proc/resample.py, external) = scipy.signal.decimate(x, q,
+ *   ftype='fir', zero_phase=True) = resample_poly(x, 1, q, window=h) with
+ *   h = firwin(20q+1, 1/q, window='hamming')
+ *   (scipy/signal/_signaltools.py decimate, _upfirdn.py):
+ *     y[k] = sum_{i < n_taps} taps[i] x[k*q + delay - i], x = 0 outside
+ *     [0, n_t), k in [0, ceil(n_t/q));  delay = resample_poly's centring
+ *     (10q for decimate's filter).  taps: device float64; y: device float64.
+ * ------------------------------------------------------------------------ */
+int lfd_fir_decimate_f32(const float *x, int64_t n_ch, int64_t n_t,
+                         int64_t s_ch, int64_t s_t, const double *taps_dev,
+                         int64_t n_taps, int64_t q, int64_t delay, double *y,
+                         int64_t ys_ch, int64_t ys_t, void *stream);
+
+/* ------------------------------------------------------------------------
  * LFProc chunk schedule (host arithmetic, no device): the index loop of
  *   lf_das.py:258-290.  rows[4*i..4*i+3] = (read_first, read_last, out_begin,
  *   out_end) grid indices of chunk i: it selects time_grid[read_first] ..

@@ -2395,7 +2395,50 @@ __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmI
   }
 }
 
-template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false>
+// tm_iter on v_mfma_f64_4x4x4_4b (mf_iter4's lane algebra): tile t's
+// functionals 4m + q accumulate in element m of acc_t (m < 3), i.e. acc_t
+// already holds (e_f[q], e_r0[q], p0) as block_done reads them
+template <bool SWAP>
+__device__ __forceinline__ void tm_iter4(const double *const (&kt)[3], int off, int kstride, const TmIter &b, int o0,
+                                         int q, bool mask, int lo, int hi, d4v &acc0, d4v &acc1) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double a[3][4];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const double2 b01 = *reinterpret_cast<const double2 *>(kt[m] + off + j * kstride);
+      const double2 b23 = *reinterpret_cast<const double2 *>(kt[m] + off + j * kstride + 2);
+      a[m][0] = b01.x;
+      a[m][1] = b01.y;
+      a[m][2] = b23.x;
+      a[m][3] = b23.y;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v0 = b.p[j][e], v1 = b.q[j][e];
+      if (SWAP) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
+        const auto s2 = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
+        v0 = __uint_as_float(s2[0]);
+        v1 = __uint_as_float(s2[1]);
+      }
+      if (mask) {
+        const int o = o0 + 16 * j + 4 * q + e;
+        if (o < lo || o >= hi) {
+          v0 = finite_or_zero(v0);
+          v1 = finite_or_zero(v1);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        acc0[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[m][e], (double)v0, acc0[m], 0, 0, 0);
+        acc1[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[m][e], (double)v1, acc1[m], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false>
 __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
@@ -2447,6 +2490,9 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
 
   const bool colv = col < tg.nc;
   const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
+  const double *kl4[3];  // (M4) tap columns of functionals 4m + (lane & 3)
+#pragma unroll
+  for (int m = 0; m < 3; ++m) kl4[m] = Ks + (q * tg.nc + min(4 * m + (lane & 3), tg.nc - 1)) * 4;
   const int nit = tg.Lp / 64;
   const int kstride = 16 * tg.nc;
   const int64_t s0 = g.base - tg.J;
@@ -2533,8 +2579,11 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     for (int it = 0; it < nit; ++it) {
       TmIter b;
       tm_load<true, SWAP, NTILE>(xc, xq, s_t, n_t, s + 64 * it + rsel, b);
-      tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0,
-                           acc1);
+      if (M4)
+        tm_iter4<SWAP>(kl4, (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0, acc1);
+      else
+        tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0,
+                             acc1);
     }
     finish_block(acc0, acc1, k);
   };
@@ -2577,7 +2626,10 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
         // a run's first and last iteration need the finite mask (chunk
         // boundaries are run boundaries)
         const bool mask = (it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen);
-        tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
+        if (M4)
+          tm_iter4<SWAP>(kl4, (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
+        else
+          tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
         if (++it == nit) {
           finish_block(acc0, acc1, k);
           acc0 = d4v{0.0, 0.0, 0.0, 0.0};
@@ -2654,6 +2706,13 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   const bool x2_ok = g.n_ch % 2 == 0 && s_t % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
   bool x2 = x2_ok;
   if (const char *v = std::getenv("LFD_TM_X2")) x2 = x2_ok && std::atoi(v) != 0;
+  bool m4 = false;
+  if (const char *v = std::getenv("LFD_TM_M4")) m4 = std::atoi(v) != 0;
+  if (m4 && x2 && !swap && ntile == 2) {
+    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, true>, 512);
+    if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true>, 512);
+    return hipErrorInvalidValue;
+  }
   if (x2 && !swap && ntile == 2) {
     if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, 512);
     if (nt == 512 && pf == 3) return go(&k_block_runs_mfma_tm<3, 512, false, 2, true>, 512);
@@ -3127,6 +3186,114 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     k_rolling_cols<<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, s_t, W, S, y, ys_ch, ys_t,
                                                     seg_out);
   }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// k_fir_decimate — FIR decimation by q (Patch.decimate(filter_type='fir'):
+// scipy.signal.decimate(x, q, ftype='fir', zero_phase=True) =
+// resample_poly(x, 1, q, window=firwin(20q+1, 1/q, 'hamming')),
+// scipy/signal/_signaltools.py decimate / resample_poly):
+//   y[k] = sum_{i < n_taps} h[i] x[k q + delay - i],  x = 0 outside [0, n_t)
+// in polyphase form: i = u q + v,  y[k] = sum_v sum_u h[u q + v] X_v[k - u]
+// with X_v[n] = x[n q + delay - v].  One workgroup = one channel x `to`
+// consecutive outputs; the input span is staged through LDS as the q
+// polyphase rows X_v (coalesced global reads, zero outside the record), so
+// the lanes' reads along a row are 2 words apart at any q (two-way bank
+// sharing, not q-dependent).  A thread owns two consecutive outputs: walking u,
+// each X_v value it loads feeds both (2 fp64 FMAs per LDS read); the taps
+// are wave-uniform (scalar loads).  Every input sample is read from HBM
+// once per tile (+ the (U - 1) q halo).
+// ---------------------------------------------------------------------------
+constexpr int FD_THREADS = 256;
+constexpr int FD_LDS = 64 * 1024;
+__global__ __launch_bounds__(FD_THREADS) void k_fir_decimate(const float *__restrict__ x, int64_t n_t, int64_t s_ch,
+                                                             int64_t s_t, const double *__restrict__ h,
+                                                             int n_taps, int q, int64_t delay, int64_t n_out,
+                                                             int tiles, int to, int U, int rowlen,
+                                                             double *__restrict__ y, int64_t ys_ch,
+                                                             int64_t ys_t) {
+  extern __shared__ float fd_x[];  // [v][rowlen]: X_v[k0 - U + 1 + n]
+  const int64_t ch = blockIdx.x / tiles;
+  const int64_t k0 = (int64_t)(blockIdx.x % tiles) * to;
+  const int nrow = to + U;  // X_v values a tile reads (+1: the odd thread's second output)
+  const int64_t g0 = (k0 - U + 1) * q + delay - (q - 1);  // sample of m = 0
+  const float *xr = x + ch * s_ch;
+  // (span <= 16384: n = m / q by a float reciprocal, corrected to exact)
+  const int span = nrow * q;
+  const float rq = 1.0f / (float)q;
+  // 8 loads per thread in flight before their LDS writes (a tile is up to
+  // 16 K samples: enough bytes in flight per CU to stream)
+  constexpr int FU = 8;
+  for (int m0 = threadIdx.x; m0 < span; m0 += FU * blockDim.x) {
+    float xv8[FU];
+#pragma unroll
+    for (int e = 0; e < FU; ++e) {
+      const int m = m0 + e * blockDim.x;
+      const int64_t t = g0 + m;
+      xv8[e] = (m < span && t >= 0 && t < n_t) ? xr[t * s_t] : 0.0f;
+    }
+#pragma unroll
+    for (int e = 0; e < FU; ++e) {
+      const int m = m0 + e * blockDim.x;
+      if (m >= span) break;
+      int n = (int)((float)m * rq);
+      n -= n * q > m ? 1 : 0;
+      n += (n + 1) * q <= m ? 1 : 0;
+      const int v = q - 1 - (m - n * q);
+      fd_x[v * rowlen + n] = xv8[e];
+    }
+  }
+  __syncthreads();
+  for (int base = 2 * threadIdx.x; base < to; base += 2 * blockDim.x) {  // outputs k0 + base, + 1
+  double a0 = 0.0, a1 = 0.0;
+  for (int v = 0; v < q; ++v) {
+    const float *xv = fd_x + v * rowlen + base;
+    // output r uses X_v[base + r + U - 1 - u]: walking s = U - 1 - u upward,
+    // x_s feeds output 0 and x_{s+1} output 1
+    double xs = (double)xv[0];
+#pragma unroll 4
+    for (int s2 = 0; s2 < U; ++s2) {
+      const int u = U - 1 - s2;
+      const double xn = (double)xv[s2 + 1];
+      if (u * q + v < n_taps) {
+        const double hv = h[u * q + v];
+        a0 = fma(hv, xs, a0);
+        a1 = fma(hv, xn, a1);
+      }
+      xs = xn;
+    }
+  }
+  const int64_t k = k0 + base;
+  if (k < n_out) y[ch * ys_ch + k * ys_t] = a0;
+  if (base + 1 < to && k + 1 < n_out) y[ch * ys_ch + (k + 1) * ys_t] = a1;
+  }
+}
+
+hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
+                               const double *h, int n_taps, int64_t q, int64_t delay, double *y, int64_t ys_ch,
+                               int64_t ys_t, hipStream_t st) {
+  const int64_t n_out = (n_t + q - 1) / q;
+  if (n_taps < 1 || q < 1 || q > (1 << 20) || n_out < 1) return hipErrorInvalidValue;
+  const int U = (int)((n_taps + q - 1) / q);  // taps per polyphase branch
+  // outputs per tile: q rows of (to + U) staged floats (odd row length) in LDS
+  const int64_t cap = std::min<int64_t>(16 * 1024 / q, FD_LDS / 4 / q) - U - 2;  // span <= 16 K samples
+  if (cap < 1) return hipErrorInvalidValue;
+  const int to = (int)std::min<int64_t>({(int64_t)2 * FD_THREADS, cap, n_out});
+  const int rowlen = (to + U) | 1;
+  const int64_t tiles = (n_out + to - 1) / to;
+  if (n_ch * tiles > (int64_t)INT32_MAX) return hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * (size_t)q * rowlen;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, FD_LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  k_fir_decimate<<<(unsigned)(n_ch * tiles), FD_THREADS, lds, st>>>(x, n_t, s_ch, s_t, h, n_taps, (int)q, delay,
+                                                                     n_out, (int)tiles, to, U, rowlen, y, ys_ch,
+                                                                     ys_t);
   return hipGetLastError();
 }
 

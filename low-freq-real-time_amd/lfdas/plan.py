@@ -242,6 +242,20 @@ def filtfilt_resample_device(x, sos, lo, w, padlen: int = -1, stream=None):
     return y
 
 
+def fir_decimate_device(x, taps, q: int, delay: int, stream=None):
+    """FIR decimation ``y[k] = sum_i taps[i] x[k q + delay - i]`` (zeros
+    outside the record) → float64 (n_ch, ceil(n_t/q)) (``lfd_fir_decimate_f32``)."""
+    import torch
+    _require_cuda(x, "x", torch.float32)
+    n_ch, n_t = x.shape
+    h = torch.as_tensor(np.ascontiguousarray(taps, dtype=np.float64)).to(x.device)
+    y = torch.empty((n_ch, -(-n_t // int(q))), dtype=torch.float64, device=x.device)
+    check(load().lfd_fir_decimate_f32(_ptr(x), n_ch, n_t, x.stride(0), x.stride(1), _ptr(h), h.numel(),
+                                      int(q), int(delay), _ptr(y), y.stride(0), y.stride(1),
+                                      _stream_ptr(stream)))
+    return y
+
+
 def rolling_mean_device(x, window: int, step: int, stream=None):
     """Rolling mean at the subsampled output points → float32 (n_ch, ceil(n_t/step))."""
     import torch

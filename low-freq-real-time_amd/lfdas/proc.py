@@ -251,8 +251,9 @@ def decimate(patch: Patch, filter_type=None, **kwargs):
     ftype='iir', axis=time, zero_phase=True)`` — 8th-order Chebyshev I at
     0.8/q (designed on the host), zero-phase ``sosfiltfilt`` and the q-th
     sample pick fused in one device pass (``lfd_sos_filtfilt_resample_f32``,
-    grid = every q-th sample).  *(DASCore, external: the wrapper is unpinned;
-    ``'fir'`` (resample_poly) is not on the device path.)*"""
+    grid = every q-th sample).  ``'fir'``: ``scipy.signal.decimate(...,
+    ftype='fir')`` = ``resample_poly`` with decimate's 20q+1-tap Hamming
+    FIR (``_decimate_fir``).  *(DASCore, external: the wrapper is unpinned.)*"""
     if len(kwargs) != 1:
         raise ValueError("decimate takes exactly one dimension keyword, e.g. time=5")
     (dim, q), = kwargs.items()
@@ -267,12 +268,13 @@ def decimate(patch: Patch, filter_type=None, **kwargs):
         idx[ax] = slice(None, None, q)
         return Patch(data=patch.device_data()[tuple(idx)], coords=coords, dims=patch.dims,
                      attrs=patch._attrs_wo_coords())
-    if str(filter_type).lower() != "iir":
-        raise NotImplementedError(f"decimate filter_type={filter_type!r} is not on the device path "
-                                  "(supported: None, 'iir')")
+    if str(filter_type).lower() not in ("iir", "fir"):
+        raise ValueError(f"decimate filter_type={filter_type!r}: expected None, 'iir' or 'fir'")
     if dim != "time":
         raise NotImplementedError("only time-axis decimation is on the device path")
     import scipy.signal as _sig
+    if str(filter_type).lower() == "fir":
+        return _decimate_fir(patch, q, coords)
 
     from .plan import filtfilt_resample_device
     sos = np.ascontiguousarray(_sig.cheby1(8, 0.05, 0.8 / q, output="sos"), dtype=np.float64)
@@ -286,6 +288,34 @@ def decimate(patch: Patch, filter_type=None, **kwargs):
     y = filtfilt_resample_device(x, sos, lo, w, padlen)
     data = _from_ct(y, patch.dims).astype(np.float64)
     return Patch(data=data, coords=coords, dims=patch.dims, attrs=patch._attrs_wo_coords())
+
+
+def fir_decimate_design(q: int):
+    """scipy.signal.decimate(ftype='fir')'s filter and resample_poly's
+    centring (scipy/signal/_signaltools.py decimate: firwin(20q+1, 1/q,
+    window='hamming'); resample_poly: n_pre_pad = q - half_len % q, output k
+    = full-convolution index (k + (half_len + n_pre_pad) // q) q)."""
+    import scipy.signal as _sig
+    h = np.asarray(_sig.firwin(20 * q + 1, 1.0 / q, window="hamming"), dtype=np.float64)
+    half = (h.size - 1) // 2
+    pre_pad = q - half % q
+    # resample_poly convolves with the pre-padded filter, so its leading
+    # zeros stay in the taps: a NaN there gives NaN as in SciPy (0 * NaN)
+    taps = np.concatenate([np.zeros(pre_pad), h])
+    delay = (half + pre_pad) // q * q
+    return taps, delay
+
+
+def _decimate_fir(patch: Patch, q: int, coords) -> Patch:
+    """``decimate(time=q, filter_type='fir')``: scipy.signal.decimate(x, q,
+    ftype='fir', axis=time, zero_phase=True) = resample_poly(x, 1, q,
+    window=firwin(20q+1, 1/q)) on the device (``lfd_fir_decimate_f32``:
+    LDS-staged float64 FIR at the kept samples only)."""
+    from .plan import fir_decimate_device
+    taps, delay = fir_decimate_design(q)
+    x = to_device_ct(patch)
+    y = fir_decimate_device(x, taps, q, delay)
+    return Patch(data=_from_ct(y, patch.dims), coords=coords, dims=patch.dims, attrs=patch._attrs_wo_coords())
 
 
 def _to_samples(patch: Patch, v) -> int:

@@ -21,7 +21,7 @@ __all__ = [
     "pass_filter", "interpolate", "rolling_mean", "rolling_out_times",
     "get_patch_time", "lfproc_time_grid", "lfproc_schedule", "lfproc_process",
     "down_sample_processing", "get_edge_effect_time", "have_c_oracle",
-    "sosfiltfilt_rows_c", "edge_loop", "lp2bp_zpk", "cheb1ap", "cheby1_sos", "decimate_iir",
+    "sosfiltfilt_rows_c", "edge_loop", "lp2bp_zpk", "cheb1ap", "cheby1_sos", "decimate_iir", "firwin_hamming", "decimate_fir",
     "median_filter", "demean_scale",
 ]
 
@@ -168,6 +168,45 @@ def decimate_iir(x, q: int, axis: int = -1):
     sl = [slice(None)] * y.ndim
     sl[axis] = slice(None, None, q)
     return y[tuple(sl)]
+
+
+def firwin_hamming(numtaps: int, cutoff: float):
+    """``scipy.signal.firwin(numtaps, cutoff, window='hamming')`` (low-pass,
+    scale=True; scipy/signal/_fir_filter_design.py firwin): windowed sinc
+    ``cutoff * sinc(cutoff * m)``, m = n - (numtaps - 1)/2, times the
+    symmetric Hamming window ``0.54 - 0.46 cos(2 pi n / (numtaps - 1))``,
+    normalised to unit DC gain."""
+    n = np.arange(numtaps, dtype=np.float64)
+    m = n - 0.5 * (numtaps - 1)
+    h = cutoff * np.sinc(cutoff * m)
+    h = h * (0.54 - 0.46 * np.cos(2.0 * np.pi * n / (numtaps - 1)))
+    return h / np.sum(h)
+
+
+def decimate_fir(x, q: int, axis: int = -1):
+    """``scipy.signal.decimate(x, q, ftype='fir', axis=axis, zero_phase=True)``
+    (scipy/signal/_signaltools.py decimate) = ``resample_poly(x, 1, q,
+    window=firwin(20q+1, 1/q, 'hamming'))`` (_signaltools.py resample_poly,
+    padtype 'constant'): the filter is pre-padded with n_pre = q - half % q
+    zeros (half = 10q), the full convolution is taken every q-th sample from
+    index n_pre_remove q (n_pre_remove = (half + n_pre) // q), ceil(n/q)
+    outputs; samples outside the record are zeros.  float64."""
+    x = np.moveaxis(np.asarray(x, dtype=np.float64), axis, -1)
+    h = firwin_hamming(20 * q + 1, 1.0 / q)
+    half = (h.size - 1) // 2
+    n_pre = q - half % q
+    n_pre_remove = (half + n_pre) // q
+    hp = np.concatenate([np.zeros(n_pre), h])
+    n = x.shape[-1]
+    n_out = -(-n // q)
+    flat = x.reshape(-1, n)
+    out = np.empty((flat.shape[0], n_out))
+    idx = (n_pre_remove + np.arange(n_out)) * q
+    for r in range(flat.shape[0]):
+        full = np.convolve(flat[r], hp)
+        full = np.concatenate([full, np.zeros(max(0, int(idx[-1]) + 1 - full.size))])
+        out[r] = full[idx]
+    return np.moveaxis(out.reshape(x.shape[:-1] + (n_out,)), -1, axis)
 
 
 def median_filter(a, size):

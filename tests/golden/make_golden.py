@@ -134,6 +134,8 @@ def main_next_rows():
     for q in (2, 5, 10, 50):
         band[f"cheby_{q}"] = ss.cheby1(8, 0.05, 0.8 / q, output="sos")
         band[f"dec_{q}"] = ss.decimate(x, q, ftype="iir", axis=-1)
+        band[f"firwin_{q}"] = ss.firwin(20 * q + 1, 1.0 / q, window="hamming")
+        band[f"decfir_{q}"] = ss.decimate(x, q, ftype="fir", axis=-1)
     np.savez_compressed(os.path.join(HERE, "band_decimate.npz"), **band)
     rng = np.random.default_rng(77)
     post = {"x2": rng.standard_normal((40, 23)), "x1": rng.standard_normal(200)}

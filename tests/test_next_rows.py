@@ -1,6 +1,6 @@
 """SURVEY §8(f) rows beside the hot path, each to the same bar:
 band-/high-pass ``pass_filter`` through the same device kernels, DASCore
-``decimate(filter_type='iir')`` (restated as scipy.signal.decimate), and the
+``decimate(filter_type='iir' | 'fir')`` (restated as scipy.signal.decimate), and the
 notebook post-processing (demean + strain-rate scale, scipy.ndimage
 median_filter) on device.
 
@@ -44,6 +44,26 @@ def test_decimate_iir_matches_golden(q):
     g = _g("band_decimate.npz")
     np.testing.assert_allclose(oracle.cheby1_sos(8, 0.05, 0.8 / q), g[f"cheby_{q}"], rtol=0, atol=1e-15)
     assert _rel(oracle.decimate_iir(g["x"], q), g[f"dec_{q}"]) < 1e-13
+
+
+@pytest.mark.parametrize("q", [2, 5, 10, 50])
+def test_decimate_fir_matches_golden(q):
+    """decimate(ftype='fir'): firwin(20q+1, 1/q, 'hamming') and resample_poly
+    restated; the device design helper uses the same taps and centring."""
+    from lfdas.proc import fir_decimate_design
+    g = _g("band_decimate.npz")
+    np.testing.assert_allclose(oracle.firwin_hamming(20 * q + 1, 1.0 / q), g[f"firwin_{q}"], rtol=0, atol=1e-16)
+    assert _rel(oracle.decimate_fir(g["x"], q), g[f"decfir_{q}"]) < 1e-13
+    taps, delay = fir_decimate_design(q)
+    np.testing.assert_array_equal(taps[taps.size - 20 * q - 1:], g[f"firwin_{q}"])
+    assert not np.any(taps[:taps.size - 20 * q - 1])
+    # y[k] = sum_i taps[i] x[k q + delay - i]: the restated kernel formula
+    x = g["x"]
+    xp = np.concatenate([np.zeros((x.shape[0], taps.size)), x, np.zeros((x.shape[0], delay + q))], axis=1)
+    n_out = -(-x.shape[1] // q)
+    k = np.arange(n_out)
+    y = np.stack([xp[:, taps.size + k * q + delay - i] for i in range(taps.size)], 0)
+    assert _rel(np.einsum("i,irk->rk", taps, y), g[f"decfir_{q}"]) < 1e-13
 
 
 def test_median_and_demean_match_golden():
@@ -134,5 +154,38 @@ def test_decimate_iir_device(q):
     np.testing.assert_array_equal(out.coords["time"], p.coords["time"][::q])
     assert _rel(out.data, ref) < 1e-4
     assert _rel(out.data, g[f"dec_{q}"]) < 1e-4  # SciPy on the float64 data
-    with pytest.raises(NotImplementedError):
-        p.decimate(time=q, filter_type="fir")
+    with pytest.raises(ValueError):
+        p.decimate(time=q, filter_type="kaiser")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [2, 5, 10, 50])
+@pytest.mark.parametrize("layout", ["row", "col"])
+def test_decimate_fir_device(q, layout):
+    """decimate(filter_type='fir') on device (lfd_fir_decimate_f32): float64
+    FIR at the kept samples vs the oracle on the same float32 samples
+    (relRMS 1e-12) and vs SciPy on the float64 data (1e-6); a NaN poisons
+    exactly the outputs whose window holds it."""
+    import lfdas.dc as dc
+    g = _g("band_decimate.npz")
+    x = g["x"]
+    x32 = x.astype(np.float32)
+    if layout == "row":
+        p = _patch(x, 250.0)
+    else:
+        t = T0 + np.arange(x.shape[1]) * np.timedelta64(4_000_000, "ns")
+        p = dc.Patch(data=np.ascontiguousarray(x.T), coords={"time": t, "distance": np.arange(float(x.shape[0]))},
+                     dims=("time", "distance"))
+    out = p.decimate(time=q, filter_type="fir")
+    d = out.data if layout == "row" else out.data.T
+    ref = oracle.decimate_fir(x32.astype(np.float64), q)
+    assert d.dtype == np.float64 and d.shape == ref.shape
+    np.testing.assert_array_equal(out.coords["time"], p.coords["time"][::q])
+    assert _rel(d, ref) < 1e-12
+    assert _rel(d, g[f"decfir_{q}"]) < 1e-6
+    xn = x32.copy()
+    xn[1, 1234] = np.nan
+    dn = _patch(xn, 250.0).decimate(time=q, filter_type="fir").data
+    refn = oracle.decimate_fir(xn.astype(np.float64), q)
+    np.testing.assert_array_equal(np.isnan(dn), np.isnan(refn))
+    assert np.isnan(dn).sum() > 0
