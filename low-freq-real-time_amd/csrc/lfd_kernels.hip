@@ -1541,14 +1541,23 @@ __device__ __forceinline__ float null_mean(int64_t code, float mean) {
 // order; bit 1 = S == 1 outputs leave through LDS the same way (coalesced
 // float4 stores); else lanes load / store their 8 positions directly.
 constexpr int RS_ROW = RS_E + 4;    // padded LDS row (floats): conflict-free ds_read_b128
-template <bool VEC, int STAGE, int NPF = 1, int MINW = 3>
+// RING: the samples leaving the window, x[t - W], come from a wave-private
+// LDS ring of the last ring_mask + 1 >= W + 512 samples (each step writes
+// its 512 new samples there) instead of a second global read: the global
+// re-read missed L2 for 40 % of its bytes (PMC, 16.9 GB fetched for 12 GB of
+// input at W = 1000, S = 1).
+template <bool VEC, int STAGE, int NPF = 1, int MINW = 3, bool RING = false>
 __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
-    float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out) {
+    float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out, int ring_mask) {
   // positions are row-relative int32 (the launcher checks n_t < 2^31 - 1024)
-  __shared__ __attribute__((aligned(16))) float lds_all[(STAGE & 3) ? 4 : 1][2][(STAGE & 3) ? 64 * RS_ROW : 4];
+  __shared__ __attribute__((aligned(16))) float lds_all[(STAGE & 3) ? 4 : 1][(STAGE & 1) ? 2 : 1]
+                                                       [(STAGE & 3) ? 64 * RS_ROW : 4];
+  extern __shared__ __attribute__((aligned(16))) float rs_ring_all[];
+  float *ring = rs_ring_all + (RING ? (threadIdx.x >> 6) * (ring_mask + 1) : 0);
   const int lane = threadIdx.x & 63;
-  float *lx = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][0], *lo_ = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][1];
+  float *lx = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][0];
+  float *lo_ = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][(STAGE & 1) ? 1 : 0];
   const int n_out = (n_t + S - 1) / S;
   const int n_seg = (n_out + seg_out - 1) / seg_out;
   const int64_t n_units = (int64_t)n_seg * n_ch;
@@ -1575,8 +1584,8 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
       double acc = 0.0;
       int64_t cnt = 0;
       for (int m = p0 - W + lane; m < p0; m += 64) {
-        if (m < 0) continue;
-        const float v = row[m];
+        const float v = m < 0 ? 0.0f : row[m];
+        if (RING) ring[m & ring_mask] = v;  // (x[m < 0] = 0 in the ring)
         acc += __builtin_isfinite(v) ? (double)v : 0.0;
         cnt += null_code(v);
       }
@@ -1591,7 +1600,21 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     };
     auto load = [&](int tb, Tile &T) {
       const int t = tb + RS_E * lane;
-      const bool full = tb + RS_P <= n_t && tb - W >= 0;
+      const bool full = tb + RS_P <= n_t && (RING || tb - W >= 0);
+      if (RING) {  // x[t - W] comes from the ring in process()
+        if (full) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f4v a = *reinterpret_cast<const f4v *>(row + t + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < RS_E; ++e) T.xi[e] = t + e < n_t ? row[t + e] : 0.0f;
+        }
+        return;
+      }
       if ((STAGE & 1) && VEC && full) {
         // coalesced: float4 j of lane l = positions 4l + 256j (unstaged here;
         // process() moves them to lane-consecutive order through LDS)
@@ -1637,7 +1660,32 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     auto process = [&](int tb, const Tile &Tin) {
       const int t = tb + RS_E * lane;  // this lane's first position
       Tile T = Tin;
-      if ((STAGE & 1) && VEC && tb + RS_P <= n_t && tb - W >= 0) {
+      if (RING) {
+        // this step's samples into the ring, then x[t - W] out of it (W + 512
+        // <= ring size: nothing a later read needs is overwritten)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          *reinterpret_cast<f4v *>(ring + ((t + 4 * h) & ring_mask)) =
+              f4v{T.xi[4 * h], T.xi[4 * h + 1], T.xi[4 * h + 2], T.xi[4 * h + 3]};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if ((W & 3) == 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f4v b = *reinterpret_cast<const f4v *>(ring + ((t + 4 * h - W) & ring_mask));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < RS_E; ++e) T.xo[e] = ring[(t + e - W) & ring_mask];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      if (!RING && (STAGE & 1) && VEC && tb + RS_P <= n_t && tb - W >= 0) {
         // coalesced -> lane-consecutive through LDS (padded rows of 12 floats)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -3154,17 +3202,34 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     int npf = 1, minw = 3;
     if (const char *v = std::getenv("LFD_ROLL_PF")) npf = std::atoi(v);
     if (const char *v = std::getenv("LFD_ROLL_MINW")) minw = std::atoi(v);
+    // LDS ring for x[t - W] (vector rows, W + 512 <= 4096): A/B knob LFD_ROLL_RING
+    int ring = 0;
+    while (ring < W + RS_P) ring = ring ? 2 * ring : 1024;
+    bool use_ring = vec && ring <= 4096 && stage == 2 && npf == 1 && minw == 3;
+    if (const char *v = std::getenv("LFD_ROLL_RING")) use_ring = use_ring && std::atoi(v) != 0;
+    if (use_ring) {
+      static bool attr = false;
+      if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rolling_scan_tc<true, 2, 1, 3, true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 4096 * 4);
+        if (e != hipSuccess) return e;
+        attr = true;
+      }
+      k_rolling_scan_tc<true, 2, 1, 3, true><<<(unsigned)blocks, 256, sizeof(float) * 4 * ring, st>>>(
+          x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, ys_t, (int)seg_out, vec_out, ring - 1);
+      return hipGetLastError();
+    }
 #define LFD_ROLL(V, ST, PF_)                                                                                    \
   k_rolling_scan_tc<V, ST, PF_><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, \
-                                                             ys_t, (int)seg_out, V && vec_out)
+                                                             ys_t, (int)seg_out, V && vec_out, 0)
     if (!vec)
       LFD_ROLL(false, 0, 1);
     else if (stage == 2 && npf == 1 && minw == 4)
       k_rolling_scan_tc<true, 2, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
-                                                                      ys_ch, ys_t, (int)seg_out, vec_out);
+                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0);
     else if (stage == 2 && npf == 2 && minw == 4)
       k_rolling_scan_tc<true, 2, 2, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
-                                                                      ys_ch, ys_t, (int)seg_out, vec_out);
+                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0);
     else if (stage == 2 && npf == 2)
       LFD_ROLL(true, 2, 2);
     else if (stage == 2 && npf == 3)

@@ -13,7 +13,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu --no-rolling --no-stream "$@" > $OUT/bench_traced.log 2>&1
-FULL="--steps 2 --warmup 0 --no-cpu --no-rolling --no-stream"
+FULL="--steps 2 --warmup 0 --no-cpu --no-rolling --no-stream --no-extra"
 timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_fetch -o fetch --pmc FETCH_SIZE \
     --kernel-include-regex k_block_ -- python3 bench.py $FULL "$@" > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d $OUT/pmc_write -o write --pmc WRITE_SIZE \
@@ -22,5 +22,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/calib_fetch -o cf --pm
     -- ./tools/ubench_hbm_pattern > $OUT/calib_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/calib_write -o cw --pmc WRITE_SIZE \
     -- ./tools/ubench_hbm_pattern > $OUT/calib_write.log 2>&1
+# the rolling-mean kernels (cfg2, W = S = 1000 and S = 1)
+timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/roll_fetch -o rf --pmc FETCH_SIZE \
+    --kernel-include-regex k_rolling -- python3 tools/roll_only.py > $OUT/roll_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/roll_write -o rw --pmc WRITE_SIZE \
+    --kernel-include-regex k_rolling -- python3 tools/roll_only.py > $OUT/roll_write.log 2>&1
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
 echo done
