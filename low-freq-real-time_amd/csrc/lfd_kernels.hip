@@ -1519,7 +1519,10 @@ __global__ __launch_bounds__(256) void k_rolling_cols(
 // tests: a null makes the lane total non-finite, which sends the step to
 // the general path).  The segment's first window is summed directly (a halo
 // of W samples per segment: segments are >= 4W).
-constexpr int RS_E = 8;             // positions per lane per step
+#ifndef LFD_RS_E
+#define LFD_RS_E 8
+#endif
+constexpr int RS_E = LFD_RS_E;      // positions per lane per step
 constexpr int RS_P = 64 * RS_E;     // positions per wave step
 // Null bookkeeping of the running sum: each sample contributes a packed code
 // (NaN: 1, +inf: 2^21, -inf: 2^42; finite: 0); a window's summed code holds
@@ -1604,7 +1607,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
       if (RING) {  // x[t - W] comes from the ring in process()
         if (full) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < RS_E / 4; ++h) {
             const f4v a = *reinterpret_cast<const f4v *>(row + t + 4 * h);
 #pragma unroll
             for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
@@ -1619,7 +1622,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         // coalesced: float4 j of lane l = positions 4l + 256j (unstaged here;
         // process() moves them to lane-consecutive order through LDS)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RS_E / 4; ++h) {
           const int tc = tb + 4 * lane + 256 * h;
           const f4v a = *reinterpret_cast<const f4v *>(row + tc);
 #pragma unroll
@@ -1635,7 +1638,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         }
       } else if (VEC && full) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RS_E / 4; ++h) {
           const f4v a = *reinterpret_cast<const f4v *>(row + t + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
@@ -1664,7 +1667,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         // this step's samples into the ring, then x[t - W] out of it (W + 512
         // <= ring size: nothing a later read needs is overwritten)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < RS_E / 4; ++h)
           *reinterpret_cast<f4v *>(ring + ((t + 4 * h) & ring_mask)) =
               f4v{T.xi[4 * h], T.xi[4 * h + 1], T.xi[4 * h + 2], T.xi[4 * h + 3]};
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1672,7 +1675,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if ((W & 3) == 0) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < RS_E / 4; ++h) {
             const f4v b = *reinterpret_cast<const f4v *>(ring + ((t + 4 * h - W) & ring_mask));
 #pragma unroll
             for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
@@ -1688,9 +1691,9 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
       if (!RING && (STAGE & 1) && VEC && tb + RS_P <= n_t && tb - W >= 0) {
         // coalesced -> lane-consecutive through LDS (padded rows of 12 floats)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RS_E / 4; ++h) {
           const int pos = 4 * lane + 256 * h;
-          const int off = (pos >> 3) * RS_ROW + (pos & 7);
+          const int off = (pos / RS_E) * RS_ROW + (pos % RS_E);
           *reinterpret_cast<f4v *>(lx + off) = f4v{Tin.xi[4 * h], Tin.xi[4 * h + 1], Tin.xi[4 * h + 2], Tin.xi[4 * h + 3]};
           *reinterpret_cast<f4v *>(lo_ + off) = f4v{Tin.xo[4 * h], Tin.xo[4 * h + 1], Tin.xo[4 * h + 2], Tin.xo[4 * h + 3]};
         }
@@ -1698,7 +1701,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RS_E / 4; ++h) {
           const f4v a = *reinterpret_cast<const f4v *>(lx + lane * RS_ROW + 4 * h);
           const f4v b = *reinterpret_cast<const f4v *>(lo_ + lane * RS_ROW + 4 * h);
 #pragma unroll
@@ -1772,22 +1775,23 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         // lane-consecutive -> coalesced through LDS: float4 j of lane l =
         // positions 4l + 256j
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < RS_E / 4; ++h)
           *reinterpret_cast<f4v *>(lx + lane * RS_ROW + 4 * h) = f4v{o8[4 * h], o8[4 * h + 1], o8[4 * h + 2], o8[4 * h + 3]};
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < RS_E / 4; ++h) {
           const int pos = 4 * lane + 256 * h;
-          *reinterpret_cast<f4v *>(yo + tb + pos) = *reinterpret_cast<const f4v *>(lx + (pos >> 3) * RS_ROW + (pos & 7));
+          *reinterpret_cast<f4v *>(yo + tb + pos) = *reinterpret_cast<const f4v *>(lx + (pos / RS_E) * RS_ROW + (pos % RS_E));
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       } else if (S == 1 && vec_out && !general) {
-        *reinterpret_cast<f4v *>(yo + t) = f4v{o8[0], o8[1], o8[2], o8[3]};
-        *reinterpret_cast<f4v *>(yo + t + 4) = f4v{o8[4], o8[5], o8[6], o8[7]};
+#pragma unroll
+        for (int h = 0; h < RS_E / 4; ++h)
+          *reinterpret_cast<f4v *>(yo + t + 4 * h) = f4v{o8[4 * h], o8[4 * h + 1], o8[4 * h + 2], o8[4 * h + 3]};
       } else {
         // outputs: positions t + e with (t + e) % S == 0
         int ph = t % S;
