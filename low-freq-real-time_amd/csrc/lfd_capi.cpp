@@ -649,7 +649,9 @@ struct lfd_lowpass_plan {
   int64_t *d_run_ks = nullptr;
   int *d_run_len = nullptr, *d_group_r0 = nullptr;
   lfd::RunConst *d_rc = nullptr;
-  size_t off_Y0 = 0, off_AG = 0, off_SR = 0;
+  std::vector<int> slot_chunk;    // run slot (chunk-ordered runs) -> its chunk
+  int *d_slot_chunk = nullptr;
+  size_t off_Y0 = 0, off_AG = 0, off_SR = 0, off_TR = 0, off_CR = 0;
   int64_t sf_blocks = 0, tp_len = 0;
   size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -851,11 +853,20 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     // that >= ~4,096 wave units cover the chip)
     // (k_block_runs_mfma holds a unit's run table one run per lane: a unit of
     // <= 32 blocks has <= 32 runs, well inside the 64 lanes)
+    // (at least ~16 rounds of units over the 4,096 resident waves: a
+    // 1,250-channel shard (8 GPUs) ran its last, partial round of 32-block
+    // units 7 % longer than with 16-block ones, tools/ab_plan.py --replan)
     int64_t unit_cap = 32;
-    if (const char *v = std::getenv("LFD_RUN_UNIT"))
+    int64_t unit_min = 16;
+    if (const char *v = std::getenv("LFD_RUN_UNIT")) {
       unit_cap = std::min<int64_t>(32, std::max(lfd::RUN_R, std::atoi(v)));
+      unit_min = lfd::RUN_R;
+    }
+    const int64_t blocks_all = ((n_ch + 15) / 16) * p->bg.nb;
     const int64_t unit_blocks =
-        std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(unit_cap, ((n_ch + 15) / 16) * p->bg.nb / 4096));
+        blocks_all / 4096 >= 32
+            ? std::max<int64_t>(std::min(unit_min, unit_cap), std::min<int64_t>(unit_cap, blocks_all / (16 * 4096)))
+            : std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(unit_cap, blocks_all / 4096));
     int acc = 0;
     for (int64_t r = 0; r < n_runs; ++r) {
       if (r == 0 || acc + p->run_len[r] > unit_blocks) {
@@ -874,11 +885,13 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
       return (int64_t)(std::lower_bound(p->run_ks.begin(), p->run_ks.end(), k) - p->run_ks.begin());
     };
     int64_t sr = 0;
-    for (auto &G : p->chunks) {
+    for (size_t ci = 0; ci < p->chunks.size(); ++ci) {
+      auto &G = p->chunks[ci];
       G.r0 = run_at(G.kb);
       G.r1 = run_at(G.ke);
       G.sr_off = sr;
       sr += G.r1 - G.r0;
+      p->slot_chunk.insert(p->slot_chunk.end(), (size_t)(G.r1 - G.r0), (int)ci);
     }
     p->n_sr = sr;
     run_constants(p->sc, p->rc);
@@ -897,7 +910,9 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     p->off_Y0 = p->off_SF;
     p->off_AG = align256(p->off_Y0 + sizeof(double) * (size_t)p->bg.nb * ch16);
     p->off_SR = align256(p->off_AG + sizeof(double) * (size_t)p->run_ks.size() * 8 * ch16);
-    end_F = std::max(end_F, align256(p->off_SR + sizeof(double) * (size_t)p->n_sr * 4 * ch64));
+    p->off_TR = align256(p->off_SR + sizeof(double) * (size_t)p->n_sr * 4 * ch64);
+    p->off_CR = align256(p->off_TR + sizeof(double) * (size_t)p->n_sr * 4 * ch64);
+    end_F = std::max(end_F, align256(p->off_CR + sizeof(double) * (size_t)n_chunks * ch64));
   }
   p->off_TP = end_F;
   p->ws_bytes = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);
@@ -951,6 +966,10 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     if (e == hipSuccess)
       e = hipMemcpy(p->d_group_r0, p->group_r0.data(), sizeof(int) * p->group_r0.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_rc, &p->rc, sizeof(lfd::RunConst), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_slot_chunk, sizeof(int) * std::max<size_t>(1, p->slot_chunk.size()));
+    if (e == hipSuccess && !p->slot_chunk.empty())
+      e = hipMemcpy(p->d_slot_chunk, p->slot_chunk.data(), sizeof(int) * p->slot_chunk.size(),
+                    hipMemcpyHostToDevice);
   }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
   if (e != hipSuccess) {
@@ -1018,8 +1037,10 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
       LFD_HIP(lfd::launch_fold_runs(F, p->bg, rg, Y0, AG, st));
     }
     if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
-    LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks,
-                                        p->n_chunks, Y0, AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st));
+    LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks, p->n_chunks, Y0,
+                                        AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st,
+                                        reinterpret_cast<double *>(ws + p->off_TR),
+                                        reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk));
     if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
     return LFD_OK;
   }
@@ -1105,7 +1126,8 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);
   if (p->d_taps_tm) (void)hipFree(p->d_taps_tm);
-  for (void *d : {(void *)p->d_run_ks, (void *)p->d_run_len, (void *)p->d_group_r0, (void *)p->d_rc})
+  for (void *d : {(void *)p->d_run_ks, (void *)p->d_run_len, (void *)p->d_group_r0, (void *)p->d_rc,
+                  (void *)p->d_slot_chunk})
     if (d) (void)hipFree(d);
   for (auto &e : p->ev)
     if (e) (void)hipEventDestroy(e);

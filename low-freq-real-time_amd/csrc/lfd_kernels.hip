@@ -482,13 +482,19 @@ __constant__ int g_scan_diag = 0;
 // K1 unit order (see k_block_runs_mfma; 0 = channel-group-major)
 __constant__ int g_k1_band = 0;
 
-template <int NS, bool RUNS>
+// DEFER (run mode): the backward run scan only carries T and stores the T
+// entering every run (TR, laid out like SR) and the chunk's p0 correction
+// (CR [chunk][ch64]); k_run_outputs then forms the outputs of every run in
+// parallel.  The per-thread chain is then the 4x4 T recurrence alone: with
+// the outputs inside the chain a 1,250-channel shard spent 2.3 us per run
+// step on one wave per 7 SIMDs.
+template <int NS, bool RUNS, bool DEFER = false>
 __global__ __launch_bounds__(256) void k_chunk_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
     const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
     const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
     int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
-    const double *__restrict__ Y0) {
+    const double *__restrict__ Y0, double *__restrict__ TR = nullptr, double *__restrict__ CR = nullptr) {
   constexpr int N = 2 * NS;
   constexpr int J = 2 * NS;
   constexpr int NF = 2 * N + 1;
@@ -626,6 +632,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     }
   }
 
+  if (DEFER) CR[c * ((g.n_ch + 63) / 64 * 64) + ch] = corr[2 * N];
   // ---- forward scan over the full blocks (run mode: over runs; SF holds S_in
   // per run, F holds the run aggregates)
   const int64_t nF = NF;
@@ -655,10 +662,14 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
         for (int i = 0; i < N; ++i) agc[i] = agq[u][i];
         const int len = lenq[u];
-        if (r + DF < G.r1) {
-          lenq[u] = rg.run_len[r + DF];
+        {
+          // unconditional (clamped) prefetch: a conditional load makes the
+          // compiler wait for every load in flight (vmcnt(0)) before using
+          // the ring, so the ring never overlapped anything
+          const int64_t rn = min(r + DF, G.r1 - 1);
+          lenq[u] = rg.run_len[rn];
 #pragma unroll
-          for (int i = 0; i < N; ++i) agq[u][i] = agb[((r + DF) * 8 + i) * 16];
+          for (int i = 0; i < N; ++i) agq[u][i] = agb[(rn * 8 + i) * 16];
         }
         double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
         const double *P = rc.PhiFp[len];
@@ -793,8 +804,12 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         o.sin[i] = sr[i * SF_ISTRIDE];
         o.er[i] = agb[(r * 8 + 4 + i) * 16];
       }
+      // every y0 slot loaded (clamped to the plan's blocks; unused ones are
+      // masked where they are consumed): a fixed number of loads per run
+      if (!DEFER) {
 #pragma unroll
-      for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = is_out(o.ks + pp) && pp < o.len ? y0b[(o.ks + pp) * 16] : 0.0;
+        for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = y0b[min(o.ks + pp, g.nb - 1) * 16];
+      }
     };
     // ring of SCAN_DB runs (r-1 .. r-SCAN_DB in flight while run r is applied)
     constexpr int DB = SCAN_DB;
@@ -809,26 +824,33 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         load_run(G.r1 - 1 - u, g0, q[u]);
       }
     }
+    // (clamped like the loop's: slot u must hold max(r - DB, r0)'s geometry
+    // when run r = r1 - 1 - u is applied)
 #pragma unroll
-    for (int u = 0; u < DB; ++u)
-      if (G.r1 - 1 - u - DB >= G.r0) load_geo(G.r1 - 1 - u - DB, gq[u]);
+    for (int u = 0; u < DB; ++u) load_geo(max(G.r1 - 1 - u - DB, G.r0), gq[u]);
     for (int64_t rb = G.r1 - 1; rb >= G.r0 && !(g_scan_diag & 8); rb -= DB)
 #pragma unroll
     for (int u = 0; u < DB; ++u) {
       const int64_t r = rb - u;
       if (r < G.r0) break;
       const RunIn cur = q[u];
-      if (r - DB >= G.r0) load_run(r - DB, gq[u], q[u]);
-      if (r - 2 * DB >= G.r0) load_geo(r - 2 * DB, gq[u]);
+      // unconditional (clamped) prefetch, see the forward scan
+      load_run(max(r - DB, G.r0), gq[u], q[u]);
+      load_geo(max(r - 2 * DB, G.r0), gq[u]);
       const int len = cur.len;
       const int64_t ks = cur.ks;
       const double *sin = cur.sin;
+      if (DEFER) {
+        double *tr = TR + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
+#pragma unroll
+        for (int i = 0; i < N; ++i) tr[i * SF_ISTRIDE] = T[i];
+      }
       float ov[RUN_R];
 #pragma unroll
       for (int pp = 0; pp < RUN_R; ++pp) {
         const int64_t k = ks + pp;
         ov[pp] = 0.f;
-        if (pp >= len || !is_out(k)) continue;
+        if (DEFER || pp >= len || !is_out(k)) continue;
         double acc = cur.y0[pp] + (k == G.kb ? corr[2 * N] : 0.0);
         const double *A = rc.A[len][pp];
         const double *B = rc.B[len - 1 - pp];
@@ -840,7 +862,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         ov[pp] = (float)acc;
         if (!coal) y[ch * ys_ch + out_j(k) * ys_t] = ov[pp];
       }
-      if (coal) {
+      if (coal && !DEFER) {
         float(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
 #pragma unroll
         for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
@@ -2943,6 +2965,98 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
 }
 
 // ---------------------------------------------------------------------------
+// k_run_outputs — the outputs of every run, after k_chunk_scan<2, true, true>
+// has carried the states: one wave = 64 channels x one run slot j (runs of
+// all chunks, SR / TR layout), y(ks + p) = y0(ks + p) + A[len][p] S_in +
+// B[len-1-p] T_in (+ the chunk's p0 correction at block kb).  Outputs leave
+// through LDS as 8 rows x 8 consecutive samples per store instruction.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeom *__restrict__ cgs, RunGeom rg,
+                                                     const int *__restrict__ slot_chunk,
+                                                     const double *__restrict__ Y0, const double *__restrict__ SR,
+                                                     const double *__restrict__ TR, const double *__restrict__ CR,
+                                                     float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+  constexpr int N = RUN_N;
+  __shared__ RunConst rcs[1];
+  __shared__ float outs[4][64][RUN_R + 1];
+  {
+    const double *src = &rg.rc->PhiFp[0][0];
+    double *dst = &rcs[0].PhiFp[0][0];
+    for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t n_c64 = (g.n_ch + 63) / 64;
+  const int64_t w = uniform64((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (w >= n_c64 * rg.n_sr) return;
+  const int64_t c64 = w % n_c64, j = w / n_c64;
+  const int64_t ch = c64 * 64 + lane;
+  const bool valid = ch < g.n_ch;
+  const int c = __builtin_amdgcn_readfirstlane(slot_chunk[j]);
+  const ChunkGeom &G = cgs[c];
+  const int64_t r = G.r0 + (j - G.sr_off);
+  const int64_t ks = rg.run_ks[r];
+  const int len = rg.run_len[r];
+  const int kst = (int)G.kstep;
+  auto is_out = [&](int64_t k) {
+    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
+  };
+  auto out_j = [&](int64_t k) -> int64_t {
+    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
+  };
+  const int64_t chc = valid ? ch : g.n_ch - 1;
+  double sin[N], tin[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    sin[i] = SR[sf_index(j, i, chc, rg.n_sr, N)];
+    tin[i] = TR[sf_index(j, i, chc, rg.n_sr, N)];
+  }
+  const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
+  const double cr = CR[c * (n_c64 * 64) + chc];
+  const RunConst &rc = rcs[0];
+  float ov[RUN_R];
+#pragma unroll
+  for (int pp = 0; pp < RUN_R; ++pp) {
+    const int64_t k = ks + pp;
+    ov[pp] = 0.f;
+    if (pp >= len || !is_out(k)) continue;
+    double acc = y0b[k * 16] + (k == G.kb ? cr : 0.0);
+    const double *A = rc.A[len][pp];
+    const double *B = rc.B[len - 1 - pp];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      acc = fma(A[i], sin[i], acc);
+      acc = fma(B[i], tin[i], acc);
+    }
+    ov[pp] = (float)acc;
+  }
+  if (c64 * 64 + 63 < g.n_ch) {
+    float(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
+#pragma unroll
+    for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int e = lane & 7;
+    const int64_t k = ks + e;
+    const bool ok = e < len && is_out(k);
+    float *yb = y + (c64 * 64) * ys_ch + (ok ? out_j(k) : 0) * ys_t;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int row = m * 8 + (lane >> 3);
+      const float v = wl[row][e];
+      if (ok) yb[row * ys_ch] = v;
+    }
+  } else if (valid) {
+#pragma unroll
+    for (int pp = 0; pp < RUN_R; ++pp) {
+      const int64_t k = ks + pp;
+      if (pp < len && is_out(k)) y[ch * ys_ch + out_j(k) * ys_t] = ov[pp];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_fold_runs — run mode for the K1 kernels that emit per-block functionals
 // F (the recurrence kernels: strided / time-major / unaligned rows; the MFMA
 // kernel when taps + run buffers exceed LDS, L = 2000).  Applies the same
@@ -3052,7 +3166,24 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
-                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR,
+                                  double *CR, const int *slot_chunk) {
+  // deferred outputs (k_run_outputs) when the scan has few (chunk, channel)
+  // threads and is latency-bound: 1,250 ch x 7 chunks (an 8-GPU shard of
+  // cfg3) 0.247 -> 0.152 ms, 2,500 ch 0.263 -> 0.191, 5,000 ch equal, 10,000
+  // ch 0.339 -> 0.431 (the TR round trip); A/B knob LFD_SCAN_DEFER=0/1
+  bool defer = n_chunks * g.n_ch < 40000;
+  if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
+  if (TR && CR && slot_chunk && defer) {
+    const unsigned nb = nblk(n_chunks * g.n_ch, 256);
+    k_chunk_scan<2, true, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP, tp_len,
+                                                    y, ys_ch, ys_t, rg, Y0, TR, CR);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t waves = ((g.n_ch + 63) / 64) * rg.n_sr;
+    k_run_outputs<<<nblk(waves, 4), 256, 0, st>>>(g, cg, rg, slot_chunk, Y0, SR, TR, CR, y, ys_ch, ys_t);
+    return hipGetLastError();
+  }
   static int diag = -1, threads = 256;
   if (diag < 0) {
     const char *v = std::getenv("LFD_SCAN_DIAG");

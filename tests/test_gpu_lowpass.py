@@ -456,3 +456,21 @@ def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
         assert np.array_equal(np.isnan(yy), np.isnan(r))
         mm = ~np.isnan(r)
         assert _relrms(yy[mm], r[mm]) < 1e-4
+
+
+@pytest.mark.parametrize("off_ns", [0, 1_900_000])
+def test_scan_deferred_outputs_bit_identical(off_ns, monkeypatch):
+    """Run-mode scan with the outputs inside the backward chain
+    (LFD_SCAN_DEFER=0) and deferred to k_run_outputs (=1): same arithmetic,
+    bit-identical outputs, both against the oracle."""
+    fs, dt_out, P, B, n_ch, dur = 500.0, 1.0, 60, 7, 70, 400.0
+    x = (np.random.default_rng(3).standard_normal((n_ch, int(dur * fs))) + 5.0).astype(np.float32)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("LFD_SCAN_DEFER", mode)
+        out[mode] = _run(x, fs, dt_out, P, B, "tc", off_ns=off_ns)
+        assert _run.last_kernel == "mfma_runs"
+    np.testing.assert_array_equal(out["0"][0], out["1"][0])
+    y, ref, sched = out["1"]
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        assert _relrms(y[:, oa:ob], r) < 1e-4

@@ -34,6 +34,8 @@ ap.add_argument("--B", type=int, default=7)
 ap.add_argument("--off-ns", type=int, default=0)
 ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("--replan", action="store_true", help="rebuild the plan per spec (plan-time knobs)")
+ap.add_argument("--pad", type=int, default=0, help="channel rows padded by this many samples (row stride)")
 ap.add_argument("specs", nargs="*")
 a = ap.parse_args()
 specs = a.specs or [""]
@@ -45,8 +47,9 @@ if a.tm:
     bench.synth_fill_time_major(xs, a.fs, 77)
     x = xs.t()
 else:
-    x = torch.empty((a.ch, n), dtype=torch.float32, device=dev)
-    bench.synth_fill(x, a.fs, 77)
+    xp = torch.empty((a.ch, n + a.pad), dtype=torch.float32, device=dev)
+    bench.synth_fill(xp, a.fs, 77)
+    x = xp[:, :n]
 y = torch.empty((a.ch, plan.n_grid), dtype=torch.float32, device=dev)
 wsb = plan.alloc_workspace(dev)
 st = torch.cuda.current_stream(dev)
@@ -63,6 +66,11 @@ for rep in range(a.reps):
         for kv in s.split():
             k, v = kv.split("=", 1)
             os.environ[k] = v
+        if a.replan:
+            plan.close()
+            plan, *_ = bench.build_plan(a.ch, n, a.fs, a.dt, a.P, a.B, a.off_ns)
+            del wsb
+            wsb = plan.alloc_workspace(dev)
         plan.execute(x, y, wsb, st)
         torch.cuda.synchronize()
         if ref is None:
