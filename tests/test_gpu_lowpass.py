@@ -474,3 +474,31 @@ def test_scan_deferred_outputs_bit_identical(off_ns, monkeypatch):
     y, ref, sched = out["1"]
     for (tt, r), (a, b, oa, ob) in zip(ref, sched):
         assert _relrms(y[:, oa:ob], r) < 1e-4
+
+
+@pytest.mark.parametrize("which", ["lo", "head_first", "head_last", "fir_history"])
+def test_offsample_head_skip_nulls(which):
+    """Off-sample grids skip the chunk head with K1's one-block run kb-1
+    (ChunkGeom::hskip).  A null at the sample before the chunk start (inside
+    block kb-1 but outside the chunk) makes that (chunk, channel) walk its
+    head instead; nulls in the head or the FIR history must poison exactly
+    what SciPy's chunked sosfiltfilt poisons."""
+    fs, dt_out, P, B, n_ch, dur, off = 500.0, 1.0, 120, 7, 6, 400.0, 1_900_000
+    n = int(dur * fs)
+    dt_ns = int(round(1e9 / fs))
+    x = (np.random.default_rng(4).standard_normal((n_ch, n)) + 2.0).astype(np.float32)
+    t0, t1 = T0 + off, T0 + 1_000_000_000
+    tg = S.time_grid(t1, t0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    s0 = S.select_range(t0, dt_ns, n, tg[sched[1][0]], tg[sched[1][1]])[0]  # chunk 1's first sample
+    L = int(round(fs * dt_out))
+    pos = {"lo": s0 - 1, "head_first": s0, "head_last": s0 + L - 2, "fir_history": s0 - 3}[which]
+    x[2, pos] = np.nan
+    x[4, pos] = -np.inf
+    y, ref, sched2 = _run(x, fs, dt_out, P, B, "tc", off_ns=off)
+    assert _run.last_kernel == "mfma_runs"
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched2):
+        yy = y[:, oa:ob]
+        assert np.array_equal(np.isnan(yy), np.isnan(r)), (which, a, b)
+        m = ~np.isnan(r)
+        assert _relrms(yy[m], r[m]) < 1e-4
