@@ -130,19 +130,20 @@ def time_plan(plan, x, y, wsb, stream, steps, warmup, barrier=None):
     import torch
     from lfdas.plan import set_timing
     barrier = barrier or (lambda: torch.cuda.synchronize(x.device))
-    set_timing(True)
+    # a ring of `steps` event triples: the timed steps are queued back to
+    # back with no host synchronisation between them (a per-step event sync
+    # left the GPU idle while the host launched the next step: 0.16 ms of a
+    # 2 ms step on a 1,250-channel shard)
+    set_timing(True, ring=max(2, steps))
     for _ in range(warmup):
         plan.execute(x, y, wsb, stream)
     barrier()
-    k1, sc = [], []
     t_a = time.perf_counter()
     for _ in range(steps):
         plan.execute(x, y, wsb, stream)
-        a, b = plan.last_timing_ms()  # syncs on this step's events
-        k1.append(a)
-        sc.append(b)
     barrier()
     el = time.perf_counter() - t_a
+    k1, sc = plan.timings_ms(steps)
     set_timing(False)
     return el, k1, sc
 
@@ -662,6 +663,20 @@ def main():
             dev, 10_000, 1000.0, 3600.0, 10.0, 120, 6,
             label="10,000 ch x 1 h @ 1 kHz (144 GB), dt = 10 s (the batch notebook's d_t), P = 120, B = 6: "
                   "R = 10,000 as 20 sub-blocks of 500")
+    if ws == 1 and not args.no_extra:
+        # strong-scaling proxy on one GPU: the channel shard one rank of an
+        # N-GPU run owns, timed alone (the driver's SCALE run is the record)
+        shards = {}
+        for n_gpu in (2, 4, 8):
+            c = -(-args.channels // n_gpu)
+            r = bench_lowpass_line(dev, c, args.fs, args.seconds, args.dt_out, args.patch_size, args.edge_buff,
+                                   steps=5, label=f"{c:,}-channel shard of cfg3 ({n_gpu} GPUs)")
+            shards[f"n{n_gpu}"] = {"channels": c, "ms_per_step": r["ms_per_step"],
+                                   "kernel_ms": r["roofline"]["kernel_ms"],
+                                   "scan_kernel_ms": r["roofline"]["scan_kernel_ms"],
+                                   "roofline_frac": r["roofline"]["frac"],
+                                   "projected_efficiency": (el / args.steps * 1e3 / n_gpu) / r["ms_per_step"]}
+        secondary["shard_widths_1gpu"] = shards
     if ws == 1 and not args.no_extra:
         secondary["fullrate_bandpass"] = bench_fullrate(dev)
     if not args.no_rolling and ws == 1:

@@ -92,7 +92,14 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *plan, const float *x,
  * with HIP events when enabled by lfd_set_timing(1). */
 int lfd_lowpass_last_timing(const lfd_lowpass_plan *plan, float *ms_blocks,
                             float *ms_scan);
+/* With lfd_set_timing(n), n > 1: the device times of the last n timed
+ * executes of this plan, oldest first (a ring of n event triples, so timed
+ * executes need no host synchronisation between them; bench.py). */
+int lfd_lowpass_timings(const lfd_lowpass_plan *plan, float *ms_blocks,
+                        float *ms_scan, int64_t n);
 void lfd_lowpass_plan_destroy(lfd_lowpass_plan *plan);
+/* 0: off; 1: time every execute / push / full-rate call; n > 1: also keep
+ * the last n low-pass executes' times per plan (lfd_lowpass_timings). */
 int lfd_set_timing(int enable);
 /* Which block-functional kernel the last execute ran: LFD_K1_MFMA (fp64
  * matrix cores over the plan's block taps; time-contiguous float32 rows,

@@ -655,6 +655,11 @@ struct lfd_lowpass_plan {
   int64_t sf_blocks = 0, tp_len = 0;
   size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // lfd_set_timing(n > 1): a ring of n event triples, so n timed executes
+  // need no host synchronisation between them (lfd_lowpass_timings)
+  mutable std::vector<hipEvent_t> ring;
+  mutable int64_t n_exec = 0;
+  mutable int last_ring = 0;  // ring size of the last timed execute (0: ev)
   mutable bool timed = false;
   mutable int last_k1 = 0;
 };
@@ -671,7 +676,7 @@ int lfd_device_count(int *count) {
 }
 
 int lfd_set_timing(int enable) {
-  g_timing.store(enable ? 1 : 0);
+  g_timing.store(enable > 0 ? enable : 0);
   return LFD_OK;
 }
 
@@ -1003,9 +1008,25 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   double *F = reinterpret_cast<double *>(ws + p->off_F);
   double *SF = reinterpret_cast<double *>(ws + p->off_SF);
   double *TP = reinterpret_cast<double *>(ws + p->off_TP);
-  const bool timed = g_timing.load() != 0;
+  const int ring_n = g_timing.load();
+  const bool timed = ring_n != 0;
   p->timed = timed;
-  if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
+  hipEvent_t *ev = const_cast<hipEvent_t *>(p->ev);
+  if (timed) {
+    if (ring_n > 1) {
+      if ((int)p->ring.size() < 3 * ring_n) {
+        for (int i = (int)p->ring.size(); i < 3 * ring_n; ++i) {
+          hipEvent_t e = nullptr;
+          LFD_HIP(hipEventCreate(&e));
+          p->ring.push_back(e);
+        }
+      }
+      ev = p->ring.data() + 3 * (p->n_exec % ring_n);
+    }
+    ++p->n_exec;
+    p->last_ring = ring_n > 1 ? ring_n : 0;
+    LFD_HIP(hipEventRecord(ev[0], st));
+  }
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
   const bool rec = env_flag("LFD_K1_REC");
   const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
@@ -1036,34 +1057,52 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
         LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
       LFD_HIP(lfd::launch_fold_runs(F, p->bg, rg, Y0, AG, st));
     }
-    if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
+    if (timed) LFD_HIP(hipEventRecord(ev[1], st));
     LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks, p->n_chunks, Y0,
                                         AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st,
                                         reinterpret_cast<double *>(ws + p->off_TR),
                                         reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk));
-    if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
+    if (timed) LFD_HIP(hipEventRecord(ev[2], st));
     return LFD_OK;
   }
   if (mfma)
     LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, F, st));
   else
     LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
-  if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
+  if (timed) LFD_HIP(hipEventRecord(ev[1], st));
   LFD_HIP(lfd::launch_chunk_scan(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
                                  p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st));
-  if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
+  if (timed) LFD_HIP(hipEventRecord(ev[2], st));
   return LFD_OK;
 }
 
 int lfd_lowpass_last_timing(const lfd_lowpass_plan *p, float *ms_blocks, float *ms_scan) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
   if (!p->timed) return fail(LFD_EINVAL, "timing was not enabled for the last execute");
-  LFD_HIP(hipEventSynchronize(p->ev[2]));
+  hipEvent_t *ev = p->last_ring > 1 ? p->ring.data() + 3 * ((p->n_exec - 1) % p->last_ring)
+                                    : const_cast<hipEvent_t *>(p->ev);
+  LFD_HIP(hipEventSynchronize(ev[2]));
   float a = 0, b = 0;
-  LFD_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
-  LFD_HIP(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
+  LFD_HIP(hipEventElapsedTime(&a, ev[0], ev[1]));
+  LFD_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
   if (ms_blocks) *ms_blocks = a;
   if (ms_scan) *ms_scan = b;
+  return LFD_OK;
+}
+
+int lfd_lowpass_timings(const lfd_lowpass_plan *p, float *ms_blocks, float *ms_scan, int64_t n) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (!p->timed || p->last_ring < 2) return fail(LFD_EINVAL, "the last execute was not timed with a ring (lfd_set_timing(n > 1))");
+  if (n < 1 || n > p->last_ring || n > p->n_exec) return fail(LFD_EINVAL, "n must be in [1, ring size] and <= timed executes");
+  LFD_HIP(hipEventSynchronize(p->ring[3 * ((p->n_exec - 1) % p->last_ring) + 2]));
+  for (int64_t i = 0; i < n; ++i) {
+    const hipEvent_t *ev = p->ring.data() + 3 * ((p->n_exec - n + i) % p->last_ring);
+    float a = 0, b = 0;
+    LFD_HIP(hipEventElapsedTime(&a, ev[0], ev[1]));
+    LFD_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
+    if (ms_blocks) ms_blocks[i] = a;
+    if (ms_scan) ms_scan[i] = b;
+  }
   return LFD_OK;
 }
 
@@ -1130,6 +1169,8 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
                   (void *)p->d_slot_chunk})
     if (d) (void)hipFree(d);
   for (auto &e : p->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &e : p->ring)
     if (e) (void)hipEventDestroy(e);
   delete p;
 }

@@ -123,6 +123,14 @@ class LowpassPlan:
         check(self._lib.lfd_lowpass_last_timing(self._h, ctypes.byref(a), ctypes.byref(b)))
         return float(a.value), float(b.value)
 
+    def timings_ms(self, n: int):
+        """(K1 ms, scan ms) lists of the last ``n`` executes timed with
+        ``set_timing(ring=n)`` (no host synchronisation between them)."""
+        a = np.zeros(n, np.float32)
+        b = np.zeros(n, np.float32)
+        check(self._lib.lfd_lowpass_timings(self._h, a.ctypes.data, b.ctypes.data, int(n)))
+        return [float(v) for v in a], [float(v) for v in b]
+
     def last_kernel(self) -> str:
         """Block-functional kernel of the last execute: "mfma_runs" (MFMA +
         run folding), "mfma_runs_tm" (the same for (time, channel) rows),
@@ -170,8 +178,10 @@ class LowpassPlan:
         return bc[0], sc[0], cg
 
 
-def set_timing(enable: bool):
-    check(load().lfd_set_timing(1 if enable else 0))
+def set_timing(enable: bool, ring: int = 1):
+    """HIP-event timing of executes; ``ring`` > 1 keeps the last ``ring``
+    executes' times per plan (``LowpassPlan.timings_ms``)."""
+    check(load().lfd_set_timing(max(1, int(ring)) if enable else 0))
 
 
 def device_count() -> int:
