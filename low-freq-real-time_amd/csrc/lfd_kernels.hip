@@ -2512,7 +2512,24 @@ __device__ __forceinline__ void tm_iter4(const double *const (&kt)[3], int off, 
   }
 }
 
-template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false>
+// BUF (with X2): interior loads as buffer loads — one descriptor per
+// iteration at the wave-uniform row base, the 16 row offsets (16j + e) s_t
+// in SGPRs (soffset), the lane's part in voffset — instead of 16 64-bit
+// wave-uniform row pointers per iteration
+__device__ __forceinline__ void tm_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t offp, const int (&soff)[16],
+                                            TmIter &b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, offp, soff[4 * j + e], 0);
+      const float2 f = __builtin_bit_cast(float2, v);
+      b.p[j][e] = f.x;
+      b.q[j][e] = f.y;
+    }
+}
+
+template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false, bool BUF = false>
 __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
@@ -2683,9 +2700,23 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
       }
     };
     TmIter buf[TM_PF + 1];
+    int soff[16];
+    const int nrec = (int)(64 * s_t * 4 + 256);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) soff[k] = (int)((16 * (k >> 2) + (k & 3)) * s_t * 4);
+    auto load_it = [&](TmIter &b) {
+      if constexpr (BUF) {
+        const float *rowp = x + uniform64(c0 + (sp + 64 * itp) * s_t);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(rowp), (short)0, nrec, 0x00020000);
+        tm_load_buf(rs, offp, soff, b);
+      } else {
+        tm_load_u<SWAP, NTILE, X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, b);
+      }
+    };
 #pragma unroll
     for (int d = 0; d < TM_PF; ++d) {
-      tm_load_u<SWAP, NTILE, X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[d]);
+      load_it(buf[d]);
       produce();
     }
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
@@ -2695,7 +2726,7 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
       for (int u = 0; u <= TM_PF; ++u) {
         constexpr int NB = TM_PF + 1;
         const int lb = (u + TM_PF) % NB;
-        tm_load_u<SWAP, NTILE, X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, buf[lb]);
+        load_it(buf[lb]);
         produce();
         // a run's first and last iteration need the finite mask (chunk
         // boundaries are run boundaries)
@@ -2787,7 +2818,18 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
     if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true>, 512);
     return hipErrorInvalidValue;
   }
+  // buffer loads at prefetch depth 1: 14.01 vs 14.18 ms on cfg3 stored
+  // time-major (in-process A/B, tools/ab_plan.py --tm; bit-identical)
+  bool buf = !std::getenv("LFD_TM_PF") && !std::getenv("LFD_TM_NT");
+  if (const char *v = std::getenv("LFD_TM_BUF")) buf = std::atoi(v) != 0;
+  if (buf && x2 && !swap && ntile == 2 && !m4 && s_t < (int64_t)1 << 22) {
+    const int pfb = std::getenv("LFD_TM_PF") ? pf : 1;
+    if (nt == 512 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true>, 512);
+    if (nt == 512 && pfb == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true>, 512);
+    return hipErrorInvalidValue;
+  }
   if (x2 && !swap && ntile == 2) {
+    if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, false, 2, true>, 768);
     if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, 512);
     if (nt == 512 && pf == 3) return go(&k_block_runs_mfma_tm<3, 512, false, 2, true>, 512);
     if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true>, 512);
