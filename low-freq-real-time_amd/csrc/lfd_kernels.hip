@@ -2122,7 +2122,10 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 // MINW: minimum waves per SIMD the register allocation must allow (0: the
 // compiler's choice; 144 VGPRs at PF 2 / 512 threads = 3 waves per SIMD,
 // fewer than the 4 that two workgroups' LDS allow)
-template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0>
+// BUFL: interior sample loads as buffer loads (descriptor at the wave-uniform
+// row base of the channel group, a constant 32-bit voffset per lane) instead
+// of a 64-bit pointer per lane and iteration (fewer VGPRs under MINW)
+template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -2281,6 +2284,10 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     int64_t kp = ka, sp = s;
     int itp = 0;
     const float *pp = addr(sp, itp);
+    // (BUFL) the channel group's row base + this lane's constant offset
+    const float *xg = x + uniform64(cg * 16 * s_ch);
+    const uint32_t voff = (uint32_t)(4 * ((xr - xg) + 4 * q));
+    const int nrec = (int)(4 * (16 * s_ch + 64));
     auto produce = [&]() {
       if (kp == kb - 1 && itp == nit - 1) return;
       if (++itp == nit) {
@@ -2288,13 +2295,25 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
         ++kp;
         sp += L;
       }
-      pp = addr(sp, itp);
+      if (!BUFL) pp = addr(sp, itp);
+    };
+    auto load_iter = [&](f4v (&b)[4]) {
+      if constexpr (BUFL) {
+        const float *ub = xg + uniform64((sp & ~(int64_t)3) + 64 * itp);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(ub), (short)0, nrec, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          b[j] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 64 * j, 0));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
+      }
     };
     f4v buf[PF + 1][4];
 #pragma unroll
     for (int d = 0; d < PF; ++d) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) buf[d][j] = ldx4(pp + 16 * j);
+      load_iter(buf[d]);
       produce();
     }
     const double *kt = table(s);
@@ -2307,8 +2326,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       for (int u = 0; u <= PF; ++u) {
         constexpr int NB = PF + 1;
         const int lb = (u + PF) % NB;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) buf[lb][j] = ldx4(pp + 16 * j);
+        load_iter(buf[lb]);
         produce();
         if (MODE == 1) {
 #pragma unroll
@@ -2921,7 +2939,7 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   return hipGetLastError();
 }
 
-template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0>
+template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
@@ -2931,13 +2949,14 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, M4, MINW>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
+    hipError_t e =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_block_runs_mfma<PF, MODE, NT, M4, MINW><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0,
-                                                                             AG);
+  k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg,
+                                                                                   Y0, AG);
   return hipGetLastError();
 }
 
@@ -2977,6 +2996,13 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   if (const char *v = std::getenv("LFD_RUN_M4")) m4 = std::atoi(v) != 0;
   int minw = 4;  // LFD_RUN_MINW=0: the compiler's register allocation
   if (const char *v = std::getenv("LFD_RUN_MINW")) minw = std::atoi(v);
+  bool bufl = false;  // LFD_RUN_BUF=1: buffer loads (A/B knob)
+  if (const char *v = std::getenv("LFD_RUN_BUF")) bufl = std::atoi(v) != 0;
+  if (bufl && 16 * s_ch + 64 < ((int64_t)1 << 29) && mode == 0 && nt == 512 && minw == 4 && !m4) {
+    if (pf == 2) return run_k1<2, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (pf == 1) return run_k1<1, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    return hipErrorInvalidValue;
+  }
   if (minw == 4 && mode == 0 && nt == 512) {
     if (m4 && pf == 2) return run_k1<2, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     if (m4 && pf == 1) return run_k1<1, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
