@@ -1369,6 +1369,36 @@ __global__ __launch_bounds__(256) void k_interp_linear(
 // ---------------------------------------------------------------------------
 // Rolling mean
 // ---------------------------------------------------------------------------
+// One DPP step on a double (both 32-bit halves; lanes without a source, or
+// in rows the mask leaves out, read 0.0).  dpp_ctrl: row_shr:n = 0x110 + n,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143 (GFX9 encodings).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROW_MASK, 0xf, false);
+  const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROW_MASK, 0xf, false);
+  return __hiloint2double(h2, l2);
+}
+
+// Inclusive wave scan of a double over the 64 lanes on DPP (VALU lane
+// moves, no LDS round trips): Kogge-Stone inside each 16-lane row, then the
+// row totals broadcast forward (row_bcast:15 into rows 1 and 3, row_bcast:31
+// into rows 2 and 3).
+__device__ __forceinline__ double wave_incl_scan_dpp(double v) {
+  v += dpp_d<0x111, 0xf>(v);
+  v += dpp_d<0x112, 0xf>(v);
+  v += dpp_d<0x114, 0xf>(v);
+  v += dpp_d<0x118, 0xf>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  return v;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l), hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1574,7 +1604,7 @@ constexpr int RS_ROW = RS_E + 4;    // padded LDS row (floats): conflict-free ds
 template <bool VEC, int STAGE, int NPF = 1, int MINW = 3, bool RING = false>
 __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
-    float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out, int ring_mask) {
+    float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out, int ring_mask, bool scan_dpp) {
   // positions are row-relative int32 (the launcher checks n_t < 2^31 - 1024)
   __shared__ __attribute__((aligned(16))) float lds_all[(STAGE & 3) ? 4 : 1][(STAGE & 1) ? 2 : 1]
                                                        [(STAGE & 3) ? 64 * RS_ROW : 4];
@@ -1757,13 +1787,17 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         for (int e = 1; e < RS_E; ++e) d[e] += d[e - 1];
       }
       double v = d[RS_E - 1];
+      if (scan_dpp) {
+        v = wave_incl_scan_dpp(v);
+      } else {
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double w_ = __shfl_up(v, o, 64);
-        if (lane >= o) v += w_;
+        for (int o = 1; o < 64; o <<= 1) {
+          const double w_ = __shfl_up(v, o, 64);
+          if (lane >= o) v += w_;
+        }
       }
       const double excl = carry + (v - d[RS_E - 1]);
-      const double tot = __shfl(v, 63, 64);
+      const double tot = readlane_d(v, 63);
       float o8[RS_E];
 #pragma unroll
       for (int e = 0; e < RS_E; ++e) o8[e] = (float)((excl + d[e]) * inv_w);
@@ -3405,6 +3439,9 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     int npf = 1, minw = 3;
     if (const char *v = std::getenv("LFD_ROLL_PF")) npf = std::atoi(v);
     if (const char *v = std::getenv("LFD_ROLL_MINW")) minw = std::atoi(v);
+    // the per-step wave scan on DPP lane moves (A/B knob LFD_ROLL_DPP=0: shuffles)
+    bool dpp = true;
+    if (const char *v = std::getenv("LFD_ROLL_DPP")) dpp = std::atoi(v) != 0;
     // LDS ring for x[t - W] (vector rows, W + 512 <= 4096): A/B knob LFD_ROLL_RING
     int ring = 0;
     while (ring < W + RS_P) ring = ring ? 2 * ring : 1024;
@@ -3419,20 +3456,20 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
         attr = true;
       }
       k_rolling_scan_tc<true, 2, 1, 3, true><<<(unsigned)blocks, 256, sizeof(float) * 4 * ring, st>>>(
-          x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, ys_t, (int)seg_out, vec_out, ring - 1);
+          x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, ys_t, (int)seg_out, vec_out, ring - 1, dpp);
       return hipGetLastError();
     }
 #define LFD_ROLL(V, ST, PF_)                                                                                    \
   k_rolling_scan_tc<V, ST, PF_><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y, ys_ch, \
-                                                             ys_t, (int)seg_out, V && vec_out, 0)
+                                                             ys_t, (int)seg_out, V && vec_out, 0, dpp)
     if (!vec)
       LFD_ROLL(false, 0, 1);
     else if (stage == 2 && npf == 1 && minw == 4)
       k_rolling_scan_tc<true, 2, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
-                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0);
+                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0, dpp);
     else if (stage == 2 && npf == 2 && minw == 4)
       k_rolling_scan_tc<true, 2, 2, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
-                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0);
+                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0, dpp);
     else if (stage == 2 && npf == 2)
       LFD_ROLL(true, 2, 2);
     else if (stage == 2 && npf == 3)
