@@ -872,9 +872,20 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
         blocks_all / 4096 >= 32
             ? std::max<int64_t>(std::min(unit_min, unit_cap), std::min<int64_t>(unit_cap, blocks_all / (16 * 4096)))
             : std::max<int64_t>(lfd::RUN_R, std::min<int64_t>(unit_cap, blocks_all / 4096));
+    // Tail: units are dispatched time-group-major (unit = channel group +
+    // n_cg x time group), so the last ~2 rounds of units (2 x 4,096 waves)
+    // are the last time groups; making those one run long shortens the
+    // kernel's drain, where a few waves each stream alone (LFD_RUN_TAIL=0:
+    // off)
+    const int64_t n_cg = (n_ch + 15) / 16;
+    int64_t tail_blocks = std::min<int64_t>(p->bg.nb / 4, 2 * ((4096 + n_cg - 1) / n_cg) * lfd::RUN_R);
+    if (const char *v = std::getenv("LFD_RUN_TAIL")) tail_blocks = std::atoi(v) ? tail_blocks : 0;
+    if (unit_blocks <= lfd::RUN_R) tail_blocks = 0;
+    const int64_t tail_k = p->bg.nb - tail_blocks;  // runs starting at or after this block
     int acc = 0;
     for (int64_t r = 0; r < n_runs; ++r) {
-      if (r == 0 || acc + p->run_len[r] > unit_blocks) {
+      const int64_t cap = p->run_ks[r] >= tail_k ? lfd::RUN_R : unit_blocks;
+      if (r == 0 || acc + p->run_len[r] > cap || (p->run_ks[r] >= tail_k && acc > 0)) {
         p->group_r0.push_back((int)r);
         acc = 0;
       }

@@ -8,8 +8,9 @@ case "$1" in
   k1)      # K1 launch configuration (profiles/r02_ab_k1_minw.txt, r02_ab_k1_diag.txt)
     timeout -k 10 400 python tools/ab_plan.py --reps 5 "" "LFD_RUN_MINW=0 LFD_RUN_PF=2" "LFD_RUN_M4=1" \
         "LFD_RUN_BUF=1" "LFD_NO_RUNS=1 LFD_MF_MODE=3" ;;
-  units)   # K1 unit size at a 1,250-channel shard (plan-time knob: --replan)
-    timeout -k 10 300 python tools/ab_plan.py --replan --ch 1250 --reps 3 "" "LFD_RUN_UNIT=8" "LFD_RUN_UNIT=32" ;;
+  units)   # K1 unit size at a 1,250-channel shard, one-run tail units (plan-time knobs: --replan)
+    timeout -k 10 300 python tools/ab_plan.py --replan --ch 1250 --reps 3 "" "LFD_RUN_UNIT=8" "LFD_RUN_UNIT=32" &&
+    timeout -k 10 300 python tools/ab_plan.py --replan --reps 4 "" "LFD_RUN_TAIL=0" ;;
   scan)    # deferred-output scan by width (DESIGN §2 k_chunk_scan)
     for c in 1250 2500 5000 10000; do
       timeout -k 10 200 python tools/ab_plan.py --ch $c --reps 3 "" "LFD_SCAN_DEFER=0" "LFD_SCAN_DEFER=1" || exit 1
