@@ -213,3 +213,48 @@ def test_cfg4_edge_full_width_sampled_channels():
         assert g.shape == want.shape
         if want.size:
             assert _rel(g, want) < 1e-4
+
+
+@pytest.mark.parametrize("variant", ["time_major", "off_sample"])
+def test_cfg3_full_size_layouts_sampled_channels(variant):
+    """cfg3 at full size through the other two production K1 paths: stored
+    (time, channel) like the real files (k_block_runs_mfma_tm, channel-pair
+    buffer loads) and an archive whose samples start 1.9 ms after the output
+    grid's second (blended output functional + scan head skip).  Sampled
+    channels against the oracle (relRMS <= 1e-4, identical output times), no
+    NaN in any produced output."""
+    import torch
+
+    import bench
+    n_ch, n, fs = 10_000, 1_800_000, 500.0
+    off = 1_900_000 if variant == "off_sample" else 0
+    plan, sched, sos, t0, dt_ns, tg = bench.build_plan(n_ch, n, fs, 1.0, 600, 7, off)
+    if variant == "time_major":
+        xs_t = torch.empty((n, n_ch), dtype=torch.float32, device="cuda")
+        bench.synth_fill_time_major(xs_t, fs, 11)
+        x = xs_t.t()
+    else:
+        x = torch.empty((n_ch, n), dtype=torch.float32, device="cuda")
+        bench.synth_fill(x, fs, 11)
+    y = torch.full((n_ch, plan.n_grid), float("nan"), dtype=torch.float32, device="cuda")
+    ws = plan.alloc_workspace()
+    plan.execute(x, y, ws)
+    torch.cuda.synchronize()
+    assert plan.last_kernel() == ("mfma_runs_tm" if variant == "time_major" else "mfma_runs")
+    rows = [0, 1, 31, 32, 5001, 9998, 9999]
+    xs = x[rows].cpu().numpy()
+    ys = y[rows].cpu().numpy()
+    ref = oracle.lfproc_process(xs, t0, dt_ns, tg[0], tg[-1] + 1, 1.0, 600, 7)
+    assert len(ref) == len(sched)
+    for (tt, r), (_, _, oa, ob) in zip(ref, sched):
+        np.testing.assert_array_equal(tt, tg[oa:ob])
+    got = np.concatenate([ys[:, oa:ob] for _, _, oa, ob in sched], axis=1)
+    want = np.concatenate([r for _, r in ref], axis=1)
+    assert got.shape == want.shape
+    assert _rel(got, want) < 1e-4
+    produced = np.zeros(plan.n_grid, bool)
+    for _, _, oa, ob in sched:
+        produced[oa:ob] = True
+    assert not torch.isnan(y[:, torch.as_tensor(produced, device="cuda")]).any()
+    del x, y, ws
+    torch.cuda.empty_cache()
