@@ -3273,8 +3273,10 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   // deferred outputs (k_run_outputs) when the scan has few (chunk, channel)
   // threads and is latency-bound: 1,250 ch x 7 chunks (an 8-GPU shard of
   // cfg3) 0.247 -> 0.152 ms, 2,500 ch 0.263 -> 0.191, 5,000 ch equal, 10,000
-  // ch 0.339 -> 0.431 (the TR round trip); A/B knob LFD_SCAN_DEFER=0/1
-  bool defer = n_chunks * g.n_ch < 40000;
+  // ch 0.339 -> 0.431 (the TR round trip); and when the chunks hold long
+  // run chains (dt = 10 s at 1 kHz: ~300 runs per chunk, 0.79 -> 0.67 ms);
+  // A/B knob LFD_SCAN_DEFER=0/1
+  bool defer = n_chunks * g.n_ch < 40000 || rg.n_sr >= 128 * n_chunks;
   if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
   if (TR && CR && slot_chunk && defer) {
     const unsigned nb = nblk(n_chunks * g.n_ch, 256);
