@@ -878,10 +878,11 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
     // kernel's drain, where a few waves each stream alone (LFD_RUN_TAIL=0:
     // off)
     const int64_t n_cg = (n_ch + 15) / 16;
-    int64_t tail_blocks = std::min<int64_t>(p->bg.nb / 4, 2 * ((4096 + n_cg - 1) / n_cg) * lfd::RUN_R);
-    if (const char *v = std::getenv("LFD_RUN_TAIL")) tail_blocks = std::atoi(v) ? tail_blocks : 0;
-    if (unit_blocks <= lfd::RUN_R) tail_blocks = 0;
-    const int64_t tail_k = p->bg.nb - tail_blocks;  // runs starting at or after this block
+    int64_t tail_rounds = 2;  // LFD_RUN_TAIL=<rounds>, 0: off
+    if (const char *v = std::getenv("LFD_RUN_TAIL")) tail_rounds = std::max(0, std::atoi(v));
+    const int64_t tail_blocks =
+        std::min<int64_t>(p->bg.nb / 4, tail_rounds * ((4096 + n_cg - 1) / n_cg) * lfd::RUN_R);
+    const int64_t tail_k = unit_blocks <= lfd::RUN_R ? p->bg.nb : p->bg.nb - tail_blocks;  // runs starting at or after this block
     int acc = 0;
     for (int64_t r = 0; r < n_runs; ++r) {
       const int64_t cap = p->run_ks[r] >= tail_k ? lfd::RUN_R : unit_blocks;
