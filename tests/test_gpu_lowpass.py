@@ -188,7 +188,8 @@ def test_long_grid_spacing_runs_mfma(cfg, off_ns):
     assert (num / den) ** 0.5 < 1e-4
 
 
-@pytest.mark.parametrize("W,S_", [(1000, 1), (1000, 250), (1000, 1000), (1000, 3), (999, 7), (64, 1)])
+@pytest.mark.parametrize("W,S_", [(1000, 1), (1000, 250), (1000, 1000), (1000, 3), (999, 7), (64, 1),
+                                  (4000, 7)])  # W + 512 > 4096: x[t - W] re-read, no LDS ring
 def test_rolling_mean_window_step(W, S_):
     """Overlapping windows (step < window) run the running-sum scan kernel
     (every sample read once); step >= window sums each window directly."""
