@@ -17,13 +17,15 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from lfdas.plan import set_timing  # noqa: E402
 
+# (the default registers are capped for 4 waves per SIMD at depth 1; the
+# other depths run with the compiler's allocation, LFD_RUN_MINW=0)
 CFGS = {
     "base": {},
-    "pf1nt512": {"LFD_RUN_PF": "1", "LFD_RUN_NT": "512"},
-    "pf3nt512": {"LFD_RUN_PF": "3", "LFD_RUN_NT": "512"},
-    "pf4nt512": {"LFD_RUN_PF": "4", "LFD_RUN_NT": "512"},
+    "pf2nt512": {"LFD_RUN_PF": "2", "LFD_RUN_NT": "512", "LFD_RUN_MINW": "0"},
+    "pf3nt512": {"LFD_RUN_PF": "3", "LFD_RUN_NT": "512", "LFD_RUN_MINW": "0"},
+    "pf4nt512": {"LFD_RUN_PF": "4", "LFD_RUN_NT": "512", "LFD_RUN_MINW": "0"},
 }
-KNOBS = ("LFD_RUN_NT", "LFD_RUN_PF")
+KNOBS = ("LFD_RUN_NT", "LFD_RUN_PF", "LFD_RUN_MINW")
 
 n_ch, n = 10000, 1_800_000
 plan, *_ = bench.build_plan(n_ch, n, 500.0, 1.0, 600, 7)
