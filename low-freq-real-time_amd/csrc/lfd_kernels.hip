@@ -951,6 +951,12 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 // float4 reads conflict-free) and y leaves through LDS as row stores.
 // ---------------------------------------------------------------------------
 typedef double fr_d4v __attribute__((ext_vector_type(4)));
+#ifndef FRS_Q
+// k_fullrate_scan: big blocks per load batch (8: 0.83 ms vs 0.91 at 4 on the
+// 2,000 x 600,000 band-pass; a software-pipelined next batch spills and is
+// slower, profiles/r02_fullrate_scan_ab.txt)
+#define FRS_Q 8
+#endif
 #ifndef FR_WAVES
 #define FR_WAVES 4  // waves per SIMD the register budget targets (<= 128 VGPRs)
 #endif
@@ -1194,7 +1200,7 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
   // The walks below are latency-bound (one thread per channel): full batches
   // of Q blocks / B samples load before they are applied, the next batch's
   // loads in flight; the remainders run one step at a time.
-  constexpr int Q = 4, B = 8;
+  constexpr int Q = FRS_Q, B = 8;
   const double *PL = cPL, *MM = cMM;
   auto mv = [&](const double *P, const double (&v)[N], double (&o)[N], bool tri) {
     asm volatile("" ::: "memory");  // re-read P from LDS (hoisted, 2 x N*N doubles spill)
