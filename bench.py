@@ -9,7 +9,10 @@ One step = one pass of the hot path over the whole hour (7 overlapping chunks,
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--weak]
 
-N > 1 is launched by torch.distributed.run (one rank per GPU).  Default
+N > 1 runs one rank per GPU: under torch.distributed.run (the driver's
+form; WORLD_SIZE must equal --gpus), or ``python bench.py --gpus N`` starts
+that launcher itself as a child process (and fails, printing no line, when
+the node has fewer than N GPUs).  Default
 (strong scaling, the config's "channel-sharded at 1/2/4/8 GPUs"): the
 10,000 channels are split into contiguous blocks (lfdas.shard.channel_range),
 no data-path collective; ``value`` = all channel-samples / max-over-ranks
@@ -52,6 +55,9 @@ def _args():
     p.add_argument("--no-extra", action="store_true",
                    help="skip the extra low-pass lines (off-sample grid, 1 kHz dt = 10 s, time-major)")
     p.add_argument("--weak", action="store_true", help="every rank owns --channels channels (weak scaling)")
+    p.add_argument("--one-device", action="store_true",
+                   help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo collectives "
+                        "(the line is marked rehearsal; not a scaling measurement)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 PMC traffic summary (tools/pmc_summary.py) for roofline.traffic")
     return p.parse_args()
@@ -62,6 +68,41 @@ def _dist():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return ws, rank, local
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_or_check(args) -> int | None:
+    """``--gpus N`` without a launcher: start N rank processes with
+    torch.distributed.run as a CHILD process (before this process touches
+    the GPU: device_count() does not initialise HIP on this image) and return
+    its exit code.  Under a launcher (WORLD_SIZE set), refuse a world size
+    that differs from ``--gpus``.  None = this process is a rank: run."""
+    ws_env = os.environ.get("WORLD_SIZE")
+    if ws_env is not None:
+        if int(ws_env) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws_env} (launcher and flag disagree)",
+                  file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import torch
+    n_dev = torch.cuda.device_count()
+    if n_dev < args.gpus and not args.one_device:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {n_dev}; "
+              "not printing an N=1 line for an N>1 request", file=sys.stderr)
+        return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def synth_fill(x, fs, seed):
@@ -362,6 +403,112 @@ def bench_ooc_cfg5(dev, n_ch=50_000, seconds=3600.0, push_s=60.0):
     return out
 
 
+def bench_ooc_cfg5_sharded(dev, ws, rank, barrier, max_over_ranks, n_ch=50_000, seconds=3600.0,
+                           push_s=60.0):
+    """cfg5 across the ranks (BASELINE configs[4], "across 8xMI355X"):
+    every rank opens ``shard_stream`` on its channel block of the 50,000-ch
+    @ 200 Hz spool and pushes its rows of each full-width host block
+    (``push_rows``; only its own rows are touched and page-locked,
+    ``pin_rows``).  No data exchange: N independent host->HBM streams.
+    ``value`` = all ranks' channel-samples / max-over-ranks wall time,
+    outputs downloaded inside the timed loop; the first and last channel of
+    every rank are checked against the oracle afterwards (untimed).  Every
+    collective here runs on every rank whatever happened locally (a local
+    failure is agreed on, not left to hang the others)."""
+    import torch
+    from lfdas.plan import set_timing
+    from lfdas.shard import pin_rows, push_rows, shard_stream
+    fs = 200.0
+    push = int(push_s * fs)
+    n = int(seconds * fs)
+    n_push = n // push
+    dt_ns = int(1e9 / fs)
+    t0 = 1_679_464_800_000_000_000
+    t_end = t0 + (n - 1) * dt_ns
+    st, blocks, pins, err = None, [], [], None
+    try:
+        st, (c0, c1) = shard_stream(n_ch, dt_ns, output_sample_interval=10.0, process_patch_size=120,
+                                    edge_buff_size=6, mode="continuous", t_start=t0, t_end=t_end,
+                                    capacity=int(1300 * fs) + 2 * push, device=dev)
+        # full-width host blocks: virtual memory, only this rank's rows written
+        for i in range(2):
+            b = np.empty((n_ch, push), np.float32)
+            d = torch.empty((c1 - c0, push), dtype=torch.float32, device=dev)
+            synth_fill(d, fs, 777 + 100 * rank + i)
+            b[c0:c1] = d.cpu().numpy()
+            del d
+            pins.append(pin_rows(b, (c0, c1)))
+            blocks.append(b)
+        st.reserve(push)
+    except Exception as e:
+        err = e
+    if max_over_ranks(1.0 if err is not None else 0.0) > 0:  # also the start barrier
+        if st is not None:
+            st.close()
+        return {"error": repr(err) if err is not None else "setup failed on another rank"}
+    rows = [c0, c1 - 1]
+    ys, ts, n_out = [], [], 0
+    torch.cuda.synchronize(dev)
+    ta = time.perf_counter()
+    try:
+        set_timing(True)
+        for k in range(n_push):
+            o = push_rows(st, blocks[k % 2], (c0, c1), t0 + k * push * dt_ns)
+            n_out += o.n_out
+            if o.n_out:
+                y = st.fetch()
+                ys.append(y[[r - c0 for r in rows]].copy())
+                ts.append(o.times_ns)
+            else:
+                st.wait_copy()
+        o = st.flush()
+        n_out += o.n_out
+        if o.n_out:
+            ys.append(st.fetch()[[r - c0 for r in rows]].copy())
+            ts.append(o.times_ns)
+        st.synchronize()
+        el = time.perf_counter() - ta
+    except Exception as e:
+        err, el = e, float("inf")
+    finally:
+        set_timing(False)
+    st.close()
+    el_max = max_over_ranks(el)
+    rel, ok = float("inf"), 0.0
+    if err is None:
+        try:
+            xs = np.concatenate([blocks[k % 2][rows] for k in range(n_push)], axis=1)
+            sys.path.insert(0, ROOT)
+            import oracle
+            ref = oracle.lfproc_process(xs, t0, dt_ns, t0, t_end, 10.0, 120, 6)
+            want = np.concatenate([r for _, r in ref], axis=1)
+            got = np.concatenate(ys, axis=1) if ys else np.zeros((len(rows), 0))
+            times_ok = bool(np.array_equal(np.concatenate(ts) if ts else np.zeros(0, np.int64),
+                                           np.concatenate([t for t, _ in ref])))
+            if got.shape == want.shape:
+                rel = float(np.sqrt(np.sum((got.astype(np.float64) - want) ** 2) / np.sum(want ** 2)))
+            ok = 1.0 if (times_ok and rel < 1e-4) else 0.0
+        except Exception as e:
+            err = e
+    for p in pins:
+        p.release()
+    del blocks
+    all_ok = -max_over_ranks(-ok)  # min over ranks
+    worst = max_over_ranks(rel)
+    if err is not None or not np.isfinite(el_max):
+        return {"error": repr(err) if err is not None else "stream failed on another rank"}
+    samples = n_ch * n_push * push
+    return {"value": samples / el_max, "unit": "channel-samples/s", "n_gpus": ws,
+            "wall_s": el_max, "h2d_GBps_total": samples * 4 / el_max / 1e9,
+            "h2d_GBps_per_gpu": samples * 4 / el_max / 1e9 / ws, "channels_rank0": c1 - c0,
+            "outputs_per_channel": n_out, "scaling": "strong",
+            "config": f"{n_ch:,} ch @ 200 Hz, {seconds:.0f} s of the 24 h spool in {push_s:.0f} s pushes, "
+                      f"dt = 10 s, P = 120, B = 6, channel-sharded over {ws} GPUs (shard_stream + push_rows, "
+                      "each rank's rows page-locked in place); outputs downloaded inside the timed loop",
+            "check": {"rows_per_rank": "first and last channel", "worst_relrms_vs_oracle": worst,
+                      "pass": bool(all_ok > 0.5), "checker": "oracle.lfproc_process (untimed)"}}
+
+
 def bench_rolling(dev, W, S_, reps=10):
     """cfg2 rolling mean (5,000 ch x 10 min @ 1 kHz), window W, step S_;
     algorithmic bytes 4 + 4/S per channel-sample."""
@@ -527,6 +674,9 @@ def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48, backend="
 
 def main():
     args = _args()
+    rc = launch_or_check(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     ws, rank, local = _dist()
     n = int(args.seconds * args.fs)
@@ -560,9 +710,13 @@ def main():
             cpu["reference_lib"] = {"error": repr(e)}
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if ws > 1 else 0)
+        if args.one_device:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if ws > 1 and not args.one_device else 0)
+    comm_dev = torch.device("cpu") if args.one_device else dev
     torch.cuda.set_device(dev)
 
     from lfdas.shard import channel_range
@@ -588,10 +742,16 @@ def main():
     def max_over_ranks(v):
         if ws == 1:
             return v
-        tt = torch.tensor([v], device=dev, dtype=torch.float64)
+        tt = torch.tensor([v], device=comm_dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         return float(tt.item())
 
+    # every rank reports in over the data-path backend (RCCL for N > 1)
+    ranks_seen = 1
+    if ws > 1:
+        one = torch.ones(1, device=comm_dev, dtype=torch.int64)
+        torch.distributed.all_reduce(one)
+        ranks_seen = int(one.item())
     el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, args.steps, args.warmup, barrier)
     el = max_over_ranks(el)
     k1_kernel = plan.last_kernel()
@@ -621,7 +781,7 @@ def main():
             for i in range(4):
                 barrier()
                 t_g = time.perf_counter()
-                full = all_gather_channels(y, n_ch_total)
+                full = all_gather_channels(y.to(comm_dev), n_ch_total)
                 torch.cuda.synchronize(dev)
                 if i:
                     g_ms.append((time.perf_counter() - t_g) * 1e3)
@@ -650,6 +810,13 @@ def main():
             "scaling": "weak", "config": f"{args.channels:,} ch x 1 h @ 500 Hz per GPU x {ws} GPUs"}
         del xw, yw, ww
         plan_w.close()
+        torch.cuda.empty_cache()
+    if ws > 1 and not args.no_stream:
+        try:
+            secondary["out_of_core_cfg5_sharded"] = bench_ooc_cfg5_sharded(dev, ws, rank, barrier,
+                                                                           max_over_ranks)
+        except Exception as e:  # pragma: no cover - reported, never voids the headline line
+            secondary["out_of_core_cfg5_sharded"] = {"error": repr(e)}
         torch.cuda.empty_cache()
     if ws == 1 and not args.no_extra:
         secondary["cfg3_offsample_grid"] = bench_lowpass_line(
@@ -695,6 +862,7 @@ def main():
             "value": value,
             "unit": "channel-samples/s",
             "n_gpus": ws,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
@@ -710,6 +878,8 @@ def main():
                        "dt_out": args.dt_out, "chunks": len(sched),
                        "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),
                        "parallelism": f"channel-shard x{ws}", "io_dtype": "f32"},
+            **({"rehearsal": "--one-device: every rank on cuda:0 over gloo; not a scaling number"}
+               if args.one_device else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": K1_KERNELS.get(k1_kernel), "kernel_ms": k1,

@@ -312,6 +312,12 @@ void lfd_stream_close(lfd_stream *s);
 /* Pinned host memory for pushes (hipHostMalloc). */
 int lfd_host_alloc(void **p, size_t bytes);
 void lfd_host_free(void *p);
+/* Page-lock an existing host range (hipHostRegister), e.g. one rank's rows
+ * of a full-width host block that several ranks read (lfdas.shard.pin_rows,
+ * the cfg5 form of lf_das.py:236-240's per-chunk read across 8 GPUs); pushes
+ * from it are then DMA'd directly.  Unregister with the same start pointer. */
+int lfd_host_register(void *p, size_t bytes);
+int lfd_host_unregister(void *p);
 
 /* ------------------------------------------------------------------------
  * Post-processing of the decimated output (low_pass_dascore.ipynb cells

@@ -1217,28 +1217,34 @@ FrLayout fullrate_layout(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64
 
 // Per-(device, cascade) device constants, built on first use (the per-call
 // path then allocates nothing and never synchronises).
+// Entries are shared: a caller holds its entry while it launches, so an
+// eviction by another thread never frees a table under a running call (the
+// destructor's hipFree also waits for queued kernels to finish).
 struct FrEntry {
   int dev = -1, n_sec = 0;
   double sos[6 * MAX_SEC] = {0};
   lfd::FRConst *d_fc = nullptr;
+  ~FrEntry() {
+    if (d_fc) (void)hipFree(d_fc);
+  }
 };
 std::mutex g_fr_mu;
-std::vector<std::unique_ptr<FrEntry>> g_fr;
+std::vector<std::shared_ptr<FrEntry>> g_fr;
 // lfd_set_timing(1): events around the three launches of the last blocked call
 hipEvent_t g_fr_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 int g_fr_ev_dev = -1;
 bool g_fr_timed = false;
 
-int fullrate_entry(const double *sos, int n_sec, const Cascade &c, const FrEntry **out) {
+int fullrate_entry(const double *sos, int n_sec, const Cascade &c, std::shared_ptr<const FrEntry> *out) {
   int dev = 0;
   LFD_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_fr_mu);
   for (const auto &e : g_fr)
     if (e->dev == dev && e->n_sec == n_sec && std::memcmp(e->sos, sos, sizeof(double) * 6 * n_sec) == 0) {
-      *out = e.get();
+      *out = e;
       return LFD_OK;
     }
-  auto e = std::make_unique<FrEntry>();
+  auto e = std::make_shared<FrEntry>();
   e->dev = dev;
   e->n_sec = n_sec;
   std::memcpy(e->sos, sos, sizeof(double) * 6 * n_sec);
@@ -1246,16 +1252,11 @@ int fullrate_entry(const double *sos, int n_sec, const Cascade &c, const FrEntry
   fullrate_constants(c, *fc);
   LFD_HIP(hipMalloc(&e->d_fc, sizeof(lfd::FRConst)));
   const hipError_t he = hipMemcpy(e->d_fc, fc.get(), sizeof(lfd::FRConst), hipMemcpyHostToDevice);
-  if (he != hipSuccess) {
-    (void)hipFree(e->d_fc);
-    return fail(LFD_EHIP, std::string("full-rate constants: ") + hipGetErrorString(he));
-  }
-  if (g_fr.size() >= 16) {  // bounded: drop the oldest (hipFree waits for the device)
-    (void)hipFree(g_fr.front()->d_fc);
-    g_fr.erase(g_fr.begin());
-  }
-  g_fr.push_back(std::move(e));
-  *out = g_fr.back().get();
+  if (he != hipSuccess) return fail(LFD_EHIP, std::string("full-rate constants: ") + hipGetErrorString(he));
+  // bounded: drop the oldest from the cache (freed when its last user returns)
+  if (g_fr.size() >= 16) g_fr.erase(g_fr.begin());
+  g_fr.push_back(e);
+  *out = std::move(e);
   return LFD_OK;
 }
 }  // namespace
@@ -1298,7 +1299,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
   // one-thread-per-channel kernel
   const int64_t nb = fullrate_blocks(n_t);
   if (nb > 0 && !env_flag("LFD_FULLRATE_SERIAL")) {
-    const FrEntry *fe = nullptr;
+    std::shared_ptr<const FrEntry> fe;
     if (int e = fullrate_entry(sos, n_sec, c, &fe)) return e;
     const FrLayout lo = fullrate_layout(n_ch, n_t, padlen, n_sec, nb);
     char *ws = static_cast<char *>(workspace);
@@ -1319,6 +1320,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
       }
       g_fr_timed = true;
     } else {
+      std::lock_guard<std::mutex> lk(g_fr_mu);
       g_fr_timed = false;
     }
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[0], st));
@@ -1341,6 +1343,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
 }
 
 int lfd_sosfiltfilt_last_timing(float *ms_functionals, float *ms_scan, float *ms_output) {
+  std::lock_guard<std::mutex> lk(g_fr_mu);
   if (!g_fr_timed) return fail(LFD_EINVAL, "timing was not enabled for the last blocked full-rate call");
   LFD_HIP(hipEventSynchronize(g_fr_ev[3]));
   float a = 0, b = 0, c = 0;

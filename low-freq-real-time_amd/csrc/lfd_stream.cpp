@@ -686,4 +686,16 @@ void lfd_host_free(void *p) {
   if (p) (void)hipHostFree(p);
 }
 
+int lfd_host_register(void *p, size_t bytes) {
+  if (!p || !bytes) return fail(LFD_EINVAL, "lfd_host_register: empty range");
+  LFD_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return LFD_OK;
+}
+
+int lfd_host_unregister(void *p) {
+  if (!p) return fail(LFD_EINVAL, "lfd_host_unregister: p is NULL");
+  LFD_HIP(hipHostUnregister(p));
+  return LFD_OK;
+}
+
 }  // extern "C"

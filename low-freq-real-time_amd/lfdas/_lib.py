@@ -153,6 +153,8 @@ def load():
         "lfd_stream_close": ([vp], None),
         "lfd_host_alloc": ([P(vp), sz], i32),
         "lfd_host_free": ([vp], None),
+        "lfd_host_register": ([vp, sz], i32),
+        "lfd_host_unregister": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -173,7 +175,7 @@ EXPORTED = (
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
-    "lfd_host_alloc", "lfd_host_free", "lfd_demean_scale_f64", "lfd_median_filter_f64",
+    "lfd_host_alloc", "lfd_host_free", "lfd_host_register", "lfd_host_unregister", "lfd_demean_scale_f64", "lfd_median_filter_f64",
 )
 
 

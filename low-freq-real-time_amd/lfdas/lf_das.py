@@ -349,7 +349,34 @@ class LFProc:
         first = [p for p in plist if p.coords["time"][-1] >= ta][0]
         return n_ok, first
 
-    def _run_chunks(self, tg, sched, data_patch, dt):
+    def process_time_range_device(self, bgtime, edtime):
+        """``process_time_range`` without the host side: every chunk's
+        decimated outputs stay in HBM.  Returns ``(y, times_ns, counts)``:
+        ``y`` a float32 (channel, time) device tensor holding the chunks'
+        outputs side by side (``counts[i]`` columns each, output times
+        ``times_ns``), or None when the range is larger than the device
+        budget (the caller then uses ``process_time_range``, which streams).
+        The sharded driver gathers ``y`` over RCCL without a host round trip.
+        Raises the gap exception like the reference (lf_das.py:18) — before
+        anything is computed, as no output files are written here."""
+        dt = self._para["output_sample_interval"]
+        tg = S.time_grid(bgtime, edtime, dt)
+        sched, self._kinds = S.lfproc_chunks(len(tg), self._para["process_patch_size"],
+                                             self._para["edge_buff_size"], with_kind=True)
+        if self._resident_bytes(tg, sched) > self._budget():
+            return None
+        n_ok, merged = self._merged_span(tg, sched)
+        if n_ok < len(sched):
+            raise Exception("patch merge failed! Gap in data exists")
+        y, chunks = self._device_outputs(tg, sched, merged, dt)
+        g0, g1 = chunks[0][2], chunks[-1][3]
+        counts = [ob - oa for _, _, oa, ob in chunks]
+        return y[:, g0:g1], np.asarray(tg[g0:g1], np.int64), counts
+
+    def _device_outputs(self, tg, sched, data_patch, dt):
+        """Run ``sched``'s chunks over ``data_patch`` on the device: returns
+        (y, chunks) — y float32 (n_ch, len(tg)) in HBM (NaN outside the
+        chunks' outputs), chunks ``(s0, s1, oa, ob)`` per chunk."""
         import torch
 
         from .plan import LowpassPlan, filtfilt_resample_device
@@ -378,6 +405,10 @@ class LFProc:
             for s0, s1, oa, ob in chunks:
                 xs = x[:, s0:s1 + 1]
                 y[:, oa:ob] = filtfilt_resample_device(xs, sos, lo[oa:ob] - s0, w[oa:ob], padlen)
+        return y, chunks
+
+    def _run_chunks(self, tg, sched, data_patch, dt):
+        y, chunks = self._device_outputs(tg, sched, data_patch, dt)
         yh = y.cpu().numpy()
         tdim = data_patch.dims.index("time")
         for i, (s0, s1, oa, ob) in enumerate(chunks, start=1):

@@ -260,6 +260,15 @@ def fir_decimate_device(x, taps, q: int, delay: int, stream=None):
     n_ch, n_t = x.shape
     h = torch.as_tensor(np.ascontiguousarray(taps, dtype=np.float64)).to(x.device)
     y = torch.empty((n_ch, -(-n_t // int(q))), dtype=torch.float64, device=x.device)
+    if stream is not None:
+        # the taps were copied on torch's current stream and are freed on
+        # return: order the copy before the launch, and keep the memory from
+        # being reused before the kernel on `stream` has read it
+        ts = stream if hasattr(stream, "cuda_stream") else torch.cuda.ExternalStream(int(stream))
+        ts.wait_stream(torch.cuda.current_stream(x.device))
+        h.record_stream(ts)
+        y.record_stream(ts)
+    _count()
     check(load().lfd_fir_decimate_f32(_ptr(x), n_ch, n_t, x.stride(0), x.stride(1), _ptr(h), h.numel(),
                                       int(q), int(delay), _ptr(y), y.stride(0), y.stride(1),
                                       _stream_ptr(stream)))

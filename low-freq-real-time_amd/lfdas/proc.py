@@ -13,6 +13,8 @@ external)*, computed on the GPU by liblfdas.so:
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 
 from . import schedule as S
@@ -122,8 +124,9 @@ class ChunkGroup:
     def __init__(self, parent: Patch):
         self.parent = parent
         self.t_ns = parent.sample_times_ns()
-        self.pending = []
-        self.results = {}
+        # requests not computed yet, held weakly: a window output thrown
+        # away unread neither keeps its request alive nor joins a batch
+        self.pending = weakref.WeakSet()
 
     def window(self, start, stop) -> Patch:
         """Inclusive time window [start, stop] of the parent."""
@@ -136,17 +139,26 @@ class ChunkGroup:
 
     def request(self, window, sos, padlen, lo, w, dims, shape):
         req = _GroupResample(self, window, sos, padlen, lo, w, dims, shape)
-        self.pending.append(req)
+        self.pending.add(req)
         return req
 
     def _run(self, req):
-        batch = [r for r in self.pending
-                 if r.padlen == req.padlen and np.array_equal(r.sos, req.sos)]
-        self.pending = [r for r in self.pending if r not in batch]
+        """Compute ``req`` with every pending sibling of the same cascade.
+        Results are stored on the requests themselves (``_result``), and a
+        request leaves ``pending`` only once its result is set, so a failed
+        execute leaves the batch pending (the next read retries and raises
+        the real error) and a request shared by several patches
+        (``update_attrs`` copies) can be read any number of times."""
+        batch = [r for r in list(self.pending)
+                 if r._result is None and r.padlen == req.padlen and np.array_equal(r.sos, req.sos)]
+        if req not in batch:
+            batch.append(req)
         done = self._run_batched(batch) if len(batch) > 1 else False
         if not done:
             for r in batch:
-                self.results[r] = r.compute_alone()
+                r._result = r.compute_alone()
+        for r in batch:
+            self.pending.discard(r)
 
     def _run_batched(self, batch) -> bool:
         """One plan over the parent for every request of ``batch``; False
@@ -178,7 +190,7 @@ class ChunkGroup:
         yh = y.cpu().numpy()
         for r, (_, _, g0, g1) in zip(batch, chunks):
             seg = yh[:, g0:g1].astype(np.float64)
-            self.results[r] = seg.T.copy() if r.dims.index("time") == 0 else seg
+            r._result = seg.T.copy() if r.dims.index("time") == 0 else seg
         return True
 
 
@@ -199,6 +211,7 @@ class _GroupResample:
         self.w = np.asarray(w, np.float64)
         self.dims = tuple(dims)
         self.shape = tuple(shape)
+        self._result = None
 
     def compute_alone(self):
         from .plan import filtfilt_resample_device
@@ -207,9 +220,9 @@ class _GroupResample:
         return _from_ct(y, self.dims).astype(np.float64)
 
     def materialize(self, patch: Patch):
-        if self not in self.group.results:
+        if self._result is None:
             self.group._run(self)
-        return self.group.results.pop(self)
+        return self._result
 
 
 def interpolate(patch: Patch, kind="linear", **kwargs):

@@ -65,13 +65,42 @@ def shard_spool(sp, world: int, rank: int):
 
 
 def lfproc_shard(sub, bgtime, edtime, params, device=None):
-    """Default per-rank compute: LFProc.process_time_range on the rank's
-    sub-spool (device plan, no files) → its output patches in chunk order."""
+    """Default per-rank compute: LFProc on the rank's sub-spool (device plan,
+    no files).  Returns the chunks' outputs as ONE float32 (channel, time)
+    device tensor (``LFProc.process_time_range_device``), so the gather runs
+    HBM to HBM; a range too large for the device budget streams through
+    ``process_time_range`` and returns its output patches instead."""
     from .lf_das import LFProc
     lfp = LFProc(sub, device=device, verbose=False, write_files=False)
     lfp.update_processing_parameter(**params)
+    res = lfp.process_time_range_device(bgtime, edtime)
+    if res is not None:
+        return res[0]
     lfp.process_time_range(bgtime, edtime)
     return lfp.outputs
+
+
+def _shard_block(outs, counts, n_local, tdim):
+    """This rank's outputs as one (n_local, sum(counts)) tensor: a device
+    tensor from ``lfproc_shard`` as is (float32), output patches (an
+    injected ``run_shard``) side by side in their own dtype.  Raises on a
+    wrong chunk count or shape, so the error agreement covers it."""
+    import torch
+    total = int(sum(counts))
+    if isinstance(outs, torch.Tensor):
+        if tuple(outs.shape) != (n_local, total):
+            raise ValueError(f"shard output {tuple(outs.shape)} != {(n_local, total)}")
+        return outs
+    if len(outs) != len(counts):
+        raise ValueError(f"shard produced {len(outs)} chunks, the schedule has {len(counts)}")
+    parts = []
+    for out, cnt in zip(outs, counts):
+        d = np.asarray(out.data)
+        d = d.T if tdim == 0 else d
+        if d.shape != (n_local, cnt):
+            raise ValueError(f"shard chunk output {d.shape} != {(n_local, cnt)}")
+        parts.append(d)
+    return torch.from_numpy(np.ascontiguousarray(np.concatenate(parts, axis=1)))
 
 
 def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=None, group=None,
@@ -80,7 +109,9 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
     default process group: rank r processes channel block r (``shard_spool``)
     with ``run_shard(sub_spool, bgtime, edtime, params)`` (default
     ``lfproc_shard``: the device plan), the decimated outputs of every chunk
-    are all-gathered (RCCL on backend "nccl", gloo on CPU) and rank 0 writes
+    are all-gathered — float32 and HBM to HBM over RCCL on backend "nccl"
+    (one device→host copy of the gathered block after it), through host
+    memory on gloo — and rank 0 writes
     the reference's files (``LFDAS_<t0>_<t1>.h5``, lf_das.py:230-232) into
     ``output_folder``.  Returns the full-width output patches (every rank when
     ``gather``; else this rank's own block).  A failure on any rank (e.g. the
@@ -100,47 +131,50 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
     counts = [ob - oa for _, _, oa, ob in sched]
     sub, (c0, c1) = shard_spool(sp, world, rank)
     run_shard = run_shard or (lambda s, a, b, p: lfproc_shard(s, a, b, p, device))
-    outs, err = [], None
-    if sub is not None:
-        try:
-            outs = run_shard(sub, bgtime, edtime, params)
-        except Exception as e:  # re-raised below, after every rank agreed
-            err = e
-    if world > 1:
-        import torch.distributed as dist
-        flag = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device=_comm_device(group))
-        dist.all_reduce(flag, group=group)
-        if int(flag.item()):
-            raise err if err is not None else RuntimeError("process_time_range failed on another rank")
-    elif err is not None:
-        raise err
     p0 = sp[0]
     tdim = p0.dims.index("time")
     n_ch = len(np.asarray(p0.coords["distance"]))
     n_local = c1 - c0
-    # this rank's block, chunks side by side: (n_local, sum(counts)) float64
-    blk = np.zeros((n_local, sum(counts)), np.float64)
-    j = 0
-    for out, cnt in zip(outs, counts):
-        d = np.asarray(out.data, np.float64)
-        blk[:, j:j + cnt] = d.T if tdim == 0 else d
-        j += cnt
+    blk, err = None, None
+    try:
+        if sub is not None:
+            blk = _shard_block(run_shard(sub, bgtime, edtime, params), counts, n_local, tdim)
+        else:
+            blk = torch.zeros((0, sum(counts)), dtype=torch.float32)
+    except Exception as e:  # re-raised below, after every rank agreed
+        err = e
+    if world > 1:
+        import torch.distributed as dist
+        # one agreement for both: did any rank fail, and does any rank
+        # hold float64 outputs (an injected host compute) — every rank then
+        # gathers in that dtype
+        is64 = int(blk is not None and blk.dtype == torch.float64)
+        flag = torch.tensor([1 if err is not None else 0, is64], dtype=torch.int64, device=_comm_device(group))
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag[0].item()):
+            raise err if err is not None else RuntimeError("process_time_range failed on another rank")
+        dtype = torch.float64 if int(flag[1].item()) else torch.float32
+    elif err is not None:
+        raise err
+    else:
+        dtype = blk.dtype
     if world > 1 and gather:
-        t = torch.from_numpy(blk).to(_comm_device(group))
+        # HBM to HBM over RCCL (backend "nccl"); host tensors over gloo
+        t = blk.to(device=_comm_device(group), dtype=dtype)
         full = all_gather_channels(t, n_ch, group=group).cpu().numpy()
         dist_coords = np.asarray(p0.coords["distance"])
     else:
-        full = blk
+        full = blk.cpu().numpy()
         dist_coords = np.asarray(sub[0].coords["distance"]) if sub is not None else np.zeros(0)
     res = []
     j = 0
     attrs = p0._attrs_wo_coords()
     for i, ((_, _, oa, ob), cnt) in enumerate(zip(sched, counts), start=1):
-        seg = full[:, j:j + cnt]
+        seg = full[:, j:j + cnt].astype(np.float64)  # DASCore's output dtype
         coords = dict(p0.coords.coord_map)
         coords["distance"] = dist_coords
         coords["time"] = tg[oa:ob].astype("datetime64[ns]")
-        out = Patch(data=seg.T.copy() if tdim == 0 else seg.copy(), coords=coords, dims=p0.dims,
+        out = Patch(data=seg.T.copy() if tdim == 0 else seg, coords=coords, dims=p0.dims,
                     attrs=attrs).update_attrs(d_time=para["output_sample_interval"])
         res.append(out)
         if rank == 0 and output_folder and (world == 1 or gather):
@@ -172,6 +206,20 @@ def shard_stream(n_ch: int, sampling_interval_ns: int, group=None, **stream_kw):
     if c1 <= c0:
         return None, (c0, c1)
     return LowpassStream(c1 - c0, sampling_interval_ns, **stream_kw), (c0, c1)
+
+
+def pin_rows(block: np.ndarray, c_range):
+    """Page-lock rows [c0, c1) of a full-width (channel, time) host block in
+    place — this rank's part only, so N ranks that share one block's layout
+    pin (and touch) only their own rows — and return the registration
+    (``lfdas.stream.HostRegistration``; ``release()`` unpins).  Pushes of
+    those rows (``push_rows``) are then one direct DMA each."""
+    from .stream import register_host
+    c0, c1 = c_range
+    rows = block[c0:c1]
+    if not rows.flags.c_contiguous:
+        raise ValueError("pin_rows needs a C-contiguous (channel, time) block")
+    return register_host(rows)
 
 
 def push_rows(stream, block, c_range, t0, time_axis: int = 1):

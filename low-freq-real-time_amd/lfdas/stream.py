@@ -43,15 +43,28 @@ class StreamOutput:
         return self.t_first_ns + np.arange(self.n_out, dtype=np.int64) * self.t_step_ns
 
 
+# page-locked host ranges registered through ``register_host`` ([start, end))
+_REGISTERED: dict = {}
+
+
+def _in_registered(ptr: int, nbytes: int) -> bool:
+    return any(a <= ptr and ptr + nbytes <= b for a, b in _REGISTERED.values())
+
+
 def _is_pinned_host(a) -> bool:
-    """True for pinned host memory: a pinned torch tensor, or a numpy view of
-    a ``pinned_empty`` buffer."""
+    """True for pinned host memory: a pinned torch tensor, a numpy view of
+    a ``pinned_empty`` buffer, or an array inside a ``register_host`` range."""
     try:
         import torch
         if isinstance(a, torch.Tensor):
             return bool(a.is_pinned())
     except ImportError:  # pragma: no cover
         pass
+    if isinstance(a, np.ndarray) and _REGISTERED and a.size:
+        lo = a.ctypes.data + sum(min(0, st * (n - 1)) for st, n in zip(a.strides, a.shape))
+        hi = a.ctypes.data + sum(max(0, st * (n - 1)) for st, n in zip(a.strides, a.shape)) + a.itemsize
+        if _in_registered(lo, hi - lo):
+            return True
     b = a
     while b is not None:
         if getattr(b, "_lfd_owner", None) is not None:
@@ -289,6 +302,38 @@ def pinned_empty(shape, dtype=np.float32):
     # keep the owner alive with the buffer object
     buf._lfd_owner = arr_owner
     return arr
+
+
+class HostRegistration:
+    """A page-locked host range (``lfd_host_register``); ``release()`` (or
+    garbage collection) unregisters it.  Keeps the array alive meanwhile."""
+
+    def __init__(self, arr: np.ndarray):
+        if not (isinstance(arr, np.ndarray) and arr.flags.c_contiguous and arr.size):
+            raise ValueError("register_host needs a non-empty C-contiguous numpy array")
+        self._lib = load()
+        self.arr = arr
+        self.ptr = int(arr.ctypes.data)
+        check(self._lib.lfd_host_register(ctypes.c_void_p(self.ptr), arr.nbytes))
+        _REGISTERED[self.ptr] = (self.ptr, self.ptr + arr.nbytes)
+
+    def release(self):
+        if _REGISTERED.pop(self.ptr, None) is not None:
+            check(self._lib.lfd_host_unregister(ctypes.c_void_p(self.ptr)))
+            self.arr = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def register_host(arr: np.ndarray) -> HostRegistration:
+    """Page-lock an existing C-contiguous host array in place (e.g. one
+    rank's rows of a full-width block): pushes from it are DMA'd directly,
+    as from ``pinned_empty``."""
+    return HostRegistration(arr)
 
 
 def lfproc_schedule(n_grid: int, patch_size: int, buff_size: int):

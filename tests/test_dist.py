@@ -144,3 +144,89 @@ def test_gloo_world2_shard_and_gather():
         x, synth.T0_NS, 4_000_000, synth.T0_NS, synth.T0_NS + 6000 * 4_000_000, 0.2, 40, 6)], axis=1)
     np.testing.assert_array_equal(y, ref)
     assert sys.modules  # keep linters quiet
+
+
+def _stream_worker(rank, world, port, n_ch, push, n_push, out_q):
+    """One rank of the out-of-core cfg5 form (``shard_stream`` + ``push_rows``)
+    in dry-run mode: the rank's bookkeeping per push."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lfdas.shard import push_rows, shard_stream
+    st, rng = shard_stream(n_ch, 10_000_000, output_sample_interval=1.0, process_patch_size=40,
+                           edge_buff_size=5, mode="continuous", t_start=STREAM_T0,
+                           t_end=STREAM_T0 + (push * n_push - 1) * 10_000_000, dry_run=True)
+    rec = []
+    block = np.zeros((n_ch, push), np.float32)  # full-width host block
+    for k in range(n_push):
+        o = push_rows(st, block, rng, STREAM_T0 + k * push * 10_000_000)
+        rec.append((o.n_out, o.t_first_ns if o.n_out else 0, tuple(o.chunk_counts)))
+    o = st.flush()
+    rec.append((o.n_out, o.t_first_ns if o.n_out else 0, tuple(o.chunk_counts)))
+    # time-major full-width blocks go through the strided view of the rank's columns
+    st2, _ = shard_stream(n_ch, 10_000_000, output_sample_interval=1.0, process_patch_size=40,
+                          edge_buff_size=5, mode="edge", t_start=STREAM_T0, dry_run=True)
+    o2 = push_rows(st2, np.zeros((push, n_ch), np.float32), rng, STREAM_T0, time_axis=0)
+    out_q.put((rank, rng, st.n_ch, rec, o2.n_out))
+    st.close()
+    st2.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+STREAM_T0 = 1_679_464_800_000_000_000
+
+
+def test_gloo_world2_shard_stream_dry_run_matches_single_stream():
+    """cfg5 across GPUs (``shard_stream`` / ``push_rows``) on 2 gloo ranks in
+    dry-run mode: each rank's stream owns its ragged channel block (4 + 3 of
+    7) and produces per push exactly the outputs, times and chunk (file)
+    boundaries of ONE stream over all channels."""
+    import lfdas.stream as ST
+    here = os.path.dirname(os.path.abspath(__file__))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n_ch, push, n_push = 7, 2_000, 9  # 100 Hz, 20 s pushes, 180 s
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, os.path.dirname(here),
+                                                os.path.join(os.path.dirname(here), "low-freq-real-time_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    procs = [ctx.Process(target=_stream_worker, args=(r, 2, port, n_ch, push, n_push, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=180) for _ in range(2)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    one = ST.LowpassStream(n_ch, 10_000_000, 1.0, 40, 5, mode="continuous", t_start=STREAM_T0,
+                           t_end=STREAM_T0 + (push * n_push - 1) * 10_000_000, dry_run=True)
+    ref = []
+    for k in range(n_push):
+        o = one.push(np.zeros((n_ch, push), np.float32), STREAM_T0 + k * push * 10_000_000)
+        ref.append((o.n_out, o.t_first_ns if o.n_out else 0, tuple(o.chunk_counts)))
+    o = one.flush()
+    ref.append((o.n_out, o.t_first_ns if o.n_out else 0, tuple(o.chunk_counts)))
+    assert [g[1] for g in got] == [(0, 4), (4, 7)]
+    assert [g[2] for g in got] == [4, 3]
+    assert sum(r[0] for r in ref) > 0
+    for _, _, _, rec, n_edge in got:
+        assert rec == ref
+        assert n_edge > 0
+
+
+def test_bench_refuses_more_gpus_than_present_and_launcher_mismatch():
+    """``bench.py --gpus 2`` on a node without 2 GPUs fails clearly and prints
+    no JSON line (never an N = 1 line for an N > 1 request); under a launcher
+    a WORLD_SIZE that differs from --gpus is refused."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # no device: the refusal needs no GPU
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2 and "needs 2 GPUs" in r.stderr and "{" not in r.stdout
+    env["WORLD_SIZE"] = "4"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr and "{" not in r.stdout

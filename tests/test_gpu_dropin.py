@@ -204,3 +204,29 @@ def test_spool_chunk_windows_reproduce_lfproc_in_one_plan():
     for o in outs2:
         assert o.data.shape == (300, 10)
     assert PL.launch_count == n1 + 2
+
+
+def test_chunk_window_output_shared_by_update_attrs_copy():
+    """A lazy chunk-window output and its update_attrs copy share one
+    request: both read the same data, in either order, any number of times
+    (the result used to be popped on the first read)."""
+    sp = _example_spool()
+    P, B, dt = 40, 6, 0.2
+    from lfdas import schedule as S
+    t1, t2 = np.datetime64("2017-09-18T00:00:00", "ns"), np.datetime64("2017-09-18T00:00:24", "ns")
+    tg = S.time_grid(t1, t2, dt)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    windows = sp.chunk(time=P * dt, overlap=2 * B * dt, keep_partial=True)
+    fc = 1 / dt / 2 * 0.9
+    a = [w.pass_filter(time=(None, fc)).interpolate(time=tg[oa:ob].astype("datetime64[ns]"))
+         for w, (_, _, oa, ob) in zip(windows, sched)]
+    b = [o.update_attrs(d_time=dt) for o in a]
+    d_a1 = a[1].data
+    d_b1 = b[1].data
+    d_b0 = b[0].data
+    d_a0 = a[0].data
+    np.testing.assert_array_equal(d_a1, d_b1)
+    np.testing.assert_array_equal(d_a0, d_b0)
+    assert b[0].attrs["d_time"] == dt
+    for o in a[2:] + b[2:]:
+        assert o.data.shape == (300, o.coords["time"].size)
