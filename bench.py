@@ -532,7 +532,8 @@ def bench_rolling(dev, W, S_, reps=10):
     torch.cuda.empty_cache()
     return {"value": 5000 * 600_000 / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms,
             "config": f"5,000 ch x 10 min @ 1 kHz fp32, W = {W}, S = {S_}",
-            "kernel": "k_rolling_tc" if S_ >= W else "k_rolling_scan_tc",
+            "kernel": ("k_rolling_tc" if S_ >= W else
+                       ("k_rolling_seg" if S_ > 1 and np.gcd(W, S_) >= 16 else "k_rolling_scan_tc")),
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_sample": 4 + 4 / S_}}
 
@@ -849,6 +850,7 @@ def main():
     if not args.no_rolling and ws == 1:
         secondary["rolling_mean_cfg2"] = bench_rolling(dev, 1000, 1000)
         secondary["rolling_mean_cfg2_step1"] = bench_rolling(dev, 1000, 1, reps=5)
+        secondary["rolling_mean_cfg2_step250"] = bench_rolling(dev, 1000, 250, reps=5)
     if not args.no_stream and ws == 1:
         secondary["edge_latency_cfg4"] = bench_edge_cfg4(dev)
         secondary["edge_latency_cfg4_time_major"] = bench_edge_cfg4(dev, time_major=True)

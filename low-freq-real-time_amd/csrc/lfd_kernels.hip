@@ -1892,6 +1892,164 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
 
 
 // ---------------------------------------------------------------------------
+// k_rolling_seg — rolling mean for 1 < S < W on time-contiguous rows by
+// segment prefix sums (g = gcd(W, S) >= 16, M = W / g, Q = S / g).  Segment
+// j holds positions ((j - 1) g, j g]; output k is the sum of segments
+// kQ - M + 1 .. kQ over W:
+//   out[k] = (SP(kQ) - SP(kQ - M)) / W,   SP(j) = sum of x over (jA g, j g]
+// with SP relative to the unit's first needed boundary jA = ka Q - M.  A
+// wave owns (channel, range of outputs); per tile of 1,024 positions (16
+// consecutive per lane, 4 float4 loads, NPF tiles in flight) every lane sums
+// its 16 samples in float64 and the sum up to the one segment boundary
+// (g >= 16) its positions may hold; one DPP wave scan of the lane sums gives
+// SP at every boundary of the tile, written to a wave-private LDS ring of
+// segment prefixes.  Outputs read two ring entries each: no per-position
+// running sum, no ring of raw samples, the only carried value is the tile
+// total.  Nulls: packed counts (null_code) ride along in an int64 ring, so a
+// window's NaN / +-inf counts give numpy's mean of it exactly; tiles without
+// a non-finite sample skip that bookkeeping.
+// ---------------------------------------------------------------------------
+constexpr int RG_E = 16;          // positions per lane per tile
+constexpr int RG_P = 64 * RG_E;   // positions per tile
+
+__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t w = __shfl_up(v, o, 64);
+    if (lane >= o) v += w;
+  }
+  return v;
+}
+
+template <int NPF>
+__global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch,
+                                                     int W, int S, int g, float *__restrict__ y, int64_t ys_ch,
+                                                     int64_t ys_t, int seg_out, int ring_mask) {
+  extern __shared__ double rg_ring_all[];
+  const int R = ring_mask + 1;
+  double *spr = rg_ring_all + (size_t)(threadIdx.x >> 6) * 2 * R;   // SP(j) at slot j & ring_mask
+  int64_t *cdr = reinterpret_cast<int64_t *>(spr + R);              // packed null counts, same slots
+  const int lane = threadIdx.x & 63;
+  const int M = W / g, Q = S / g;
+  const int n_out = (n_t + S - 1) / S;
+  const int n_seg = (n_out + seg_out - 1) / seg_out;
+  const int64_t n_units = (int64_t)n_seg * n_ch;
+  const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int k_first = (M + Q - 1) / Q;  // first output with a full window (kS >= W - 1 <=> kQ >= M)
+  const float nanv = __builtin_nanf("");
+  const double inv_w = 1.0 / (double)W;
+  for (int64_t u = uniform64(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); u < n_units; u += n_waves) {
+    const int useg = (int)(u % n_seg);
+    const int64_t ch = u / n_seg;
+    const int k0 = useg * seg_out;
+    const int k1 = min(n_out, k0 + seg_out);
+    const float *row = x + ch * s_ch;
+    float *yo = y + ch * ys_ch;
+    for (int k = k0 + lane; k < k1 && k < k_first; k += 64) yo[k * ys_t] = nanv;
+    const int ka = max(k0, k_first);
+    if (ka >= k1) continue;
+    const int jA = ka * Q - M;               // SP(jA) = 0
+    const int pos0 = jA * g + 1;             // first accumulated position
+    const int pend = (k1 - 1) * S;           // last one (< n_t)
+    if (lane == 0) {
+      spr[jA & ring_mask] = 0.0;
+      cdr[jA & ring_mask] = 0;
+    }
+    double carry = 0.0;
+    int64_t ccarry = 0;
+    int kn = ka;  // next output to emit
+    struct Tile {
+      float v[RG_E];
+    };
+    auto load = [&](int tb, Tile &T) {
+      const int p = tb + RG_E * lane;
+      if (tb >= pos0 && tb + RG_P - 1 <= pend) {
+#pragma unroll
+        for (int h = 0; h < RG_E / 4; ++h) {
+          const f4v a = *reinterpret_cast<const f4v *>(row + p + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T.v[4 * h + e] = a[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < RG_E; ++e) T.v[e] = (p + e >= pos0 && p + e <= pend) ? row[p + e] : 0.0f;
+      }
+    };
+    auto process = [&](int tb, const Tile &T) {
+      const int p = tb + RG_E * lane;
+      // this lane's segment boundary (a multiple of g), if any: offset eb
+      const int bq = (p + g - 1) / g;
+      const int bpos = bq * g;
+      const int eb = bpos - p;
+      const bool has = eb < RG_E && bpos > jA * g && bpos <= pend;
+      double tot = 0.0, part = 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int e = 0; e < RG_E; ++e) {
+        const float v = T.v[e];
+        const bool f = __builtin_isfinite(v);
+        bad |= !f;
+        const double d = f ? (double)v : 0.0;
+        tot += d;
+        part += e <= eb ? d : 0.0;
+      }
+      const double incl = wave_incl_scan_dpp(tot);
+      if (has) spr[bq & ring_mask] = carry + (incl - tot) + part;
+      carry += readlane_d(incl, 63);
+      if (__any(bad)) {
+        int64_t ct = 0, cp = 0;
+#pragma unroll
+        for (int e = 0; e < RG_E; ++e) {
+          const int64_t c = null_code(T.v[e]);  // 0 for the masked positions (0.0f)
+          ct += c;
+          cp += e <= eb ? c : 0;
+        }
+        const int64_t ci = wave_incl_scan_i64(ct, lane);
+        if (has) cdr[bq & ring_mask] = ccarry + (ci - ct) + cp;
+        ccarry += __shfl(ci, 63, 64);
+      } else if (has) {
+        cdr[bq & ring_mask] = ccarry;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // outputs whose window ends in this tile (kS <= its last position)
+      const int kmax = min(k1 - 1, (tb + RG_P - 1) / S);
+      for (int k = kn + lane; k <= kmax; k += 64) {
+        const int j = k * Q;
+        const double sum = spr[j & ring_mask] - spr[(j - M) & ring_mask];
+        const int64_t code = cdr[j & ring_mask] - cdr[(j - M) & ring_mask];
+        const float mean = (float)(sum * inv_w);
+        yo[(int64_t)k * ys_t] = code ? null_mean(code, mean) : mean;
+      }
+      kn = max(kn, kmax + 1);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    Tile Tr[NPF + 1];
+    int tb = pos0 & ~3;
+#pragma unroll
+    for (int d = 0; d < NPF; ++d)
+      if (tb + d * RG_P <= pend) load(tb + d * RG_P, Tr[d]);
+    bool fin = false;
+    while (!fin) {
+#pragma unroll
+      for (int uu = 0; uu <= NPF; ++uu) {
+        if (tb + NPF * RG_P <= pend) load(tb + NPF * RG_P, Tr[(uu + NPF) % (NPF + 1)]);
+        process(tb, Tr[uu]);
+        tb += RG_P;
+        if (tb > pend) {
+          fin = true;
+          break;
+        }
+      }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
 // k_block_functionals_mfma — the block functionals as a skinny GEMM on the
 // fp64 matrix cores (lfd_internal.h TapGeom):
 //   F[k][c][ch] = sum_p Kx[c][p] x[ch][base + k*L + row_off + p].
@@ -2432,6 +2590,68 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
 // tile.  512-thread workgroups: taps + 8 waves x 2 run buffers in LDS.
 // ---------------------------------------------------------------------------
 
+// The 4 values a column's lanes hold in the 4 16-lane rows (lane 16k + c
+// holds component k of column c in the MFMA output layout), gathered into
+// every lane of that column: three permlane swaps per 32-bit half (VALU lane
+// exchanges, no LDS round trip).  permlane32_swap(x, x) leaves row (k & 1)'s
+// value in [0] and row 2 + (k & 1)'s in [1]; permlane16_swap(y, y) then
+// leaves y's even row in [0] and its odd row in [1] of every lane.
+__device__ __forceinline__ void row_gather4(double v, double (&o)[4]) {
+  const uint32_t lo = (uint32_t)__double2loint(v), hi = (uint32_t)__double2hiint(v);
+  const auto r_lo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto r_hi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const auto a_lo = __builtin_amdgcn_permlane16_swap(r_lo[0], r_lo[0], false, false);
+  const auto a_hi = __builtin_amdgcn_permlane16_swap(r_hi[0], r_hi[0], false, false);
+  const auto b_lo = __builtin_amdgcn_permlane16_swap(r_lo[1], r_lo[1], false, false);
+  const auto b_hi = __builtin_amdgcn_permlane16_swap(r_hi[1], r_hi[1], false, false);
+  o[0] = __hiloint2double((int)a_hi[0], (int)a_lo[0]);
+  o[1] = __hiloint2double((int)a_hi[1], (int)a_lo[1]);
+  o[2] = __hiloint2double((int)b_hi[0], (int)b_lo[0]);
+  o[3] = __hiloint2double((int)b_hi[1], (int)b_lo[1]);
+}
+
+// Streaming run epilogue (SEPI): the run's reverse pass accumulated FORWARD,
+// block by block, in registers — no LDS run buffer, no backward sweep at
+// the run end.  With v_p = e_r0(p) + M S0(p) and pg_p = p0(p) + G0 S0(p):
+//   E_r  = T0(ks)  = sum_p PhiR^p v_p
+//   y0_p = pg_p + sum_{m > p} H0 PhiR^(m-p-1) v_m      (RunConst::B[d] = H0 PhiR^d)
+// Lane (q, col) keeps S0[q], E_r[q] and the y0 of the run's blocks q and
+// q + 4 (the blocks it stores), adding each later block's contribution as
+// that block arrives.
+constexpr int RUN_CST_S = 224;  // doubles: PhiF M PhiR G0 H0 (56) + PhiR^p (128) + B (32)
+struct RunAccS {
+  double S0 = 0.0, Er = 0.0, ya = 0.0, yb = 0.0;
+};
+__device__ __forceinline__ void run_block_stream(const double *__restrict__ cst, int q, int p, const double (&a)[3],
+                                                 RunAccS &st) {
+  const double *PhiF = cst, *Mm = cst + 16, *G0 = cst + 48, *PhiRp = cst + 56, *Bc = cst + 184;
+  double sv[4];
+  row_gather4(st.S0, sv);
+  double v = a[1], pg = a[2], sn = a[0];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v = fma(Mm[q * 4 + j], sv[j], v);
+    pg = fma(G0[j], sv[j], pg);
+    sn = fma(PhiF[q * 4 + j], sv[j], sn);
+  }
+  st.S0 = sn;
+  double vv[4];
+  row_gather4(v, vv);
+  const double *pr = PhiRp + p * 16 + q * 4;
+  const int da = p - q - 1, db = p - q - 5;  // held blocks q, q + 4: offsets m - p' - 1
+  const double *ca = Bc + (da > 0 ? da : 0) * 4, *cb = Bc + (db > 0 ? db : 0) * 4;
+  double er = st.Er, ya = st.ya, yb = st.yb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    er = fma(pr[j], vv[j], er);
+    ya = fma(ca[j], vv[j], ya);
+    yb = fma(cb[j], vv[j], yb);
+  }
+  st.Er = er;
+  st.ya = da >= 0 ? ya : (da == -1 ? pg : st.ya);
+  st.yb = db >= 0 ? yb : (db == -1 ? pg : st.yb);
+}
+
 struct TmIter {
   float p[4][4], q[4][4];  // [16-sample group j][step e]
 };
@@ -2591,20 +2811,28 @@ __device__ __forceinline__ void tm_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t 
 // LFD_TM_MODE, X2 + BUF instantiations): 3 = loads only (a VALU sum of the
 // samples, no MFMA, no run epilogue, no stores) = the floor of this access
 // shape; 4 = loads + MFMAs, the run epilogue reduced to nothing.
+// SEPI: streaming run epilogue (run_block_stream): the LDS holds only the
+// taps and RUN_CST_S constants, and registers are capped for 4 waves per
+// SIMD, so two 512-thread workgroups share a CU (16 waves instead of 8).
 template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false, bool BUF = false,
-          int MODE = 0>
-__global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
+          int MODE = 0, bool SEPI = false>
+__global__ __launch_bounds__(NT, (NTILE == 1 || SEPI) ? 4 : 1) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
   extern __shared__ double Ks[];
   const int tab = tg.Lp * tg.nc;  // one table: row shift 0
   for (int i = 2 * threadIdx.x; i < tab; i += 2 * blockDim.x)
     *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
-  double *cst = Ks + tab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4]
+  double *cst = Ks + tab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4] (SEPI: + PhiR^p[8][16] + B[8][4])
   for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
+  if (SEPI) {
+    for (int i = threadIdx.x; i < RUN_R * 16; i += blockDim.x) cst[56 + i] = (&rg.rc->PhiRp[0][0])[i];
+    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x) cst[184 + i] = (&rg.rc->B[0][0])[i];
+  }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double *wbase = Ks + tab + RUN_CST + wave * NTILE * RUN_WB;  // tile t's buffer: wbase + t * RUN_WB
+  (void)wbase;
   constexpr int CW = 16 * NTILE;  // channels per wave
   const int64_t n_c32 = (g.n_ch + CW - 1) / CW;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -2718,7 +2946,42 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
       rlen = run_len_of(r);
     }
   };
+  RunAccS ra[2];
+  // SEPI run end: tile t's y0 of blocks q and q + 4, and the aggregates
+  auto run_end_stream = [&]() {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (!X2 && t == 1 && !tile1) break;
+      const int64_t chn = X2 ? c32 * 32 + 2 * col + t : (NTILE * c32 + t) * 16 + col;
+      const int64_t cg = chn >> 4;
+      const int cc = (int)(chn & 15);
+      if (X2 && cg * 16 >= g.n_ch) continue;
+      double *y0o = Y0 + (cg * g.nb + rks) * 16 + cc;
+      if (q < rlen) y0o[q * 16] = ra[t].ya;
+      if (q + 4 < rlen) y0o[(q + 4) * 16] = ra[t].yb;
+      double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + cc;
+      ag[q * 16] = ra[t].S0;
+      ag[(4 + q) * 16] = ra[t].Er;
+      ra[t] = RunAccS{};
+    }
+    ++r;
+    if (r < r_end) {
+      rks = run_ks_of(r);
+      rlen = run_len_of(r);
+    }
+  };
   auto finish_block = [&](const d4v &acc0, const d4v &acc1, int64_t k) {
+    if constexpr (SEPI) {
+      const int p = (int)(k - rks);
+      const double a0[3] = {acc0[0], acc0[1], acc0[2]};
+      run_block_stream(cst, q, p, a0, ra[0]);
+      if (NTILE == 2) {
+        const double a1[3] = {acc1[0], acc1[1], acc1[2]};
+        run_block_stream(cst, q, p, a1, ra[1]);
+      }
+      if (p + 1 == rlen) run_end_stream();
+      return;
+    }
     if (NTILE == 2) {
       block_done(acc0, 0, k);
       block_done(acc1, 1, k);
@@ -2739,7 +3002,7 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : 1) void k_block_runs_mfma_tm(
         tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0,
                              acc1);
     }
-    finish_block(acc0, acc1, k);
+    if (MODE == 0) finish_block(acc0, acc1, k);  // (diagnostics: no LDS run buffers)
   };
 
   int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
@@ -2865,7 +3128,7 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   if (const char *v = std::getenv("LFD_TM_PF")) pf = std::atoi(v);
   int ntile = 2;
   if (const char *v = std::getenv("LFD_TM_NTILE")) ntile = std::atoi(v) == 1 ? 1 : 2;
-  const size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * ntile * RUN_WB;
+  size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * ntile * RUN_WB;
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   auto go = [&](auto kern, int NT) -> hipError_t {
     static bool attr[2] = {false, false};  // per instantiation below
@@ -2899,8 +3162,20 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
     const int pfb = std::getenv("LFD_TM_PF") ? pf : 1;
     int mode = 0;
     if (const char *v = std::getenv("LFD_TM_MODE")) mode = std::atoi(v);
+    // (LFD_TM_DIAG_LDS=1: the diagnostics allocate only the tap table, so
+    // their occupancy is set by registers, not by the run buffers)
+    if (mode >= 3 && getenv_flag("LFD_TM_DIAG_LDS")) lds = tab;
+    if (mode == 3 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 3>, 512);
     if (mode == 3) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 3>, 512);
     if (mode == 4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 4>, 512);
+    // streaming run epilogue: taps + constants only in LDS (A/B knob LFD_TM_SEPI=0)
+    bool sepi = false;
+    if (const char *v = std::getenv("LFD_TM_SEPI")) sepi = std::atoi(v) != 0;
+    if (sepi && nt == 512) {
+      lds = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
+      if (pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 0, true>, 512);
+      return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
+    }
     if (nt == 512 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true>, 512);
     if (nt == 512 && pfb == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true>, 512);
     return hipErrorInvalidValue;
@@ -3437,6 +3712,42 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
   // cfg2), so the scan takes every W > 2S (A/B knob LFD_ROLL_DIRECT_MAX)
   int64_t direct_max = 2;
   if (const char *v = std::getenv("LFD_ROLL_DIRECT_MAX")) direct_max = std::atoll(v);
+  // segment prefix sums (k_rolling_seg) when g = gcd(W, S) >= 16 and the
+  // prefix ring fits: no per-position running sum (A/B knob LFD_ROLL_SEGSUM=0)
+  {
+    int64_t ga = W, gb = S;
+    while (gb) {
+      const int64_t t = ga % gb;
+      ga = gb;
+      gb = t;
+    }
+    const int64_t g = ga;
+    int ring = 16;
+    while (ring < W / g + RG_P / g + 3) ring *= 2;
+    bool seg = s_t == 1 && S > 1 && S < W && g >= 16 && ring <= 1024 && n_t < (int64_t)INT32_MAX - 2 * RG_P &&
+               (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
+    if (const char *v = std::getenv("LFD_ROLL_SEGSUM")) seg = seg && std::atoi(v) != 0;
+    if (seg) {
+      int64_t span = std::max<int64_t>(32768, 8 * W);
+      if (const char *v = std::getenv("LFD_ROLL_SEG")) span = std::max<int64_t>(4 * W, std::atoll(v));
+      while (span > std::max<int64_t>(4096, 4 * W) && n_ch * ((n_t + span - 1) / span) < 16384) span /= 2;
+      const int64_t seg_out = std::max<int64_t>(1, span / S);
+      const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
+      int64_t blocks = (units + 3) / 4;
+      if (blocks > cap) blocks = cap;
+      const size_t lds = sizeof(double) * 2 * (size_t)ring * 4;
+      static bool attr = false;
+      if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rolling_seg<2>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+      }
+      k_rolling_seg<2><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y, ys_ch,
+                                                           ys_t, (int)seg_out, ring - 1);
+      return hipGetLastError();
+    }
+  }
   if (s_t == 1 && W <= direct_max * S) {
     // windows overlap little or not at all: each is summed directly by one wave
     const int64_t waves = n_ch * n_out;

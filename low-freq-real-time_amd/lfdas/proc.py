@@ -165,7 +165,10 @@ class ChunkGroup:
         when their grids do not form one uniform, non-overlapping grid."""
         from ._lib import LFDUnsupported
         from .plan import LowpassPlan
-        batch = sorted(batch, key=lambda r: (int(r.lo[0]) + float(r.w[0])) if len(r.lo) else np.inf)
+        # order by the first output's position in the PARENT (r.lo is
+        # window-relative: every LFProc window starts its outputs B grid
+        # points in, so window-relative keys tie)
+        batch = sorted(batch, key=lambda r: (r.s0 + int(r.lo[0]) + float(r.w[0])) if len(r.lo) else np.inf)
         if any(len(r.lo) == 0 for r in batch):
             return False
         lo = np.concatenate([r.lo + r.s0 for r in batch])

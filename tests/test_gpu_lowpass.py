@@ -189,10 +189,13 @@ def test_long_grid_spacing_runs_mfma(cfg, off_ns):
 
 
 @pytest.mark.parametrize("W,S_", [(1000, 1), (1000, 250), (1000, 1000), (1000, 3), (999, 7), (64, 1),
-                                  (4000, 7)])  # W + 512 > 4096: x[t - W] re-read, no LDS ring
+                                  (4000, 7),  # W + 512 > 4096: x[t - W] re-read, no LDS ring
+                                  # gcd(W, S) >= 16: segment prefix sums (k_rolling_seg)
+                                  (1000, 200), (1000, 400), (2500, 1000), (4096, 64), (48, 16), (1000, 500)])
 def test_rolling_mean_window_step(W, S_):
     """Overlapping windows (step < window) run the running-sum scan kernel
-    (every sample read once); step >= window sums each window directly."""
+    (every sample read once), or segment prefix sums when gcd(W, S) >= 16;
+    step >= window sums each window directly."""
     import torch
     from lfdas.plan import rolling_mean_device
     rng = np.random.default_rng(W + S_)
@@ -214,14 +217,16 @@ def test_rolling_mean_window_step(W, S_):
         assert _relrms(y[m], ref[m]) < 1e-6, layout
 
 
-def test_rolling_mean_overlapping_nulls():
+@pytest.mark.parametrize("S_", [1, 250, 200])
+def test_rolling_mean_overlapping_nulls(S_):
     """step < window: a NaN / inf sample turns exactly the windows holding it
-    into NaN / inf (the running sum carries a count of nulls), the rest stay
-    exact, also right after the null leaves the window."""
+    into NaN / inf (the running sum, or the segment prefix ring, carries a
+    count of nulls), the rest stay exact, also right after the null leaves
+    the window."""
     import torch
     from lfdas.plan import rolling_mean_device
     rng = np.random.default_rng(8)
-    n_ch, n, W, S_ = 5, 20_000, 1000, 1
+    n_ch, n, W = 5, 20_000, 1000
     x = (rng.standard_normal((n_ch, n)) + 0.5).astype(np.float32)
     x[0, 2999] = np.nan
     x[1, 5000] = np.inf

@@ -12,3 +12,8 @@ tail -1 gpurun_out/r03_rehearsal.json | python -c "import json,sys; d=json.loads
 # time-major K1: production vs loads-only floor (MODE 3) vs no epilogue (MODE 4), one allocation
 timeout -k 10 300 python tools/ab_plan.py --tm --reps 3 "" "LFD_TM_MODE=3" "LFD_TM_MODE=4" > gpurun_out/r03_tm_diag.txt 2>&1 || { tail -20 gpurun_out/r03_tm_diag.txt; exit 1; }
 tail -4 gpurun_out/r03_tm_diag.txt
+# rolling mean: the new segment-sum kernel vs the running-sum scan (cfg2, S = 250 / 200)
+timeout -k 10 300 python -u -m pytest tests/test_gpu_lowpass.py -x -q -k rolling --timeout 120 --timeout-method thread > gpurun_out/r03_roll_tests.log 2>&1 || { tail -30 gpurun_out/r03_roll_tests.log; exit 1; }
+tail -1 gpurun_out/r03_roll_tests.log
+timeout -k 10 200 python tools/roll_ab.py > gpurun_out/r03_roll_ab.txt 2>&1 || { tail -20 gpurun_out/r03_roll_ab.txt; exit 1; }
+cat gpurun_out/r03_roll_ab.txt
