@@ -2311,6 +2311,68 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
 // the run's last block a backward sweep over it gives y0 and E_r = T0(ks).
 // One 1024-thread workgroup per CU (taps + constants + 16 run buffers).
 // ---------------------------------------------------------------------------
+// The 4 values a column's lanes hold in the 4 16-lane rows (lane 16k + c
+// holds component k of column c in the MFMA output layout), gathered into
+// every lane of that column: three permlane swaps per 32-bit half (VALU lane
+// exchanges, no LDS round trip).  permlane32_swap(x, x) leaves row (k & 1)'s
+// value in [0] and row 2 + (k & 1)'s in [1]; permlane16_swap(y, y) then
+// leaves y's even row in [0] and its odd row in [1] of every lane.
+__device__ __forceinline__ void row_gather4(double v, double (&o)[4]) {
+  const uint32_t lo = (uint32_t)__double2loint(v), hi = (uint32_t)__double2hiint(v);
+  const auto r_lo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto r_hi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const auto a_lo = __builtin_amdgcn_permlane16_swap(r_lo[0], r_lo[0], false, false);
+  const auto a_hi = __builtin_amdgcn_permlane16_swap(r_hi[0], r_hi[0], false, false);
+  const auto b_lo = __builtin_amdgcn_permlane16_swap(r_lo[1], r_lo[1], false, false);
+  const auto b_hi = __builtin_amdgcn_permlane16_swap(r_hi[1], r_hi[1], false, false);
+  o[0] = __hiloint2double((int)a_hi[0], (int)a_lo[0]);
+  o[1] = __hiloint2double((int)a_hi[1], (int)a_lo[1]);
+  o[2] = __hiloint2double((int)b_hi[0], (int)b_lo[0]);
+  o[3] = __hiloint2double((int)b_hi[1], (int)b_lo[1]);
+}
+
+// Streaming run epilogue (SEPI): the run's reverse pass accumulated FORWARD,
+// block by block, in registers — no LDS run buffer, no backward sweep at
+// the run end.  With v_p = e_r0(p) + M S0(p) and pg_p = p0(p) + G0 S0(p):
+//   E_r  = T0(ks)  = sum_p PhiR^p v_p
+//   y0_p = pg_p + sum_{m > p} H0 PhiR^(m-p-1) v_m      (RunConst::B[d] = H0 PhiR^d)
+// Lane (q, col) keeps S0[q], E_r[q] and the y0 of the run's blocks q and
+// q + 4 (the blocks it stores), adding each later block's contribution as
+// that block arrives.
+constexpr int RUN_CST_S = 224;  // doubles: PhiF M PhiR G0 H0 (56) + PhiR^p (128) + B (32)
+struct RunAccS {
+  double S0 = 0.0, Er = 0.0, ya = 0.0, yb = 0.0;
+};
+__device__ __forceinline__ void run_block_stream(const double *__restrict__ cst, int q, int p, const double (&a)[3],
+                                                 RunAccS &st) {
+  const double *PhiF = cst, *Mm = cst + 16, *G0 = cst + 48, *PhiRp = cst + 56, *Bc = cst + 184;
+  double sv[4];
+  row_gather4(st.S0, sv);
+  double v = a[1], pg = a[2], sn = a[0];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v = fma(Mm[q * 4 + j], sv[j], v);
+    pg = fma(G0[j], sv[j], pg);
+    sn = fma(PhiF[q * 4 + j], sv[j], sn);
+  }
+  st.S0 = sn;
+  double vv[4];
+  row_gather4(v, vv);
+  const double *pr = PhiRp + p * 16 + q * 4;
+  const int da = p - q - 1, db = p - q - 5;  // held blocks q, q + 4: offsets m - p' - 1
+  const double *ca = Bc + (da > 0 ? da : 0) * 4, *cb = Bc + (db > 0 ? db : 0) * 4;
+  double er = st.Er, ya = st.ya, yb = st.yb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    er = fma(pr[j], vv[j], er);
+    ya = fma(ca[j], vv[j], ya);
+    yb = fma(cb[j], vv[j], yb);
+  }
+  st.Er = er;
+  st.ya = da >= 0 ? ya : (da == -1 ? pg : st.ya);
+  st.yb = db >= 0 ? yb : (db == -1 ? pg : st.yb);
+}
+
 constexpr int RUN_WB = RUN_R * 5 * 16;  // doubles per wave run buffer
 constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 
@@ -2323,7 +2385,9 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 // BUFL: interior sample loads as buffer loads (descriptor at the wave-uniform
 // row base of the channel group, a constant 32-bit voffset per lane) instead
 // of a 64-bit pointer per lane and iteration (fewer VGPRs under MINW)
-template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false>
+// SEPI: streaming run epilogue (run_block_stream; LDS: taps + RUN_CST_S
+// constants, no run buffers, no backward sweep at run ends)
+template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -2333,11 +2397,16 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   const int ntab = tab * tg.nvar;
   for (int i = 2 * threadIdx.x; i < ntab; i += 2 * blockDim.x)
     *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
-  double *cst = Ks + ntab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4]
+  double *cst = Ks + ntab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4] (SEPI: + PhiR^p[8][16] + B[8][4])
   for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
+  if (SEPI) {
+    for (int i = threadIdx.x; i < RUN_R * 16; i += blockDim.x) cst[56 + i] = (&rg.rc->PhiRp[0][0])[i];
+    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x) cst[184 + i] = (&rg.rc->B[0][0])[i];
+  }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double *wb = Ks + ntab + RUN_CST + wave * RUN_WB;
+  (void)wb;
   const int64_t n_cg = (g.n_ch + 15) / 16;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_cg * rg.n_groups) return;
@@ -2393,9 +2462,29 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   int64_t rks = k0;
   int rlen = run_len_of(r);
   double S0 = 0.0;  // run prefix state, component q of channel col
+  RunAccS ra;       // (SEPI)
   auto block_done = [&](const d4v &a, int64_t k) {
     // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
     const int p = (int)(k - rks);
+    if constexpr (SEPI) {
+      const double a3[3] = {a[0], a[1], a[2]};
+      run_block_stream(cst, q, p, a3, ra);
+      if (p + 1 == rlen) {
+        double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
+        if (q < rlen) y0o[q * 16] = ra.ya;
+        if (q + 4 < rlen) y0o[(q + 4) * 16] = ra.yb;
+        double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + col;
+        ag[q * 16] = ra.S0;
+        ag[(4 + q) * 16] = ra.Er;
+        ra = RunAccS{};
+        ++r;
+        if (r < r_end) {
+          rks = run_ks_of(r);
+          rlen = run_len_of(r);
+        }
+      }
+      return;
+    }
     double sv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) sv[j] = __shfl(S0, col + 16 * j, 64);
@@ -2590,68 +2679,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
 // tile.  512-thread workgroups: taps + 8 waves x 2 run buffers in LDS.
 // ---------------------------------------------------------------------------
 
-// The 4 values a column's lanes hold in the 4 16-lane rows (lane 16k + c
-// holds component k of column c in the MFMA output layout), gathered into
-// every lane of that column: three permlane swaps per 32-bit half (VALU lane
-// exchanges, no LDS round trip).  permlane32_swap(x, x) leaves row (k & 1)'s
-// value in [0] and row 2 + (k & 1)'s in [1]; permlane16_swap(y, y) then
-// leaves y's even row in [0] and its odd row in [1] of every lane.
-__device__ __forceinline__ void row_gather4(double v, double (&o)[4]) {
-  const uint32_t lo = (uint32_t)__double2loint(v), hi = (uint32_t)__double2hiint(v);
-  const auto r_lo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto r_hi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  const auto a_lo = __builtin_amdgcn_permlane16_swap(r_lo[0], r_lo[0], false, false);
-  const auto a_hi = __builtin_amdgcn_permlane16_swap(r_hi[0], r_hi[0], false, false);
-  const auto b_lo = __builtin_amdgcn_permlane16_swap(r_lo[1], r_lo[1], false, false);
-  const auto b_hi = __builtin_amdgcn_permlane16_swap(r_hi[1], r_hi[1], false, false);
-  o[0] = __hiloint2double((int)a_hi[0], (int)a_lo[0]);
-  o[1] = __hiloint2double((int)a_hi[1], (int)a_lo[1]);
-  o[2] = __hiloint2double((int)b_hi[0], (int)b_lo[0]);
-  o[3] = __hiloint2double((int)b_hi[1], (int)b_lo[1]);
-}
-
-// Streaming run epilogue (SEPI): the run's reverse pass accumulated FORWARD,
-// block by block, in registers — no LDS run buffer, no backward sweep at
-// the run end.  With v_p = e_r0(p) + M S0(p) and pg_p = p0(p) + G0 S0(p):
-//   E_r  = T0(ks)  = sum_p PhiR^p v_p
-//   y0_p = pg_p + sum_{m > p} H0 PhiR^(m-p-1) v_m      (RunConst::B[d] = H0 PhiR^d)
-// Lane (q, col) keeps S0[q], E_r[q] and the y0 of the run's blocks q and
-// q + 4 (the blocks it stores), adding each later block's contribution as
-// that block arrives.
-constexpr int RUN_CST_S = 224;  // doubles: PhiF M PhiR G0 H0 (56) + PhiR^p (128) + B (32)
-struct RunAccS {
-  double S0 = 0.0, Er = 0.0, ya = 0.0, yb = 0.0;
-};
-__device__ __forceinline__ void run_block_stream(const double *__restrict__ cst, int q, int p, const double (&a)[3],
-                                                 RunAccS &st) {
-  const double *PhiF = cst, *Mm = cst + 16, *G0 = cst + 48, *PhiRp = cst + 56, *Bc = cst + 184;
-  double sv[4];
-  row_gather4(st.S0, sv);
-  double v = a[1], pg = a[2], sn = a[0];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v = fma(Mm[q * 4 + j], sv[j], v);
-    pg = fma(G0[j], sv[j], pg);
-    sn = fma(PhiF[q * 4 + j], sv[j], sn);
-  }
-  st.S0 = sn;
-  double vv[4];
-  row_gather4(v, vv);
-  const double *pr = PhiRp + p * 16 + q * 4;
-  const int da = p - q - 1, db = p - q - 5;  // held blocks q, q + 4: offsets m - p' - 1
-  const double *ca = Bc + (da > 0 ? da : 0) * 4, *cb = Bc + (db > 0 ? db : 0) * 4;
-  double er = st.Er, ya = st.ya, yb = st.yb;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    er = fma(pr[j], vv[j], er);
-    ya = fma(ca[j], vv[j], ya);
-    yb = fma(cb[j], vv[j], yb);
-  }
-  st.Er = er;
-  st.ya = da >= 0 ? ya : (da == -1 ? pg : st.ya);
-  st.yb = db >= 0 ? yb : (db == -1 ? pg : st.yb);
-}
-
 struct TmIter {
   float p[4][4], q[4][4];  // [16-sample group j][step e]
 };
@@ -2812,11 +2839,13 @@ __device__ __forceinline__ void tm_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t 
 // samples, no MFMA, no run epilogue, no stores) = the floor of this access
 // shape; 4 = loads + MFMAs, the run epilogue reduced to nothing.
 // SEPI: streaming run epilogue (run_block_stream): the LDS holds only the
-// taps and RUN_CST_S constants, and registers are capped for 4 waves per
-// SIMD, so two 512-thread workgroups share a CU (16 waves instead of 8).
+// taps and RUN_CST_S constants; no backward sweep at run ends, during which
+// a wave issued no loads.  Registers allow 2 waves per SIMD (8 per CU: the
+// occupancy at which this access shape streams fastest,
+// profiles/r03_ubench_tm.txt).
 template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false, bool BUF = false,
           int MODE = 0, bool SEPI = false>
-__global__ __launch_bounds__(NT, (NTILE == 1 || SEPI) ? 4 : 1) void k_block_runs_mfma_tm(
+__global__ __launch_bounds__(NT, NTILE == 1 ? 4 : (SEPI ? 2 : 1)) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
   extern __shared__ double Ks[];
@@ -3168,8 +3197,10 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
     if (mode == 3 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 3>, 512);
     if (mode == 3) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 3>, 512);
     if (mode == 4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 4>, 512);
-    // streaming run epilogue: taps + constants only in LDS (A/B knob LFD_TM_SEPI=0)
-    bool sepi = false;
+    // streaming run epilogue: taps + constants only in LDS: 13.85 vs 14.35 ms
+    // on cfg3 stored time-major (in-process A/B on one allocation,
+    // profiles/r03_ab_tm_sepi.txt; A/B knob LFD_TM_SEPI=0)
+    bool sepi = true;
     if (const char *v = std::getenv("LFD_TM_SEPI")) sepi = std::atoi(v) != 0;
     if (sepi && nt == 512) {
       lds = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
@@ -3273,24 +3304,24 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   return hipGetLastError();
 }
 
-template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false>
+template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
-  // (MODE 4 diagnostic: no run buffers needed)
-  const size_t lds =
-      sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
+  // (MODE 4 diagnostic and SEPI: no run buffers)
+  const size_t lds = SEPI ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
+                          : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     hipError_t e =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL>),
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg,
-                                                                                   Y0, AG);
+  k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI><<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg,
+                                                                                         rg, Y0, AG);
   return hipGetLastError();
 }
 
@@ -3335,6 +3366,18 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   if (bufl && 16 * s_ch + 64 < ((int64_t)1 << 29) && mode == 0 && nt == 512 && minw == 4 && !m4) {
     if (pf == 2) return run_k1<2, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     if (pf == 1) return run_k1<1, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    return hipErrorInvalidValue;
+  }
+  // streaming run epilogue (A/B knob LFD_RUN_SEPI=1): no gain on
+  // channel-major rows (12.59 / 12.52 vs 12.50 ms on cfg3, 1.88 / 1.76 vs 1.76
+  // on a 1,250-channel shard; profiles/r03_ab_cm_sepi.txt), where 16 waves
+  // per CU already hide the run-end sweep
+  bool sepi = false;
+  if (const char *v = std::getenv("LFD_RUN_SEPI")) sepi = std::atoi(v) != 0;
+  if (sepi && mode == 0 && nt == 512 && !m4 && !bufl) {
+    if (minw == 4 && pf == 1) return run_k1<1, 0, 512, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (minw == 4 && pf == 2) return run_k1<2, 0, 512, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (minw == 0 && pf == 2) return run_k1<2, 0, 512, false, 0, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     return hipErrorInvalidValue;
   }
   if (minw == 4 && mode == 0 && nt == 512) {
