@@ -7,17 +7,18 @@ Butterworth at 0.45 Hz, decimate to 1 Hz, LFProc chunking P = 600, B = 7.
 One step = one pass of the hot path over the whole hour (7 overlapping chunks,
 3,585 outputs per channel), inputs resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--weak]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--strong]
 
 N > 1 runs one rank per GPU: under torch.distributed.run (the driver's
 form; WORLD_SIZE must equal --gpus), or ``python bench.py --gpus N`` starts
 that launcher itself as a child process (and fails, printing no line, when
-the node has fewer than N GPUs).  Default
-(strong scaling, the config's "channel-sharded at 1/2/4/8 GPUs"): the
-10,000 channels are split into contiguous blocks (lfdas.shard.channel_range),
-no data-path collective; ``value`` = all channel-samples / max-over-ranks
-time.  ``--weak``: every rank owns its own 10,000-channel spool; with N > 1
-the weak figure is also reported as ``secondary.weak_scaling_cfg3``.
+the node has fewer than N GPUs).  The path partitions by channel with
+no data-path collective, so the default is weak scaling: every rank owns
+its own 10,000-channel spool and ``value`` = all ranks' channel-samples /
+max-over-ranks time.  With N > 1 the config's "channel-sharded at 1/2/4/8
+GPUs" strong-scaling figure (cfg3's 10,000 channels split into contiguous
+blocks, lfdas.shard.channel_range) is reported beside it as
+``secondary.strong_scaling_cfg3``; ``--strong`` makes it the headline.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -54,7 +55,9 @@ def _args():
     p.add_argument("--no-stream", action="store_true", help="skip the cfg4 / cfg5 streaming lines")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the extra low-pass lines (off-sample grid, 1 kHz dt = 10 s, time-major)")
-    p.add_argument("--weak", action="store_true", help="every rank owns --channels channels (weak scaling)")
+    p.add_argument("--strong", action="store_true",
+                   help="headline = --channels split over the ranks (strong scaling); default: every rank "
+                        "owns --channels channels (weak scaling)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo collectives "
                         "(the line is marked rehearsal; not a scaling measurement)")
@@ -549,8 +552,10 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
 
     import torch
     import oracle
+    from lfdas.design import pass_filter_sos
     from lfdas.plan import load, set_timing, sosfiltfilt_device, sosfiltfilt_last_timing_ms
-    sos = oracle.dascore_pass_filter_sos(fs, band[0], band[1])
+    # the product's own filter design (the oracle is only the spot check below)
+    sos = pass_filter_sos(fs, band[0], band[1])
     x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
     synth_fill(x, fs, 77)
     y = torch.empty((n_ch, n), dtype=torch.float64, device=dev)
@@ -721,7 +726,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from lfdas.shard import channel_range
-    if args.weak:
+    if not args.strong:
         n_ch_total, (c0, c1) = args.channels * ws, (0, args.channels)
     else:
         n_ch_total = args.channels
@@ -796,19 +801,26 @@ def main():
     del x, y, wsb
     plan.close()
     torch.cuda.empty_cache()
-    if ws > 1 and not args.weak:
-        # weak scaling: every rank its own 10,000-channel spool
-        plan_w, _, _, _, _, _ = build_plan(args.channels, n, args.fs, args.dt_out, args.patch_size, args.edge_buff)
-        xw = torch.empty((args.channels, n), dtype=torch.float32, device=dev)
+    if ws > 1:
+        # the other scaling mode beside the headline: strong (cfg3's channels
+        # split over the ranks) under the weak default, weak under --strong
+        if args.strong:
+            o0, o1, o_tot, o_key = 0, args.channels, ws * args.channels, "weak_scaling_cfg3"
+        else:
+            (o0, o1), o_tot, o_key = channel_range(args.channels, ws, rank), args.channels, "strong_scaling_cfg3"
+        plan_w, _, _, _, _, _ = build_plan(o1 - o0, n, args.fs, args.dt_out, args.patch_size, args.edge_buff)
+        xw = torch.empty((o1 - o0, n), dtype=torch.float32, device=dev)
         synth_fill(xw, args.fs, 4321 + rank)
-        yw = torch.empty((args.channels, plan_w.n_grid), dtype=torch.float32, device=dev)
+        yw = torch.empty((o1 - o0, plan_w.n_grid), dtype=torch.float32, device=dev)
         ww = plan_w.alloc_workspace(dev)
         el_w, k1_w, _ = time_plan(plan_w, xw, yw, ww, stream, args.steps, 1, barrier)
         el_w = max_over_ranks(el_w)
-        secondary["weak_scaling_cfg3"] = {
-            "value": ws * args.channels * n * args.steps / el_w, "unit": "channel-samples/s",
+        secondary[o_key] = {
+            "value": o_tot * n * args.steps / el_w, "unit": "channel-samples/s",
             "ms_per_step": el_w / args.steps * 1e3, "kernel_ms_rank0": float(np.mean(k1_w)),
-            "scaling": "weak", "config": f"{args.channels:,} ch x 1 h @ 500 Hz per GPU x {ws} GPUs"}
+            "channels_rank0": o1 - o0, "scaling": "strong" if o_key.startswith("strong") else "weak",
+            "config": (f"{args.channels:,} ch x 1 h @ 500 Hz split over {ws} GPUs" if o_key.startswith("strong")
+                       else f"{args.channels:,} ch x 1 h @ 500 Hz per GPU x {ws} GPUs")}
         del xw, yw, ww
         plan_w.close()
         torch.cuda.empty_cache()
@@ -869,13 +881,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if args.weak else "strong",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (0.5 + sin + N(0,1), generated on device)",
             "config": {"workload": "cfg3: 10,000 ch x 1 h @ 500 Hz fp32 (72 GB), 4th-order Butterworth "
                                    "0.45 Hz zero-phase, decimate to 1 Hz, LFProc P=600 B=7"
-                                   + (", per GPU" if args.weak else ", channel-sharded over the GPUs"),
+                                   + (", channel-sharded over the GPUs" if args.strong else ", per GPU"),
                        "channels": n_ch_total, "channels_rank0": n_ch, "samples": n, "fs": args.fs,
                        "dt_out": args.dt_out, "chunks": len(sched),
                        "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),

@@ -1431,6 +1431,8 @@ int lfd_rolling_mean_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch
   return LFD_OK;
 }
 
+static thread_local int g_fir_kernel = -1;
+
 int lfd_fir_decimate_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
                          const double *taps, int64_t n_taps, int64_t q, int64_t delay, double *y, int64_t ys_ch,
                          int64_t ys_t, void *stream) {
@@ -1440,9 +1442,11 @@ int lfd_fir_decimate_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch
   if (n_ch < 1 || n_t < 1) return LFD_OK;
   if (!x || !y || !taps) return fail(LFD_EINVAL, "x, taps and y must be device pointers");
   LFD_HIP(lfd::launch_fir_decimate(x, n_ch, n_t, s_ch, s_t, taps, (int)n_taps, q, delay, y, ys_ch, ys_t,
-                                   reinterpret_cast<hipStream_t>(stream)));
+                                   reinterpret_cast<hipStream_t>(stream), &g_fir_kernel));
   return LFD_OK;
 }
+
+int lfd_fir_decimate_last_kernel(void) { return g_fir_kernel; }
 
 int lfd_demean_scale_f64(const double *x, int64_t n_rows, int64_t n_cols, int64_t s_r, int64_t s_c,
                          int64_t c0, int64_t c1, double scale, double *y, int64_t ys_r, int64_t ys_c,

@@ -262,9 +262,10 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                hipStream_t st);
 // FIR decimation: y[k] = sum_i h[i] x[k q + delay - i] (x = 0 outside the
 // record), k < ceil(n_t / q); h on the device, n_taps <= 12,288.
+// *kernel_used = 1 for the matrix-core kernel, 0 for the VALU one.
 hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
                                const double *h, int n_taps, int64_t q, int64_t delay, double *y, int64_t ys_ch,
-                               int64_t ys_t, hipStream_t st);
+                               int64_t ys_t, hipStream_t st, int *kernel_used);
 // dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.
 hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
                             int64_t dp, hipStream_t st);

@@ -3956,12 +3956,203 @@ __global__ __launch_bounds__(FD_THREADS) void k_fir_decimate(const float *__rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_fir_decimate_mfma — the same FIR decimation on the fp64 matrix cores
+// (v_mfma_f64_4x4x4_4b: 4 x 4 x 4 per block, 4 blocks per instruction).
+// Polyphase: y[o] = sum_v sum_u h_v[u] X_v[o - u], h_v[u] = h[u q + v].  For
+// 4 consecutive outputs o = 4G + i and 4 consecutive polyphase indices
+// n = 4(G - d) + k the taps form a 4 x 4 Toeplitz piece A_{v,d}[i][k] =
+// h_v[4d + i - k] that depends on (v, d) only, so
+//   Y[G] = sum_v sum_{d < D_v} A_{v,d} X_v[4(G - d) .. 4(G - d) + 3]
+// with D_v = ceil((U_v - 1)/4) + 1 (U_v = taps of phase v).  MFMA lane
+// layout (tools/check_mfma4x4.hip): A[i][k] at lane 16k + 4b + i, B[k][j] at
+// 16k + 4b + j, D[i][j] at 16i + 4b + j.  Blocks b = 4 consecutive output
+// groups, j = 4 channels: one MFMA = 16 outputs x 4 channels x 4 indices;
+// a wave owns 64 consecutive outputs (4 accumulators) of 4 channels.
+// A workgroup (NW waves) stages its 4 channels' span of input through LDS as
+// the q polyphase rows X_v (coalesced reads, zeros outside the record; row
+// starts offset so one B read — 4 rows x 16 consecutive indices — hits 64
+// distinct banks); the A pieces sit in LDS ([v][d][16 lanes]).  Each B value
+// read from LDS (one ds_read_b32 + cvt) feeds every (tile, d) pair with the
+// same index offset.  Slots of the Toeplitz pieces outside a row's taps
+// multiply neighbouring samples by 0, so a non-finite sample there would
+// poison a finite output: every non-finite result is recomputed by the
+// direct sum (SciPy's value: NaN / +-inf exactly where 0 * NaN, inf * h
+// arise), which also keeps SciPy's NaN footprint of the zero pre-pad taps.
+// ---------------------------------------------------------------------------
+constexpr int FDM_RLMOD = 4;  // row length = 4 (mod 32): staging writes <= 2-way
+template <int DM>
+__global__ __launch_bounds__(256) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
+                                                          int64_t s_ch, int64_t s_t, const double *__restrict__ h,
+                                                          int n_taps, int q, int64_t delay, int64_t n_out,
+                                                          int64_t tiles_o, int RL, double *__restrict__ y,
+                                                          int64_t ys_ch, int64_t ys_t) {
+  extern __shared__ double fdm_lds[];
+  double *At = fdm_lds;                                      // [v][d][16]
+  float *Xs = reinterpret_cast<float *>(fdm_lds + q * DM * 16);  // [j][v][RL] (+ off_j)
+  const int NW = blockDim.x >> 6;
+  const int NO = 64 * NW;  // outputs per workgroup
+  const int NN = NO + 4 * (DM - 1);
+  // XCD-aware order: consecutive output tiles of one channel group on one XCD
+  // (their input halos meet in that XCD's L2)
+  int64_t bid = blockIdx.x;
+  const int64_t nb = (int64_t)gridDim.x;
+  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  const int64_t cg = bid / tiles_o;
+  const int64_t O = (bid % tiles_o) * NO;
+  const int64_t nlo = O - 4 * (DM - 1);
+  const int64_t s0 = nlo * q + delay - (q - 1);
+  const int span = NN * q;
+  // row (j, v) starts at (j q + v) RL + off_j; off_j puts the 4 rows of one
+  // phase at banks {0, 2, 16, 18} (mod 32) so a B read is conflict-free
+  int offj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int tgt = (j & 1) * 2 + (j >> 1) * 16;
+    offj[j] = ((tgt - j * q * RL) % 32 + 32) % 32;
+  }
+  // A pieces
+  for (int e = threadIdx.x; e < q * DM * 16; e += blockDim.x) {
+    const int l16 = e & 15, vd = e >> 4;
+    const int v = vd / DM, d = vd - v * DM;
+    const int kk = l16 >> 2, ii = l16 & 3;
+    const int u = 4 * d + ii - kk;
+    const int64_t ti = (int64_t)u * q + v;
+    At[e] = (u >= 0 && ti < n_taps) ? h[ti] : 0.0;
+  }
+  // input span -> polyphase rows (8 loads in flight per thread)
+  const float rq = 1.0f / (float)q;
+  constexpr int FU = 8;
+  for (int j = 0; j < 4; ++j) {
+    const int64_t ch = cg * 4 + j;
+    const bool live = ch < n_ch;
+    const float *xr = x + (live ? ch : 0) * s_ch;
+    float *row0 = Xs + (int64_t)j * q * RL + offj[j];
+    for (int m0 = threadIdx.x; m0 < span; m0 += FU * blockDim.x) {
+      float xv8[FU];
+#pragma unroll
+      for (int e = 0; e < FU; ++e) {
+        const int m = m0 + e * blockDim.x;
+        const int64_t t = s0 + m;
+        xv8[e] = (live && m < span && t >= 0 && t < n_t) ? xr[t * s_t] : 0.0f;
+      }
+#pragma unroll
+      for (int e = 0; e < FU; ++e) {
+        const int m = m0 + e * blockDim.x;
+        if (m >= span) break;
+        int n = (int)((float)m * rq);
+        n -= n * q > m ? 1 : 0;
+        n += (n + 1) * q <= m ? 1 : 0;
+        const int v = q - 1 - (m - n * q);
+        row0[v * RL + n] = xv8[e];
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int jl = lane & 3;                            // B / D channel
+  const int lane_n = 4 * ((lane >> 2) & 3) + (lane >> 4);  // B index 4b + k
+  const int lane_a = 4 * (lane >> 4) + (lane & 3);          // A slot (k, i)
+  const float *xb = Xs + (int64_t)jl * q * RL + offj[jl] + 64 * w + lane_n;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int v = 0; v < q; ++v) {
+    // taps of phase v: U_v = ceil((n_taps - v) / q), D_v = ceil((U_v - 1)/4) + 1
+    const int Uv = (n_taps - v + q - 1) / q;
+    const int dv = Uv <= 1 ? 1 : (Uv - 1 + 3) / 4 + 1;
+    double a[DM];
+#pragma unroll
+    for (int d = 0; d < DM; ++d) a[d] = At[(v * DM + d) * 16 + lane_a];
+    const float *xv = xb + v * RL;
+#pragma unroll
+    for (int sidx = 0; sidx < DM + 12; ++sidx) {
+      // index offset 4 sidx: tile t, step d with 4t - d + DM - 1 = sidx
+      bool need = false;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int d = 4 * t + DM - 1 - sidx;
+        need = need || (d >= 0 && d < DM && d < dv);
+      }
+      if (!need) continue;
+      const double bv = (double)xv[4 * sidx];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int d = 4 * t + DM - 1 - sidx;
+        if (d >= 0 && d < DM && d < dv) acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[d], bv, acc[t], 0, 0, 0);
+      }
+    }
+  }
+  const int64_t ch = cg * 4 + jl;
+  const int io = lane >> 4, bo = (lane >> 2) & 3;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int64_t o = O + 64 * w + 16 * t + 4 * bo + io;
+    if (ch >= n_ch || o >= n_out) continue;
+    double val = acc[t];
+    if (!isfinite(val)) {
+      // direct sum (rare: a non-finite sample within reach of this output)
+      const float *xr = x + ch * s_ch;
+      double a2 = 0.0;
+      for (int i = 0; i < n_taps; ++i) {
+        const int64_t tt = o * q + delay - i;
+        if (tt >= 0 && tt < n_t) a2 = fma(h[i], (double)xr[tt * s_t], a2);
+      }
+      val = a2;
+    }
+    y[ch * ys_ch + o * ys_t] = val;
+  }
+}
+
 hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
                                const double *h, int n_taps, int64_t q, int64_t delay, double *y, int64_t ys_ch,
-                               int64_t ys_t, hipStream_t st) {
+                               int64_t ys_t, hipStream_t st, int *kernel_used) {
   const int64_t n_out = (n_t + q - 1) / q;
   if (n_taps < 1 || q < 1 || q > (1 << 20) || n_out < 1) return hipErrorInvalidValue;
   const int U = (int)((n_taps + q - 1) / q);  // taps per polyphase branch
+  // matrix-core path: D_0 = ceil((U - 1)/4) + 1 <= 8 Toeplitz steps
+  const int D0 = U <= 1 ? 1 : (U - 1 + 3) / 4 + 1;
+  if (D0 <= 8 && !getenv_flag("LFD_FIR_VALU")) {
+    for (int NW = 4; NW >= 1; NW >>= 1) {
+      const int DM = D0 < 2 ? 2 : D0;
+      const int NN = 64 * NW + 4 * (DM - 1);
+      int RL = NN + 31;
+      RL += ((FDM_RLMOD - RL) % 32 + 32) % 32;
+      const size_t lds = sizeof(double) * (size_t)q * DM * 16 + sizeof(float) * (size_t)4 * q * RL;
+      // >= 2 workgroups per CU, else the VALU kernel (long decimation factors)
+      if (lds > 64 * 1024 && NW > 1) continue;
+      if (lds > 80 * 1024) break;
+      const int64_t tiles_o = (n_out + 64 * NW - 1) / (64 * NW);
+      const int64_t grid = (n_ch + 3) / 4 * tiles_o;
+      if (grid > (int64_t)INT32_MAX) break;
+      hipError_t e = hipSuccess;
+#define LFD_FDM(DMV)                                                                                        \
+  case DMV: {                                                                                              \
+    static bool attr = false;                                                                              \
+    if (!attr) {                                                                                           \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<DMV>),                   \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                     \
+      if (e != hipSuccess) return e;                                                                       \
+      attr = true;                                                                                         \
+    }                                                                                                      \
+    k_fir_decimate_mfma<DMV><<<(unsigned)grid, 64 * NW, lds, st>>>(x, n_ch, n_t, s_ch, s_t, h, n_taps,      \
+                                                                   (int)q, delay, n_out, tiles_o, RL, y,   \
+                                                                   ys_ch, ys_t);                           \
+    break;                                                                                                 \
+  }
+      switch (DM) {
+        LFD_FDM(2)
+        LFD_FDM(3)
+        LFD_FDM(4)
+        LFD_FDM(5)
+        LFD_FDM(6)
+        LFD_FDM(7)
+        LFD_FDM(8)
+        default: return hipErrorInvalidValue;
+      }
+#undef LFD_FDM
+      if (kernel_used) *kernel_used = 1;
+      return hipGetLastError();
+    }
+  }
   // outputs per tile: q rows of (to + U) staged floats (odd row length) in LDS
   const int64_t cap = std::min<int64_t>(16 * 1024 / q, FD_LDS / 4 / q) - U - 2;  // span <= 16 K samples
   if (cap < 1) return hipErrorInvalidValue;
@@ -3980,6 +4171,7 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
   k_fir_decimate<<<(unsigned)(n_ch * tiles), FD_THREADS, lds, st>>>(x, n_t, s_ch, s_t, h, n_taps, (int)q, delay,
                                                                      n_out, (int)tiles, to, U, rowlen, y, ys_ch,
                                                                      ys_t);
+  if (kernel_used) *kernel_used = 0;
   return hipGetLastError();
 }
 

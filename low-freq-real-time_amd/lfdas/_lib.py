@@ -136,6 +136,7 @@ def load():
         "lfd_rolling_mean_f32": ([vp, i64, i64, i64, i64, i64, i64, vp, i64, i64,
                                   vp], i32),
         "lfd_fir_decimate_f32": ([vp, i64, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64, vp], i32),
+        "lfd_fir_decimate_last_kernel": ([], i32),
         "lfd_lfproc_schedule": ([i64, i64, i64, vp, i64, P(i64)], i32),
         "lfd_demean_scale_f64": ([vp, i64, i64, i64, i64, i64, i64, ctypes.c_double, vp, i64, i64, vp], i32),
         "lfd_median_filter_f64": ([vp, i64, i64, i64, i64, i32, i32, vp, i64, i64, vp], i32),
@@ -171,7 +172,7 @@ EXPORTED = (
     "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_debug_runs",
     "lfd_sos_filtfilt_resample_f32",
     "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32", "lfd_sosfiltfilt_last_timing",
-    "lfd_interp_linear_f64", "lfd_rolling_mean_f32", "lfd_fir_decimate_f32",
+    "lfd_interp_linear_f64", "lfd_rolling_mean_f32", "lfd_fir_decimate_f32", "lfd_fir_decimate_last_kernel",
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",

@@ -189,3 +189,41 @@ def test_decimate_fir_device(q, layout):
     refn = oracle.decimate_fir(xn.astype(np.float64), q)
     np.testing.assert_array_equal(np.isnan(dn), np.isnan(refn))
     assert np.isnan(dn).sum() > 0
+    if q <= 10:  # firwin(20q+1) polyphase pieces fit the matrix-core kernel
+        from lfdas._lib import load
+        assert load().lfd_fir_decimate_last_kernel() == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [3, 10])
+def test_decimate_fir_device_nulls_and_ragged(q):
+    """Matrix-core FIR decimation on a ragged array (6 channels: one
+    partial 4-channel group; several 256-output tiles) with NaN / +-inf
+    samples at tile edges, inside the zero pre-pad taps' reach and in the
+    Toeplitz corners: the NaN / inf footprint and every finite value match
+    the oracle (relRMS 1e-12 over finite outputs)."""
+    import torch
+    from lfdas._lib import load
+    from lfdas.plan import fir_decimate_device
+    from lfdas.proc import fir_decimate_design
+    rng = np.random.default_rng(7 + q)
+    n_ch, n_t = 6, 256 * q * 3 + 17 * q + 5
+    x = rng.standard_normal((n_ch, n_t)).astype(np.float32)
+    tile = 256 * q
+    x[0, tile - 1] = np.nan
+    x[1, tile] = np.inf
+    x[2, 2 * tile + 3] = -np.inf
+    x[3, 5] = np.nan
+    x[4, n_t - 1] = np.nan
+    x[5, 1000] = np.inf
+    x[5, 1000 + q] = -np.inf  # +inf and -inf in one window -> NaN
+    taps, delay = fir_decimate_design(q)
+    y = fir_decimate_device(torch.from_numpy(x).cuda(), taps, q, delay).cpu().numpy()
+    assert load().lfd_fir_decimate_last_kernel() == 1
+    ref = oracle.decimate_fir(x.astype(np.float64), q)
+    assert y.shape == ref.shape
+    np.testing.assert_array_equal(np.isnan(y), np.isnan(ref))
+    np.testing.assert_array_equal(np.isposinf(y), np.isposinf(ref))
+    np.testing.assert_array_equal(np.isneginf(y), np.isneginf(ref))
+    f = np.isfinite(ref)
+    assert _rel(y[f], ref[f]) < 1e-12

@@ -12,6 +12,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from lfdas.plan import fir_decimate_device  # noqa: E402
 from lfdas.proc import fir_decimate_design  # noqa: E402
+from lfdas._lib import load  # noqa: E402
 
 n_ch, n = 2000, 600_000
 x = torch.empty((n_ch, n), dtype=torch.float32, device="cuda")
@@ -28,5 +29,6 @@ for q in (2, 5, 10, 50):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 5
     alg = n_ch * n * (4 + 8 / q)
-    print(f"q={q:3d} taps={taps.size:5d} {ms:.3f} ms  {alg / ms / 1e6:.0f} GB/s  frac {alg / ms / 1e6 / 8000:.3f}  "
+    kern = "mfma" if load().lfd_fir_decimate_last_kernel() == 1 else "valu"
+    print(f"{kern} q={q:3d} taps={taps.size:5d} {ms:.3f} ms  {alg / ms / 1e6:.0f} GB/s  frac {alg / ms / 1e6 / 8000:.3f}  "
           f"{n_ch * n * taps.size / q / ms / 1e9:.1f} TFMA/s", flush=True)
