@@ -196,7 +196,7 @@ int lfd_fir_decimate_f32(const float *x, int64_t n_ch, int64_t n_t,
                          int64_t n_taps, int64_t q, int64_t delay, double *y,
                          int64_t ys_ch, int64_t ys_t, void *stream);
 /* Kernel of this thread's last lfd_fir_decimate_f32: 1 = fp64 matrix cores
- * (k_fir_decimate_mfma, taps with ceil((ceil(n_taps/q) - 1)/4) <= 7),
+ * (k_fir_decimate_mfma: time-contiguous rows, q in {4, 5, 6, 8, 10}, n_taps <= 21q + 1),
  * 0 = the VALU kernel (longer filters, or LFD_FIR_VALU=1), -1 = none yet. */
 int lfd_fir_decimate_last_kernel(void);
 

@@ -3980,125 +3980,164 @@ __global__ __launch_bounds__(FD_THREADS) void k_fir_decimate(const float *__rest
 // direct sum (SciPy's value: NaN / +-inf exactly where 0 * NaN, inf * h
 // arise), which also keeps SciPy's NaN footprint of the zero pre-pad taps.
 // ---------------------------------------------------------------------------
-constexpr int FDM_RLMOD = 4;  // row length = 4 (mod 32): staging writes <= 2-way
-template <int DM>
-__global__ __launch_bounds__(256) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
-                                                          int64_t s_ch, int64_t s_t, const double *__restrict__ h,
-                                                          int n_taps, int q, int64_t delay, int64_t n_out,
-                                                          int64_t tiles_o, int RL, double *__restrict__ y,
-                                                          int64_t ys_ch, int64_t ys_t) {
+// Compile-time geometry per decimation factor Q: DM = 6 Toeplitz steps cover
+// taps u <= 20 of every phase and u = 21 for rows i >= 1; the one tap
+// h[21 Q] (phase 0, u = 21: decimate's firwin(20Q+1) behind its Q pre-pad
+// zeros has n_taps = 21Q + 1) of row-0 outputs is added in the epilogue.
+constexpr int FDM_DM = 6;
+constexpr int FDM_NO = 256;                          // outputs per tile: 4 waves x 64
+constexpr int FDM_NN = FDM_NO + 4 * (FDM_DM - 1) + 1;  // polyphase indices per tile (+1: the u = 21 tap)
+// row length >= NN and = +-4 (mod 32): staging writes <= 2-way conflicts
+constexpr int fdm_rl() {
+  const int a = FDM_NN + ((4 - FDM_NN) % 32 + 32) % 32, b = FDM_NN + ((28 - FDM_NN) % 32 + 32) % 32;
+  return a < b ? a : b;
+}
+template <int Q>
+constexpr size_t fdm_lds_bytes() {
+  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32);
+}
+template <int Q>
+__global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
+                                                          int64_t s_ch, const double *__restrict__ h, int n_taps,
+                                                          int64_t delay, int64_t n_out, int64_t tiles_o, int strip,
+                                                          double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
+                                                          int diag) {
+  constexpr int DM = FDM_DM, NO = FDM_NO, NN = FDM_NN, RL = fdm_rl();
+  constexpr int SPAN = NN * Q;             // samples per channel and tile
+  constexpr int NR = (SPAN + 63) / 64;     // staging loads per lane
+  constexpr int JB = Q * RL + 32;          // j-block stride (floats)
   extern __shared__ double fdm_lds[];
-  double *At = fdm_lds;                                      // [v][d][16]
-  float *Xs = reinterpret_cast<float *>(fdm_lds + q * DM * 16);  // [j][v][RL] (+ off_j)
-  const int NW = blockDim.x >> 6;
-  const int NO = 64 * NW;  // outputs per workgroup
-  const int NN = NO + 4 * (DM - 1);
-  // XCD-aware order: consecutive output tiles of one channel group on one XCD
-  // (their input halos meet in that XCD's L2)
+  double *At = fdm_lds;                                          // [v][d][16]
+  float *Xs = reinterpret_cast<float *>(fdm_lds + Q * DM * 16);  // [j][v][RL] (+ off_j)
+  // a workgroup walks `strip` consecutive tiles of one 4-channel group; the
+  // next tile's input is loaded into registers while the current one computes
+  const int64_t n_strips = (tiles_o + strip - 1) / strip;
   int64_t bid = blockIdx.x;
   const int64_t nb = (int64_t)gridDim.x;
+  // XCD-aware order: consecutive strips of one channel group on one XCD
+  // (their input halos meet in that XCD's L2)
   if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
-  const int64_t cg = bid / tiles_o;
-  const int64_t O = (bid % tiles_o) * NO;
-  const int64_t nlo = O - 4 * (DM - 1);
-  const int64_t s0 = nlo * q + delay - (q - 1);
-  const int span = NN * q;
-  // row (j, v) starts at (j q + v) RL + off_j; off_j puts the 4 rows of one
-  // phase at banks {0, 2, 16, 18} (mod 32) so a B read is conflict-free
-  int offj[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int tgt = (j & 1) * 2 + (j >> 1) * 16;
-    offj[j] = ((tgt - j * q * RL) % 32 + 32) % 32;
-  }
-  // A pieces
-  for (int e = threadIdx.x; e < q * DM * 16; e += blockDim.x) {
+  const int64_t cg = bid / n_strips;
+  const int64_t t_begin = (bid % n_strips) * strip;
+  const int64_t t_end = t_begin + strip < tiles_o ? t_begin + strip : tiles_o;
+  // row (j, v) starts at j JB + v RL + off_j; off_j puts the 4 rows of one
+  // phase at banks {0, 2, 16, 18} (mod 32): a B read is conflict-free
+  auto offj = [](int j) { return (((j & 1) * 2 + (j >> 1) * 16 - j * JB) % 32 + 32) % 32; };
+  for (int e = threadIdx.x; e < Q * DM * 16; e += blockDim.x) {
     const int l16 = e & 15, vd = e >> 4;
     const int v = vd / DM, d = vd - v * DM;
     const int kk = l16 >> 2, ii = l16 & 3;
     const int u = 4 * d + ii - kk;
-    const int64_t ti = (int64_t)u * q + v;
+    const int64_t ti = (int64_t)u * Q + v;
     At[e] = (u >= 0 && ti < n_taps) ? h[ti] : 0.0;
   }
-  // input span -> polyphase rows (8 loads in flight per thread)
-  const float rq = 1.0f / (float)q;
-  constexpr int FU = 8;
-  for (int j = 0; j < 4; ++j) {
-    const int64_t ch = cg * 4 + j;
-    const bool live = ch < n_ch;
-    const float *xr = x + (live ? ch : 0) * s_ch;
-    float *row0 = Xs + (int64_t)j * q * RL + offj[j];
-    for (int m0 = threadIdx.x; m0 < span; m0 += FU * blockDim.x) {
-      float xv8[FU];
-#pragma unroll
-      for (int e = 0; e < FU; ++e) {
-        const int m = m0 + e * blockDim.x;
-        const int64_t t = s0 + m;
-        xv8[e] = (live && m < span && t >= 0 && t < n_t) ? xr[t * s_t] : 0.0f;
-      }
-#pragma unroll
-      for (int e = 0; e < FU; ++e) {
-        const int m = m0 + e * blockDim.x;
-        if (m >= span) break;
-        int n = (int)((float)m * rq);
-        n -= n * q > m ? 1 : 0;
-        n += (n + 1) * q <= m ? 1 : 0;
-        const int v = q - 1 - (m - n * q);
-        row0[v * RL + n] = xv8[e];
-      }
-    }
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int jl = lane & 3;                            // B / D channel
-  const int lane_n = 4 * ((lane >> 2) & 3) + (lane >> 4);  // B index 4b + k
-  const int lane_a = 4 * (lane >> 4) + (lane & 3);          // A slot (k, i)
-  const float *xb = Xs + (int64_t)jl * q * RL + offj[jl] + 64 * w + lane_n;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int v = 0; v < q; ++v) {
-    // taps of phase v: U_v = ceil((n_taps - v) / q), D_v = ceil((U_v - 1)/4) + 1
-    const int Uv = (n_taps - v + q - 1) / q;
-    const int dv = Uv <= 1 ? 1 : (Uv - 1 + 3) / 4 + 1;
-    double a[DM];
+  // staging: wave w loads channel w of the group, sample m = lane + 64 r of
+  // the tile's span, polyphase row v = Q - 1 - m % Q, index m / Q
+  const int64_t ch_ld = cg * 4 + w;
+  const bool live = ch_ld < n_ch;
+  const float *xr_ld = x + (live ? ch_ld : 0) * s_ch;
+  float *row_ld = Xs + w * JB + offj(w);
+  float pf[NR];
+  auto issue = [&](int64_t Ot) {
+    const int64_t s0 = (Ot - 4 * (DM - 1) - 1) * Q + delay - (Q - 1);
+    if (live && s0 >= 0 && s0 + 64 * NR <= n_t) {
+      const float *p = xr_ld + s0 + lane;
 #pragma unroll
-    for (int d = 0; d < DM; ++d) a[d] = At[(v * DM + d) * 16 + lane_a];
-    const float *xv = xb + v * RL;
+      for (int r = 0; r < NR; ++r) pf[r] = p[64 * r];
+    } else {  // record edges / channels past n_ch: clamped loads, zeros outside
 #pragma unroll
-    for (int sidx = 0; sidx < DM + 12; ++sidx) {
-      // index offset 4 sidx: tile t, step d with 4t - d + DM - 1 = sidx
-      bool need = false;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int d = 4 * t + DM - 1 - sidx;
-        need = need || (d >= 0 && d < DM && d < dv);
-      }
-      if (!need) continue;
-      const double bv = (double)xv[4 * sidx];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int d = 4 * t + DM - 1 - sidx;
-        if (d >= 0 && d < DM && d < dv) acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[d], bv, acc[t], 0, 0, 0);
+      for (int r = 0; r < NR; ++r) {
+        const int64_t t = s0 + lane + 64 * r;
+        const int64_t tc = t < 0 ? 0 : (t >= n_t ? n_t - 1 : t);
+        const float v = xr_ld[tc];
+        pf[r] = (live && t >= 0 && t < n_t) ? v : 0.0f;
       }
     }
-  }
+  };
+  auto commit = [&]() {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // recomputed per tile, not hoisted into registers
+    const int n_l = ln / Q, r_l = ln - n_l * Q;
+    float *a0 = row_ld + (Q - 1 - r_l) * RL + n_l;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int c = (64 * r) % Q, f = (64 * r) / Q;
+      const bool carry = r_l + c >= Q;
+      float *dst = a0 + (f - c * RL) + (carry ? Q * RL + 1 : 0);
+      if (64 * (r + 1) <= SPAN || ln + 64 * r < SPAN) *dst = pf[r];
+    }
+  };
+  const int jl = lane & 3;                                  // B / D channel
+  const int lane_n = 4 * ((lane >> 2) & 3) + (lane >> 4);  // B index 4b + k
+  const int lane_a = 4 * (lane >> 4) + (lane & 3);         // A slot (k, i)
   const int64_t ch = cg * 4 + jl;
   const int io = lane >> 4, bo = (lane >> 2) & 3;
+  const float *xb = Xs + jl * JB + offj(jl) + 64 * w + lane_n + 1;
+  // phase 0's tap u = 21 (row-0 outputs only): X_0[o - 21] at index 64 w + 16 t + 4 b
+  const double h21 = (io == 0 && 21 * Q < n_taps) ? h[21 * Q] : 0.0;
+  const float *x21 = Xs + jl * JB + offj(jl) + 64 * w + 4 * ((lane >> 2) & 3);
+  // diag (LFD_FIR_DIAG, timing breakdowns only): 1 = staging without the
+  // MFMA phase loop, 2 = MFMA phase loop without the staging
+  if (diag != 2) issue(t_begin * NO);
+  for (int64_t tt = t_begin; tt < t_end; ++tt) {
+    __syncthreads();  // the previous tile's reads of X are done
+    if (diag != 2) commit();
+    __syncthreads();
+    if (tt + 1 < t_end && diag != 2) issue((tt + 1) * NO);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (diag != 1) {
+      // phase v: acc[t] += sum_d A_{v,d} B(index offset 4 (4t + DM - 1 - d));
+      // the next phase's A / B values load while this phase's MFMAs run
+      constexpr int NB = DM + 12;
+      double an[DM];
+      float bn[NB];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int64_t o = O + 64 * w + 16 * t + 4 * bo + io;
-    if (ch >= n_ch || o >= n_out) continue;
-    double val = acc[t];
-    if (!isfinite(val)) {
-      // direct sum (rare: a non-finite sample within reach of this output)
-      const float *xr = x + ch * s_ch;
-      double a2 = 0.0;
-      for (int i = 0; i < n_taps; ++i) {
-        const int64_t tt = o * q + delay - i;
-        if (tt >= 0 && tt < n_t) a2 = fma(h[i], (double)xr[tt * s_t], a2);
+      for (int d = 0; d < DM; ++d) an[d] = At[d * 16 + lane_a];
+#pragma unroll
+      for (int si = 0; si < NB; ++si) bn[si] = xb[4 * si];
+#pragma unroll
+      for (int v = 0; v < Q; ++v) {
+        double ac[DM], bd[NB];
+#pragma unroll
+        for (int d = 0; d < DM; ++d) ac[d] = an[d];
+#pragma unroll
+        for (int si = 0; si < NB; ++si) bd[si] = (double)bn[si];
+        if (v + 1 < Q) {
+#pragma unroll
+          for (int d = 0; d < DM; ++d) an[d] = At[((v + 1) * DM + d) * 16 + lane_a];
+#pragma unroll
+          for (int si = 0; si < NB; ++si) bn[si] = xb[(v + 1) * RL + 4 * si];
+        }
+        // the four tiles' accumulators alternate: dependent MFMAs sit 4 apart
+#pragma unroll
+        for (int d = DM - 1; d >= 0; --d) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(ac[d], bd[4 * t + DM - 1 - d], acc[t], 0, 0, 0);
+        }
       }
-      val = a2;
     }
-    y[ch * ys_ch + o * ys_t] = val;
+    const int64_t O = tt * NO;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int64_t o = O + 64 * w + 16 * t + 4 * bo + io;
+      if (ch >= n_ch || o >= n_out) continue;
+      double val = fma(h21, (double)x21[16 * t], acc[t]);
+      if (!isfinite(val)) {
+        // direct sum (rare: a non-finite sample within reach of this output)
+        const float *xr = x + ch * s_ch;
+        double a2 = 0.0;
+        for (int i = 0; i < n_taps; ++i) {
+          const int64_t ts = o * Q + delay - i;
+          if (ts >= 0 && ts < n_t) a2 = fma(h[i], (double)xr[ts], a2);
+        }
+        val = a2;
+      }
+      y[ch * ys_ch + o * ys_t] = val;
+    }
   }
 }
 
@@ -4108,47 +4147,45 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
   const int64_t n_out = (n_t + q - 1) / q;
   if (n_taps < 1 || q < 1 || q > (1 << 20) || n_out < 1) return hipErrorInvalidValue;
   const int U = (int)((n_taps + q - 1) / q);  // taps per polyphase branch
-  // matrix-core path: D_0 = ceil((U - 1)/4) + 1 <= 8 Toeplitz steps
-  const int D0 = U <= 1 ? 1 : (U - 1 + 3) / 4 + 1;
-  if (D0 <= 8 && !getenv_flag("LFD_FIR_VALU")) {
-    for (int NW = 4; NW >= 1; NW >>= 1) {
-      const int DM = D0 < 2 ? 2 : D0;
-      const int NN = 64 * NW + 4 * (DM - 1);
-      int RL = NN + 31;
-      RL += ((FDM_RLMOD - RL) % 32 + 32) % 32;
-      const size_t lds = sizeof(double) * (size_t)q * DM * 16 + sizeof(float) * (size_t)4 * q * RL;
-      // >= 2 workgroups per CU, else the VALU kernel (long decimation factors)
-      if (lds > 64 * 1024 && NW > 1) continue;
-      if (lds > 80 * 1024) break;
-      const int64_t tiles_o = (n_out + 64 * NW - 1) / (64 * NW);
-      const int64_t grid = (n_ch + 3) / 4 * tiles_o;
-      if (grid > (int64_t)INT32_MAX) break;
-      hipError_t e = hipSuccess;
-#define LFD_FDM(DMV)                                                                                        \
-  case DMV: {                                                                                              \
-    static bool attr = false;                                                                              \
-    if (!attr) {                                                                                           \
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<DMV>),                   \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                     \
-      if (e != hipSuccess) return e;                                                                       \
-      attr = true;                                                                                         \
-    }                                                                                                      \
-    k_fir_decimate_mfma<DMV><<<(unsigned)grid, 64 * NW, lds, st>>>(x, n_ch, n_t, s_ch, s_t, h, n_taps,      \
-                                                                   (int)q, delay, n_out, tiles_o, RL, y,   \
-                                                                   ys_ch, ys_t);                           \
-    break;                                                                                                 \
+  // matrix-core path (time-contiguous rows, q in {4, 5, 6, 8, 10}, phase 0
+  // at most 22 taps, the others 21: n_taps <= 21 q + 1)
+  if (s_t == 1 && n_taps <= 21 * q + 1 && !getenv_flag("LFD_FIR_VALU")) {
+    const int64_t tiles_o = (n_out + FDM_NO - 1) / FDM_NO;
+    int strip = 8;
+    if (const char *sv = std::getenv("LFD_FIR_STRIP")) strip = std::max(1, std::atoi(sv));
+    if (strip > tiles_o) strip = (int)tiles_o;
+    const int64_t grid = (n_ch + 3) / 4 * ((tiles_o + strip - 1) / strip);
+    int diag = 0;
+    if (const char *dv = std::getenv("LFD_FIR_DIAG")) diag = std::atoi(dv);
+    bool launched = false;
+    hipError_t e = hipSuccess;
+#define LFD_FDM(QV)                                                                                          \
+  case QV: {                                                                                                 \
+    static bool attr = false;                                                                                \
+    if (!attr) {                                                                                             \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV>());         \
+      if (e != hipSuccess) return e;                                                                         \
+      attr = true;                                                                                           \
+    }                                                                                                        \
+    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdm_lds_bytes<QV>(), st>>>(x, n_ch, n_t, s_ch, h, n_taps, \
+                                                                              delay, n_out, tiles_o, strip,  \
+                                                                              y, ys_ch, ys_t, diag);         \
+    launched = true;                                                                                         \
+    break;                                                                                                   \
   }
-      switch (DM) {
-        LFD_FDM(2)
-        LFD_FDM(3)
+    if (grid <= (int64_t)INT32_MAX) {
+      switch (q) {
         LFD_FDM(4)
         LFD_FDM(5)
         LFD_FDM(6)
-        LFD_FDM(7)
         LFD_FDM(8)
-        default: return hipErrorInvalidValue;
+        LFD_FDM(10)
+        default: break;
       }
+    }
 #undef LFD_FDM
+    if (launched) {
       if (kernel_used) *kernel_used = 1;
       return hipGetLastError();
     }
@@ -4160,7 +4197,7 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
   const int rowlen = (to + U) | 1;
   const int64_t tiles = (n_out + to - 1) / to;
   if (n_ch * tiles > (int64_t)INT32_MAX) return hipErrorInvalidValue;
-  const size_t lds = sizeof(float) * (size_t)q * rowlen;
+  const size_t lds_v = sizeof(float) * (size_t)q * rowlen;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate),
@@ -4168,7 +4205,7 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_fir_decimate<<<(unsigned)(n_ch * tiles), FD_THREADS, lds, st>>>(x, n_t, s_ch, s_t, h, n_taps, (int)q, delay,
+  k_fir_decimate<<<(unsigned)(n_ch * tiles), FD_THREADS, lds_v, st>>>(x, n_t, s_ch, s_t, h, n_taps, (int)q, delay,
                                                                      n_out, (int)tiles, to, U, rowlen, y, ys_ch,
                                                                      ys_t);
   if (kernel_used) *kernel_used = 0;

@@ -189,13 +189,13 @@ def test_decimate_fir_device(q, layout):
     refn = oracle.decimate_fir(xn.astype(np.float64), q)
     np.testing.assert_array_equal(np.isnan(dn), np.isnan(refn))
     assert np.isnan(dn).sum() > 0
-    if q <= 10:  # firwin(20q+1) polyphase pieces fit the matrix-core kernel
+    if 4 <= q <= 10 and layout == "row":  # time-contiguous rows, firwin(20q+1) pieces fit the matrix-core kernel
         from lfdas._lib import load
         assert load().lfd_fir_decimate_last_kernel() == 1
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("q", [3, 10])
+@pytest.mark.parametrize("q", [4, 10])
 def test_decimate_fir_device_nulls_and_ragged(q):
     """Matrix-core FIR decimation on a ragged array (6 channels: one
     partial 4-channel group; several 256-output tiles) with NaN / +-inf
