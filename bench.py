@@ -512,6 +512,58 @@ def bench_ooc_cfg5_sharded(dev, ws, rank, barrier, max_over_ranks, n_ch=50_000, 
                       "pass": bool(all_ok > 0.5), "checker": "oracle.lfproc_process (untimed)"}}
 
 
+def bench_fir_decimate(dev, q=10, n_ch=2000, n=600_000, fs=1000.0, reps=10):
+    """Patch.decimate(time=q, filter_type='fir') (scipy.signal.decimate
+    ftype='fir': firwin(20q+1, 1/q) via resample_poly): 2,000 ch x 10 min @
+    1 kHz float32 -> float64 at fs/q.  Algorithmic bytes 4 + 8/q per input
+    sample; kernel k_fir_decimate_mfma (fp64 matrix cores)."""
+    import torch
+    import oracle
+    from lfdas._lib import load
+    from lfdas.plan import fir_decimate_device
+    from lfdas.proc import fir_decimate_design
+    taps, delay = fir_decimate_design(q)
+    x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
+    synth_fill(x, fs, 91)
+    h = torch.as_tensor(taps).to(dev)
+    y = torch.empty((n_ch, -(-n // q)), dtype=torch.float64, device=dev)
+    lib = load()
+    stream = torch.cuda.current_stream(dev)
+
+    from lfdas._lib import check
+    from lfdas.plan import _ptr
+
+    def run():
+        check(lib.lfd_fir_decimate_f32(_ptr(x), n_ch, n, x.stride(0), x.stride(1), _ptr(h), h.numel(), q, delay,
+                                       _ptr(y), y.stride(0), y.stride(1), stream.cuda_stream))
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    kern = "k_fir_decimate_mfma" if lib.lfd_fir_decimate_last_kernel() == 1 else "k_fir_decimate"
+    gbs = n_ch * n * (4 + 8 / q) / (ms * 1e-3) / 1e9
+    # parity spot check outside the timed region (2 channels vs the oracle)
+    rows = [0, n_ch - 1]
+    ref = oracle.decimate_fir(x[rows].double().cpu().numpy(), q)
+    got = y[rows].cpu().numpy()
+    rel = float(np.sqrt(np.sum((got - ref) ** 2) / np.sum(ref ** 2)))
+    del x, y, h
+    torch.cuda.empty_cache()
+    return {"value": n_ch * n / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms, "kernel": kern,
+            "config": f"{n_ch:,} ch x {n:,} @ {fs:g} Hz fp32 -> f64, decimate(time={q}, filter_type='fir'), "
+                      f"{taps.size} taps",
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_sample": 4 + 8 / q},
+            "relrms_vs_oracle_2ch": rel}
+
+
 def bench_rolling(dev, W, S_, reps=10):
     """cfg2 rolling mean (5,000 ch x 10 min @ 1 kHz), window W, step S_;
     algorithmic bytes 4 + 4/S per channel-sample."""
@@ -859,6 +911,7 @@ def main():
         secondary["shard_widths_1gpu"] = shards
     if ws == 1 and not args.no_extra:
         secondary["fullrate_bandpass"] = bench_fullrate(dev)
+        secondary["fir_decimate_q10"] = bench_fir_decimate(dev)
     if not args.no_rolling and ws == 1:
         secondary["rolling_mean_cfg2"] = bench_rolling(dev, 1000, 1000)
         secondary["rolling_mean_cfg2_step1"] = bench_rolling(dev, 1000, 1, reps=5)

@@ -3178,7 +3178,7 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   if (const char *v = std::getenv("LFD_TM_X2")) x2 = x2_ok && std::atoi(v) != 0;
   bool m4 = false;
   if (const char *v = std::getenv("LFD_TM_M4")) m4 = std::atoi(v) != 0;
-  if (m4 && x2 && !swap && ntile == 2) {
+  if (m4 && x2 && !swap && ntile == 2 && (std::getenv("LFD_TM_PF") || std::getenv("LFD_TM_NT"))) {
     if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, true>, 512);
     if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true>, 512);
     return hipErrorInvalidValue;
@@ -3187,7 +3187,7 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   // time-major (in-process A/B, tools/ab_plan.py --tm; bit-identical)
   bool buf = !std::getenv("LFD_TM_PF") && !std::getenv("LFD_TM_NT");
   if (const char *v = std::getenv("LFD_TM_BUF")) buf = std::atoi(v) != 0;
-  if (buf && x2 && !swap && ntile == 2 && !m4 && s_t < (int64_t)1 << 22) {
+  if (buf && x2 && !swap && ntile == 2 && s_t < (int64_t)1 << 22) {
     const int pfb = std::getenv("LFD_TM_PF") ? pf : 1;
     int mode = 0;
     if (const char *v = std::getenv("LFD_TM_MODE")) mode = std::atoi(v);
@@ -3204,6 +3204,8 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
     if (const char *v = std::getenv("LFD_TM_SEPI")) sepi = std::atoi(v) != 0;
     if (sepi && nt == 512) {
       lds = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
+      // (LFD_TM_M4=1: v_mfma_f64_4x4x4 steps, a third less matrix-core issue time)
+      if (m4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true, true, 0, true>, 512);
       if (pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 0, true>, 512);
       return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
     }
@@ -4081,14 +4083,17 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
   const float *x21 = Xs + jl * JB + offj(jl) + 64 * w + 4 * ((lane >> 2) & 3);
   // diag (LFD_FIR_DIAG, timing breakdowns only): 1 = staging without the
   // MFMA phase loop, 2 = MFMA phase loop without the staging
-  if (diag != 2) issue(t_begin * NO);
+  if ((diag & 3) != 2) issue(t_begin * NO);
   for (int64_t tt = t_begin; tt < t_end; ++tt) {
     __syncthreads();  // the previous tile's reads of X are done
-    if (diag != 2) commit();
+    if ((diag & 3) != 2) commit();
     __syncthreads();
-    if (tt + 1 < t_end && diag != 2) issue((tt + 1) * NO);
+    // (diag bit 4: the next tile's loads issued half-way through the phases)
+    const bool pf_next = tt + 1 < t_end && (diag & 3) != 2;
+    if (pf_next && !(diag & 4)) issue((tt + 1) * NO);
+    if (diag & 8) __builtin_amdgcn_s_setprio(2);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (diag != 1) {
+    if ((diag & 3) != 1) {
       // phase v: acc[t] += sum_d A_{v,d} B(index offset 4 (4t + DM - 1 - d));
       // the next phase's A / B values load while this phase's MFMAs run
       constexpr int NB = DM + 12;
@@ -4105,6 +4110,7 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
         for (int d = 0; d < DM; ++d) ac[d] = an[d];
 #pragma unroll
         for (int si = 0; si < NB; ++si) bd[si] = (double)bn[si];
+        if (v == Q / 2 && pf_next && (diag & 4)) issue((tt + 1) * NO);
         if (v + 1 < Q) {
 #pragma unroll
           for (int d = 0; d < DM; ++d) an[d] = At[((v + 1) * DM + d) * 16 + lane_a];
@@ -4120,6 +4126,7 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
         }
       }
     }
+    if (diag & 8) __builtin_amdgcn_s_setprio(0);
     const int64_t O = tt * NO;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
