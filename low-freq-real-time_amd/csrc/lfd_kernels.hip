@@ -951,6 +951,8 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 // float4 reads conflict-free) and y leaves through LDS as row stores.
 // ---------------------------------------------------------------------------
 typedef double fr_d4v __attribute__((ext_vector_type(4)));
+// LFD_FR_STAGE_OLD=1 (A/B knob): the big block's loads in groups of 8 dwords
+__constant__ int g_fr_stage_old = 0;
 #ifndef FRS_Q
 // k_fullrate_scan: big blocks per load batch (8: 0.83 ms vs 0.91 at 4 on the
 // 2,000 x 600,000 band-pass; a software-pipelined next batch spills and is
@@ -980,9 +982,23 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
   const int64_t a = k * L;
   {
+    // every load of the big block issued before the first LDS write (8 KB
+    // per wave in flight, one memory latency per block); time-contiguous,
+    // 16-B aligned rows as float4 (1 KB per instruction)
     const float *row = x + ch * s_ch + a * s_t;
+    if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !g_fr_stage_old) {
+      float4 v[L / 256];
+#pragma unroll
+      for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
+#pragma unroll
+      for (int i = 0; i < L / 256; ++i) {
+        const int u = 4 * lane + 256 * i;
+        *reinterpret_cast<float4 *>(tile + u + 4 * (u >> 5)) = v[i];
+      }
+    } else {
 #pragma unroll 8
-    for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = row[u * s_t];
+      for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = row[u * s_t];
+    }
   }
   __syncthreads();
   FwdRec<NS> fr;
@@ -3678,6 +3694,11 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
                                   hipStream_t st) {
   const int64_t n_wg = n_ch * nb;
   if (n_wg < 1 || n_wg > INT32_MAX) return hipErrorInvalidValue;
+  static int stage_old = -1;
+  if (stage_old < 0) {
+    stage_old = getenv_flag("LFD_FR_STAGE_OLD") ? 1 : 0;
+    if (stage_old) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stage_old), &stage_old, sizeof(int));
+  }
 #define LFD_FR(NS, OUT)                                                                                \
   k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
                                                          ys_t)
