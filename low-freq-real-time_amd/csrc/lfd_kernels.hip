@@ -4015,12 +4015,14 @@ constexpr int fdm_rl() {
   const int a = FDM_NN + ((4 - FDM_NN) % 32 + 32) % 32, b = FDM_NN + ((28 - FDM_NN) % 32 + 32) % 32;
   return a < b ? a : b;
 }
-template <int Q>
+// DB: two X buffers (the next tile's staging lands in the other one, one
+// barrier per tile, 1 workgroup per CU) instead of one (two barriers, 3 per CU)
+template <int Q, bool DB = false>
 constexpr size_t fdm_lds_bytes() {
-  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32);
+  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32) * (DB ? 2 : 1);
 }
-template <int Q>
-__global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
+template <int Q, bool DB = false>
+__global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
                                                           int64_t s_ch, const double *__restrict__ h, int n_taps,
                                                           int64_t delay, int64_t n_out, int64_t tiles_o, int strip,
                                                           double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
@@ -4078,11 +4080,11 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
       }
     }
   };
-  auto commit = [&]() {
+  auto commit = [&](int cpar = 0) {
     int ln = lane;
     asm volatile("" : "+v"(ln));  // recomputed per tile, not hoisted into registers
     const int n_l = ln / Q, r_l = ln - n_l * Q;
-    float *a0 = row_ld + (Q - 1 - r_l) * RL + n_l;
+    float *a0 = row_ld + cpar * (4 * JB) + (Q - 1 - r_l) * RL + n_l;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       constexpr int dummy = 0;
@@ -4104,14 +4106,26 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
   const float *x21 = Xs + jl * JB + offj(jl) + 64 * w + 4 * ((lane >> 2) & 3);
   // diag (LFD_FIR_DIAG, timing breakdowns only): 1 = staging without the
   // MFMA phase loop, 2 = MFMA phase loop without the staging
+  constexpr int XB = 4 * JB;  // floats per X buffer
   if ((diag & 3) != 2) issue(t_begin * NO);
-  for (int64_t tt = t_begin; tt < t_end; ++tt) {
-    __syncthreads();  // the previous tile's reads of X are done
+  if (DB) {
     if ((diag & 3) != 2) commit();
+  }
+  if (diag & 16) {  // (A/B: stagger the workgroups sharing a CU by a third of a tile)
+    const int sk = (int)(blockIdx.x % 3);
+    for (int i = 0; i < sk * (1 + ((diag >> 5) & 3)); ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  for (int64_t tt = t_begin; tt < t_end; ++tt) {
+    const int par = DB ? (int)((tt - t_begin) & 1) : 0;
+    if (!DB) {
+      __syncthreads();  // the previous tile's reads of X are done
+      if ((diag & 3) != 2) commit();
+    }
     __syncthreads();
     // (diag bit 4: the next tile's loads issued half-way through the phases)
     const bool pf_next = tt + 1 < t_end && (diag & 3) != 2;
     if (pf_next && !(diag & 4)) issue((tt + 1) * NO);
+    const float *xbc = xb + par * XB;
     if (diag & 8) __builtin_amdgcn_s_setprio(2);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     if ((diag & 3) != 1) {
@@ -4123,7 +4137,7 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
 #pragma unroll
       for (int d = 0; d < DM; ++d) an[d] = At[d * 16 + lane_a];
 #pragma unroll
-      for (int si = 0; si < NB; ++si) bn[si] = xb[4 * si];
+      for (int si = 0; si < NB; ++si) bn[si] = xbc[4 * si];
 #pragma unroll
       for (int v = 0; v < Q; ++v) {
         double ac[DM], bd[NB];
@@ -4136,7 +4150,7 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
 #pragma unroll
           for (int d = 0; d < DM; ++d) an[d] = At[((v + 1) * DM + d) * 16 + lane_a];
 #pragma unroll
-          for (int si = 0; si < NB; ++si) bn[si] = xb[(v + 1) * RL + 4 * si];
+          for (int si = 0; si < NB; ++si) bn[si] = xbc[(v + 1) * RL + 4 * si];
         }
         // the four tiles' accumulators alternate: dependent MFMAs sit 4 apart
 #pragma unroll
@@ -4153,7 +4167,7 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
     for (int t = 0; t < 4; ++t) {
       const int64_t o = O + 64 * w + 16 * t + 4 * bo + io;
       if (ch >= n_ch || o >= n_out) continue;
-      double val = fma(h21, (double)x21[16 * t], acc[t]);
+      double val = fma(h21, (double)x21[par * XB + 16 * t], acc[t]);
       if (!isfinite(val)) {
         // direct sum (rare: a non-finite sample within reach of this output)
         const float *xr = x + ch * s_ch;
@@ -4166,6 +4180,7 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
       }
       y[ch * ys_ch + o * ys_t] = val;
     }
+    if (DB && pf_next) commit(par ^ 1);  // next tile into the other buffer
   }
 }
 
@@ -4185,22 +4200,29 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     const int64_t grid = (n_ch + 3) / 4 * ((tiles_o + strip - 1) / strip);
     int diag = 0;
     if (const char *dv = std::getenv("LFD_FIR_DIAG")) diag = std::atoi(dv);
+    const bool db = getenv_flag("LFD_FIR_DB");
     bool launched = false;
     hipError_t e = hipSuccess;
-#define LFD_FDM(QV)                                                                                          \
-  case QV: {                                                                                                 \
+#define LFD_FDM1(QV, DBV)                                                                                    \
+  {                                                                                                          \
     static bool attr = false;                                                                                \
     if (!attr) {                                                                                             \
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                      \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV>());         \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV, DBV>),                 \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV, DBV>());    \
       if (e != hipSuccess) return e;                                                                         \
       attr = true;                                                                                           \
     }                                                                                                        \
-    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdm_lds_bytes<QV>(), st>>>(x, n_ch, n_t, s_ch, h, n_taps, \
-                                                                              delay, n_out, tiles_o, strip,  \
-                                                                              y, ys_ch, ys_t, diag);         \
-    launched = true;                                                                                         \
-    break;                                                                                                   \
+    k_fir_decimate_mfma<QV, DBV><<<(unsigned)grid, 256, fdm_lds_bytes<QV, DBV>(), st>>>(                    \
+        x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, diag);                  \
+  }
+#define LFD_FDM(QV)          \
+  case QV: {                 \
+    if (db)                  \
+      LFD_FDM1(QV, true)     \
+    else                     \
+      LFD_FDM1(QV, false)    \
+    launched = true;         \
+    break;                   \
   }
     if (grid <= (int64_t)INT32_MAX) {
       switch (q) {
@@ -4213,6 +4235,7 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
       }
     }
 #undef LFD_FDM
+#undef LFD_FDM1
     if (launched) {
       if (kernel_used) *kernel_used = 1;
       return hipGetLastError();
