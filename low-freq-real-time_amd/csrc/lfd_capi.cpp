@@ -662,6 +662,18 @@ struct lfd_lowpass_plan {
   mutable int last_ring = 0;  // ring size of the last timed execute (0: ev)
   mutable bool timed = false;
   mutable int last_k1 = 0;
+  // Composite plan (grids that are not one uniform lattice with one fraction
+  // w: 3 kHz data on integer-ns times, jittered archives): one uniform,
+  // sample-aligned sub-plan per lattice phase d (positions lo0 + j R + d),
+  // each writing its lattice outputs into rows [toff, toff + n) of an
+  // [n_ch][comp_T] float32 scratch, then k_blend_grid forms
+  // y[j] = (1 - w_j) Y_{d_j}[j] + w_j Y_{d_j + 1}[j] (linear interp1d).
+  std::vector<lfd_lowpass_plan *> subs;
+  std::vector<int64_t> sub_toff;
+  int64_t comp_T = 0, n_blend = 0;
+  size_t off_tmp = 0;
+  int64_t *d_bj = nullptr, *d_bi = nullptr;  // grid index; scratch index of y[lo], y[lo + 1] (-1: w == 0)
+  double *d_bw = nullptr;
 };
 
 extern "C" {
@@ -680,11 +692,37 @@ int lfd_set_timing(int enable) {
   return LFD_OK;
 }
 
+static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_sec,
+                               int padlen, int64_t n_ch, int64_t n_t,
+                               const int64_t *grid_lo, const double *grid_w,
+                               int64_t n_grid, const lfd_chunk *chunks,
+                               int64_t n_chunks);
+static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int n_sec,
+                                 int padlen, int64_t n_ch, int64_t n_t,
+                                 const int64_t *grid_lo, const double *grid_w,
+                                 int64_t n_grid, const lfd_chunk *chunks,
+                                 int64_t n_chunks);
+
 int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec,
                             int padlen, int64_t n_ch, int64_t n_t,
                             const int64_t *grid_lo, const double *grid_w,
                             int64_t n_grid, const lfd_chunk *chunks,
                             int64_t n_chunks) {
+  const int rc = plan_create_uniform(out, sos, n_sec, padlen, n_ch, n_t, grid_lo, grid_w, n_grid, chunks,
+                                     n_chunks);
+  if (rc != LFD_EUNSUPPORTED || n_grid < 2 || !grid_lo || !grid_w || !chunks || n_chunks < 1) return rc;
+  const std::string why = g_err;
+  const int rc2 = plan_create_composite(out, sos, n_sec, padlen, n_ch, n_t, grid_lo, grid_w, n_grid, chunks,
+                                        n_chunks);
+  if (rc2 == LFD_EUNSUPPORTED) return fail(LFD_EUNSUPPORTED, why + "; lattice plan: " + g_err);
+  return rc2;
+}
+
+static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_sec,
+                               int padlen, int64_t n_ch, int64_t n_t,
+                               const int64_t *grid_lo, const double *grid_w,
+                               int64_t n_grid, const lfd_chunk *chunks,
+                               int64_t n_chunks) {
   if (!out) return fail(LFD_EINVAL, "plan out-pointer is NULL");
   *out = nullptr;
   Cascade c;
@@ -997,6 +1035,138 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **out, const double *sos, int n_sec
   return LFD_OK;
 }
 
+// Lattice decomposition of a general grid (see lfd_lowpass_plan::subs):
+// nominal spacing R = round((lo_last - lo_0) / (n - 1)), phase of point j
+// d_j = lo_j - (lo_0 + j R); point j needs phase d_j (y[lo_j]) and, when
+// w_j > 0, phase d_j + 1 (y[lo_j + 1]).  Every phase is a uniform,
+// sample-aligned grid, so each sub-plan is an ordinary block plan over the
+// original chunks (each chunk filtered with its own edges, as the reference
+// filters each chunk); only the lattice points a chunk needs are put in its
+// grid range.  At most LATTICE_MAX phases (3 kHz data with integer-ns times
+// drift one sample per ~333 s at dt = 1 s).
+static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int n_sec,
+                                 int padlen, int64_t n_ch, int64_t n_t,
+                                 const int64_t *lo, const double *w,
+                                 int64_t n, const lfd_chunk *chunks,
+                                 int64_t n_chunks) {
+  constexpr int LATTICE_MAX = 32;
+  if (env_flag("LFD_NO_LATTICE")) return fail(LFD_EUNSUPPORTED, "disabled (LFD_NO_LATTICE)");
+  for (int64_t j = 0; j < n; ++j) {
+    if (!(w[j] >= 0.0 && w[j] < 1.0)) return fail(LFD_EINVAL, "grid weights must be in [0, 1)");
+    if (j > 0 && lo[j] + w[j] <= lo[j - 1] + w[j - 1]) return fail(LFD_EUNSUPPORTED, "grid not increasing");
+  }
+  const int64_t R = (int64_t)std::llround((double)(lo[n - 1] - lo[0]) / (double)(n - 1));
+  if (R < 2) return fail(LFD_EUNSUPPORTED, "grid spacing below 2 samples");
+  auto phase = [&](int64_t j) { return lo[j] - (lo[0] + j * R); };
+  // phase -> [j_first, j_last] over the points the chunks need
+  std::vector<std::pair<int64_t, std::pair<int64_t, int64_t>>> ph;
+  auto need = [&](int64_t d, int64_t j) {
+    for (auto &e : ph)
+      if (e.first == d) {
+        e.second.first = std::min(e.second.first, j);
+        e.second.second = std::max(e.second.second, j);
+        return;
+      }
+    ph.push_back({d, {j, j}});
+  };
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    if (chunks[c].g0 < 0 || chunks[c].g1 > n || chunks[c].g1 < chunks[c].g0)
+      return fail(LFD_EINVAL, "chunk " + std::to_string(c) + ": grid range outside the grid");
+    for (int64_t j = chunks[c].g0; j < chunks[c].g1; ++j) {
+      need(phase(j), j);
+      if (w[j] != 0.0) need(phase(j) + 1, j);
+      if ((int)ph.size() > LATTICE_MAX) return fail(LFD_EUNSUPPORTED, "more than 32 lattice phases");
+    }
+  }
+  if (ph.empty()) return fail(LFD_EUNSUPPORTED, "no output points");
+  std::sort(ph.begin(), ph.end());
+  auto *p = new lfd_lowpass_plan();
+  p->n_sec = n_sec;
+  p->n_ch = n_ch;
+  p->n_t = n_t;
+  p->n_grid = n;
+  p->n_chunks = n_chunks;
+  auto bad = [&](int code) {
+    lfd_lowpass_plan_destroy(p);
+    return code;
+  };
+  size_t ws_max = 256;
+  std::vector<int64_t> jfirst;
+  for (const auto &e : ph) {
+    const int64_t d = e.first, j0 = e.second.first;
+    const int64_t j1 = std::max(e.second.second, j0 + 1);  // a lattice of >= 2 points
+    std::vector<int64_t> sl((size_t)(j1 - j0 + 1));
+    for (int64_t i = 0; i <= j1 - j0; ++i) sl[i] = lo[0] + (j0 + i) * R + d;
+    std::vector<double> sw(sl.size(), 0.0);
+    std::vector<lfd_chunk> sc;
+    for (int64_t c = 0; c < n_chunks; ++c) {
+      int64_t a = INT64_MAX, b = INT64_MIN;
+      for (int64_t j = chunks[c].g0; j < chunks[c].g1; ++j)
+        if (phase(j) == d || (w[j] != 0.0 && phase(j) + 1 == d)) {
+          a = std::min(a, j);
+          b = std::max(b, j);
+        }
+      if (a <= b) sc.push_back(lfd_chunk{chunks[c].s0, chunks[c].s1, a - j0, b + 1 - j0});
+    }
+    lfd_lowpass_plan *sub = nullptr;
+    const int rc = plan_create_uniform(&sub, sos, n_sec, padlen, n_ch, n_t, sl.data(), sw.data(),
+                                       (int64_t)sl.size(), sc.data(), (int64_t)sc.size());
+    if (rc != LFD_OK) {
+      const std::string m = g_err;
+      bad(rc);
+      return fail(rc, "phase " + std::to_string(d) + ": " + m);
+    }
+    p->subs.push_back(sub);
+    p->sub_toff.push_back(p->comp_T);
+    jfirst.push_back(j0);
+    p->comp_T += (int64_t)sl.size();
+    ws_max = std::max(ws_max, sub->ws_bytes);
+  }
+  p->padlen = p->subs[0]->padlen;
+  p->bg = p->subs[0]->bg;
+  // blend map over the chunks' output points
+  auto slot = [&](int64_t d, int64_t j) -> int64_t {
+    for (size_t i = 0; i < ph.size(); ++i)
+      if (ph[i].first == d) return p->sub_toff[i] + (j - jfirst[i]);
+    return -1;
+  };
+  std::vector<int64_t> bj, bi;
+  std::vector<double> bw;
+  for (int64_t c = 0; c < n_chunks; ++c)
+    for (int64_t j = chunks[c].g0; j < chunks[c].g1; ++j) {
+      bj.push_back(j);
+      bi.push_back(slot(phase(j), j));
+      bi.push_back(w[j] != 0.0 ? slot(phase(j) + 1, j) : -1);
+      bw.push_back(w[j]);
+    }
+  p->n_blend = (int64_t)bj.size();
+  p->off_tmp = align256(ws_max);
+  p->ws_bytes = align256(p->off_tmp + sizeof(float) * (size_t)n_ch * (size_t)p->comp_T);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    (void)hipGetLastError();
+    p->device = -1;
+    *out = p;
+    return LFD_OK;
+  }
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess) e = hipMalloc(&p->d_bj, sizeof(int64_t) * std::max<size_t>(1, bj.size()));
+  if (e == hipSuccess) e = hipMalloc(&p->d_bi, sizeof(int64_t) * std::max<size_t>(1, bi.size()));
+  if (e == hipSuccess) e = hipMalloc(&p->d_bw, sizeof(double) * std::max<size_t>(1, bw.size()));
+  if (e == hipSuccess && !bj.empty()) e = hipMemcpy(p->d_bj, bj.data(), sizeof(int64_t) * bj.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !bi.empty()) e = hipMemcpy(p->d_bi, bi.data(), sizeof(int64_t) * bi.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !bw.empty()) e = hipMemcpy(p->d_bw, bw.data(), sizeof(double) * bw.size(), hipMemcpyHostToDevice);
+  for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
+  // (the sub-plans hold the chunk tables; d_chunks marks the plan executable)
+  if (e == hipSuccess) e = hipMalloc(&p->d_chunks, sizeof(lfd::ChunkGeom));
+  if (e != hipSuccess) {
+    bad(LFD_EHIP);
+    return fail(LFD_EHIP, std::string("plan allocation: ") + hipGetErrorString(e));
+  }
+  *out = p;
+  return LFD_OK;
+}
+
 int lfd_lowpass_plan_info(const lfd_lowpass_plan *p, size_t *ws, int64_t *nb, int64_t *L) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
   if (ws) *ws = p->ws_bytes;
@@ -1017,6 +1187,26 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   if (dev != p->device) return fail(LFD_EINVAL, "plan was created on another device");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   char *ws = static_cast<char *>(workspace);
+  if (!p->subs.empty()) {
+    // composite: the lattice sub-plans into the scratch, then the blend
+    const bool timed = g_timing.load() != 0;
+    p->timed = timed;
+    p->last_ring = 0;
+    if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
+    float *tmp = reinterpret_cast<float *>(ws + p->off_tmp);
+    for (size_t i = 0; i < p->subs.size(); ++i)
+    {
+      const int rc = lfd_lowpass_execute(p->subs[i], x, s_ch, s_t, tmp + p->sub_toff[i], p->comp_T, 1, workspace,
+                                         stream);
+      if (rc != LFD_OK) return rc;
+    }
+    if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
+    LFD_HIP(lfd::launch_blend_grid(tmp, p->comp_T, p->n_ch, p->d_bj, p->d_bi, p->d_bw, p->n_blend, y, ys_ch,
+                                   ys_t, st));
+    if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
+    p->last_k1 = p->subs[0]->last_k1;
+    return LFD_OK;
+  }
   double *F = reinterpret_cast<double *>(ws + p->off_F);
   double *SF = reinterpret_cast<double *>(ws + p->off_SF);
   double *TP = reinterpret_cast<double *>(ws + p->off_TP);
@@ -1122,6 +1312,7 @@ int lfd_debug_plan_constants(const lfd_lowpass_plan *p, void *block_const, size_
                              void *scan_const, size_t sc_bytes, void *chunk_geom,
                              size_t cg_bytes) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (!p->subs.empty()) return fail(LFD_EUNSUPPORTED, "lattice (composite) plan: see its sub-plans");
   if (bc_bytes != sizeof(lfd::BlockConst) || sc_bytes != sizeof(lfd::ScanConst) ||
       cg_bytes != sizeof(lfd::ChunkGeom) * p->chunks.size())
     return fail(LFD_EINVAL, "size mismatch: BlockConst " + std::to_string(sizeof(lfd::BlockConst)) +
@@ -1174,6 +1365,9 @@ int lfd_lowpass_last_kernel(const lfd_lowpass_plan *p) {
 
 void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   if (!p) return;
+  for (auto *sp : p->subs) lfd_lowpass_plan_destroy(sp);
+  for (void *d : {(void *)p->d_bj, (void *)p->d_bi, (void *)p->d_bw})
+    if (d) (void)hipFree(d);
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);
   if (p->d_taps_tm) (void)hipFree(p->d_taps_tm);

@@ -266,6 +266,10 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
 hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
                                const double *h, int n_taps, int64_t q, int64_t delay, double *y, int64_t ys_ch,
                                int64_t ys_t, hipStream_t st, int *kernel_used);
+// Lattice (composite) plans: y[ch, bj[i]] = (1 - bw[i]) tmp[ch, bi[2i]] +
+// bw[i] tmp[ch, bi[2i+1]] (bi[2i+1] < 0: tmp[ch, bi[2i]]), tmp rows of T.
+hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st);
 // dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.
 hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
                             int64_t dp, hipStream_t st);

@@ -4263,6 +4263,33 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
   return hipGetLastError();
 }
 
+// Lattice-plan blend (lfd_capi.cpp plan_create_composite): linear interp1d
+// between the two lattice phases' outputs y[lo] and y[lo + 1] of every grid
+// point; one thread per (channel, point), points fastest.
+__global__ __launch_bounds__(256) void k_blend_grid(const float *__restrict__ tmp, int64_t T, int64_t n_ch,
+                                                    const int64_t *__restrict__ bj, const int64_t *__restrict__ bi,
+                                                    const double *__restrict__ bw, int64_t nb, float *__restrict__ y,
+                                                    int64_t ys_ch, int64_t ys_t) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nb * n_ch) return;
+  const int64_t ch = idx / nb, i = idx - ch * nb;
+  const float *row = tmp + ch * T;
+  const int64_t ia = bi[2 * i], ib = bi[2 * i + 1];
+  double v = (double)row[ia];
+  if (ib >= 0) {
+    const double wv = bw[i];
+    v = fma(wv, (double)row[ib] - v, v);
+  }
+  y[ch * ys_ch + bj[i] * ys_t] = (float)v;
+}
+
+hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+  if (nb <= 0 || n_ch <= 0) return hipSuccess;
+  k_blend_grid<<<nblk(nb * n_ch, 256), 256, 0, st>>>(tmp, T, n_ch, bj, bi, bw, nb, y, ys_ch, ys_t);
+  return hipGetLastError();
+}
+
 // Time-major -> channel-major transpose for the stream arena
 // (host (time, distance) rows, as real DAS files store them,
 // low_pass_dascore.ipynb:222 data[:, ch]).  64x64 tiles through LDS (one

@@ -345,10 +345,18 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
   float *y = s->out[oi];
   const float *x = s->arena[s->cur] + x0;
   lfd_lowpass_plan *plan = nullptr;
-  if (aligned && n_out >= 2) {
+  if (n_out >= 2) {
+    // uniform grids: keyed by (first point, spacing, fraction); other grids
+    // (varying fraction or spacing) become lattice plans keyed by every point
     int64_t wbits = 0;
     std::memcpy(&wbits, &w[0], sizeof(wbits));
-    std::vector<int64_t> key = {nt, lo[0] - x0, lo[1] - lo[0], n_out, wbits};
+    std::vector<int64_t> key = {nt, aligned ? 1 : 0, lo[0] - x0, lo[1] - lo[0], n_out, wbits};
+    if (!aligned)
+      for (int64_t j = 0; j < n_out; ++j) {
+        int64_t wb = 0;
+        std::memcpy(&wb, &w[j], sizeof(wb));
+        key.insert(key.end(), {lo[j] - x0, wb});
+      }
     for (auto &c : cs) key.insert(key.end(), {c[0] - x0, c[1] - x0, c[2] - j0, c[3] - j0});
     auto it = s->plans.find(key);
     if (it != s->plans.end()) {
@@ -377,7 +385,8 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
     LFD_TRY(ensure_dev(&s->ws, &s->ws_bytes, std::max<size_t>(need, 256), s->s_comp));
     LFD_TRY(lfd_lowpass_execute(plan, x, s->cap, 1, y, n_out, 1, s->ws, s->s_comp));
   } else {
-    // off-grid or single-point output: per-chunk general path (still on device)
+    // single-point output, or a grid no block plan takes (more than 32
+    // lattice phases): per-chunk general path (still on device)
     for (auto &c : cs) {
       const int64_t m = c[3] - c[2];
       if (m <= 0) continue;

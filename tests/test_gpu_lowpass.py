@@ -80,6 +80,31 @@ def test_lfproc_parity(cfg, dc, layout, off_ns):
     assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
+@pytest.mark.parametrize("off_ns", [0, 123_457])
+def test_lfproc_parity_lattice_grid(off_ns):
+    """3 kHz data on integer-ns sample times (333,333 ns): the 1 s output grid
+    drifts against the samples, so the fraction w varies from point to point
+    and the spacing is 3,000 or 3,001 samples.  The plan decomposes the grid
+    into lattice phases (one uniform block sub-plan per phase, then the
+    interp1d blend) and still runs the block-plan kernels; outputs match the
+    oracle (relRMS 1e-4) with identical shapes."""
+    fs, dt_out, P, B, n_ch, dur = 3000.0, 1.0, 120, 7, 20, 1300.0
+    n = int(dur * fs)
+    rng = np.random.default_rng(5)
+    t = np.arange(n) / fs
+    x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.02 * t) + 50.0).astype(np.float32)
+    y, ref, sched = _run(x, fs, dt_out, P, B, off_ns=off_ns)
+    w = _run.w
+    assert len(np.unique(w)) > 100  # a varying fraction
+    num = den = 0.0
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        assert r.shape == (n_ch, ob - oa)
+        num += float(np.sum((y[:, oa:ob] - r) ** 2))
+        den += float(np.sum(r ** 2))
+    assert (num / den) ** 0.5 < 1e-4
+    assert _run.last_kernel == "mfma_runs"
+
+
 def _plan_cfg(fs, dt_out, P, B, n_ch, n):
     from lfdas.plan import LowpassPlan
     dt_ns = int(round(1e9 / fs))

@@ -94,12 +94,34 @@ def test_plan_geometry_cfg3():
 
 def test_plan_rejects_unsupported_grids():
     sos = lowpass_sos(250.0, 1.0)
-    with pytest.raises(_lib.LFDUnsupported):
-        LowpassPlan(sos, 2, 1000, [0, 10, 25], [0, 0, 0], [(0, 999, 0, 3)])
-    with pytest.raises(_lib.LFDUnsupported):
-        LowpassPlan(sos, 2, 1000, [0, 10, 20], [0, 0.5, 0], [(0, 999, 0, 3)])
+    # grids that are not one uniform lattice with one fraction become lattice
+    # (composite) plans: one uniform sub-plan per phase + the interp1d blend
+    for lo, w in (([0, 10, 25], [0, 0, 0]), ([0, 10, 20], [0, 0.5, 0])):
+        plan = LowpassPlan(sos, 2, 1000, lo, w, [(0, 999, 0, 3)])
+        with pytest.raises(_lib.LFDUnsupported, match="lattice"):
+            plan.constants()
+        assert plan.workspace_bytes > 0
+        plan.close()
+    # more than 32 lattice phases (a jittered grid): the general path
+    rng = np.random.default_rng(3)
+    lo = np.arange(60) * 100 + rng.integers(-30, 30, 60)
+    with pytest.raises(_lib.LFDUnsupported, match="32 lattice phases"):
+        LowpassPlan(sos, 2, 7000, np.sort(lo), np.zeros(60), [(0, 6999, 0, 60)])
     with pytest.raises(ValueError, match="padlen"):
         LowpassPlan(sos, 2, 1000, [0, 10, 20], [0, 0, 0], [(0, 12, 0, 1)])
+
+
+def test_lattice_plan_3khz_grid_host_only():
+    """3 kHz on integer-ns times (333,333 ns): the 1 s grid's fraction varies
+    and its spacing is 3,000 or 3,001 samples; the plan is a lattice plan
+    (a few phases), created without a device."""
+    plan, sched, tg = _plan_for(3000.0, 1.0, 120, 7, 8, 3000 * 1300)
+    lo, w = S.grid_positions(synth.T0_NS, 333_333, tg)
+    assert len(np.unique(np.diff(lo))) == 2 and len(np.unique(w)) > 100
+    with pytest.raises(_lib.LFDUnsupported, match="lattice"):
+        plan.constants()
+    assert plan.block_len == 500  # the sub-plans' sub-blocks (R = 3,000 = 6 x 500)
+    plan.close()
 
 
 @pytest.mark.parametrize("name", ["lfproc_cfg1.npz", "lfproc_cfg5_slice.npz"])
