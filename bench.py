@@ -896,6 +896,15 @@ def main():
             label="10,000 ch x 1 h @ 1 kHz (144 GB), dt = 10 s (the batch notebook's d_t), P = 120, B = 6: "
                   "R = 10,000 as 20 sub-blocks of 500")
     if ws == 1 and not args.no_extra:
+        # a grid no single uniform block plan takes: 3 kHz samples on integer-ns
+        # times (333,333 ns) drift against the 1 s output grid (lattice plan:
+        # one block sub-plan per phase + the interp1d blend)
+        secondary["lowpass_3khz_lattice"] = bench_lowpass_line(
+            dev, 2000, 3000.0, 1800.0, 1.0, 600, 7,
+            label="2,000 ch x 30 min @ 3 kHz (333,333 ns samples: varying interpolation fraction, spacing "
+                  "3,000 / 3,001), dt = 1 s, P = 600, B = 7: lattice plan (kernel_ms = all phase sub-plans, "
+                  "scan_kernel_ms = the blend)")
+    if ws == 1 and not args.no_extra:
         # strong-scaling proxy on one GPU: the channel shard one rank of an
         # N-GPU run owns, timed alone (the driver's SCALE run is the record)
         shards = {}

@@ -68,6 +68,12 @@ int lfd_device_count(int *count);
  * (padlen < 0 → SciPy's default 3*(2*n_sec+1 - ...)) and linearly
  * interpolated at its grid points.  Chunks may overlap (they do in
  * LFProc); overlapping samples are read from HBM once.
+ * Grids: uniform spacing with one fraction w (one block plan), or a slowly
+ * drifting fraction / spacing (a lattice plan: one block sub-plan per
+ * lattice phase + an interp1d blend; e.g. 3 kHz data on integer-ns times).
+ * LFD_EUNSUPPORTED for other grids (the caller uses the per-chunk
+ * lfd_sos_filtfilt_resample_f32).  For a lattice plan, lfd_lowpass_last_timing
+ * reports (all sub-plans, the blend).
  * ------------------------------------------------------------------------ */
 typedef struct lfd_chunk {
   int64_t s0, s1; /* inclusive input sample range                         */

@@ -1079,6 +1079,13 @@ static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int 
     }
   }
   if (ph.empty()) return fail(LFD_EUNSUPPORTED, "no output points");
+  // every phase re-runs K1 over its chunks: only grids with few phases per
+  // point (slow drift) pay off against the per-chunk general path
+  int64_t n_pts = 0;
+  for (int64_t c = 0; c < n_chunks; ++c) n_pts += chunks[c].g1 - chunks[c].g0;
+  if ((int64_t)ph.size() * 8 > n_pts + 16)
+    return fail(LFD_EUNSUPPORTED, std::to_string(ph.size()) + " lattice phases for " + std::to_string(n_pts) +
+                                      " points");
   std::sort(ph.begin(), ph.end());
   auto *p = new lfd_lowpass_plan();
   p->n_sec = n_sec;
@@ -1187,26 +1194,6 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   if (dev != p->device) return fail(LFD_EINVAL, "plan was created on another device");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   char *ws = static_cast<char *>(workspace);
-  if (!p->subs.empty()) {
-    // composite: the lattice sub-plans into the scratch, then the blend
-    const bool timed = g_timing.load() != 0;
-    p->timed = timed;
-    p->last_ring = 0;
-    if (timed) LFD_HIP(hipEventRecord(p->ev[0], st));
-    float *tmp = reinterpret_cast<float *>(ws + p->off_tmp);
-    for (size_t i = 0; i < p->subs.size(); ++i)
-    {
-      const int rc = lfd_lowpass_execute(p->subs[i], x, s_ch, s_t, tmp + p->sub_toff[i], p->comp_T, 1, workspace,
-                                         stream);
-      if (rc != LFD_OK) return rc;
-    }
-    if (timed) LFD_HIP(hipEventRecord(p->ev[1], st));
-    LFD_HIP(lfd::launch_blend_grid(tmp, p->comp_T, p->n_ch, p->d_bj, p->d_bi, p->d_bw, p->n_blend, y, ys_ch,
-                                   ys_t, st));
-    if (timed) LFD_HIP(hipEventRecord(p->ev[2], st));
-    p->last_k1 = p->subs[0]->last_k1;
-    return LFD_OK;
-  }
   double *F = reinterpret_cast<double *>(ws + p->off_F);
   double *SF = reinterpret_cast<double *>(ws + p->off_SF);
   double *TP = reinterpret_cast<double *>(ws + p->off_TP);
@@ -1228,6 +1215,22 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
     ++p->n_exec;
     p->last_ring = ring_n > 1 ? ring_n : 0;
     LFD_HIP(hipEventRecord(ev[0], st));
+  }
+  if (!p->subs.empty()) {
+    // lattice plan: the phase sub-plans into the scratch (ev[0] .. ev[1]),
+    // then the blend (ev[1] .. ev[2])
+    float *tmp = reinterpret_cast<float *>(ws + p->off_tmp);
+    for (size_t i = 0; i < p->subs.size(); ++i) {
+      const int rc = lfd_lowpass_execute(p->subs[i], x, s_ch, s_t, tmp + p->sub_toff[i], p->comp_T, 1, workspace,
+                                         stream);
+      if (rc != LFD_OK) return rc;
+    }
+    if (timed) LFD_HIP(hipEventRecord(ev[1], st));
+    LFD_HIP(lfd::launch_blend_grid(tmp, p->comp_T, p->n_ch, p->d_bj, p->d_bi, p->d_bw, p->n_blend, y, ys_ch,
+                                   ys_t, st));
+    if (timed) LFD_HIP(hipEventRecord(ev[2], st));
+    p->last_k1 = p->subs[0]->last_k1;
+    return LFD_OK;
   }
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
   const bool rec = env_flag("LFD_K1_REC");

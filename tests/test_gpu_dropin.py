@@ -197,7 +197,8 @@ def test_spool_chunk_windows_reproduce_lfproc_in_one_plan():
         yf = oracle.sosfiltfilt(oracle.butter_sos(4, fc / 125.0), xd[:, s0:s1 + 1])
         want = oracle.interpolate(yf, -1, tx[s0:s1 + 1], tg[oa:ob])
         assert _rel(d, want) < 1e-4
-    # overlapping output grids cannot share one plan: one fused call each
+    # two short grids far apart (a lattice phase per point): no shared plan,
+    # one fused call each
     n1 = PL.launch_count
     outs2 = [windows[0].pass_filter(time=(None, fc)).interpolate(time=windows[0].coords["time"][1500:1510]),
              windows[1].pass_filter(time=(None, fc)).interpolate(time=windows[1].coords["time"][0:10])]

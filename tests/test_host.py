@@ -94,14 +94,20 @@ def test_plan_geometry_cfg3():
 
 def test_plan_rejects_unsupported_grids():
     sos = lowpass_sos(250.0, 1.0)
-    # grids that are not one uniform lattice with one fraction become lattice
-    # (composite) plans: one uniform sub-plan per phase + the interp1d blend
-    for lo, w in (([0, 10, 25], [0, 0, 0]), ([0, 10, 20], [0, 0.5, 0])):
-        plan = LowpassPlan(sos, 2, 1000, lo, w, [(0, 999, 0, 3)])
-        with pytest.raises(_lib.LFDUnsupported, match="lattice"):
-            plan.constants()
-        assert plan.workspace_bytes > 0
-        plan.close()
+    # a phase per point: no lattice plan either (the per-chunk general path)
+    with pytest.raises(_lib.LFDUnsupported, match="lattice phases for 3 points"):
+        LowpassPlan(sos, 2, 1000, [0, 10, 25], [0, 0, 0], [(0, 999, 0, 3)])
+    # uniform spacing with one off-sample point: two phases (y[lo], y[lo + 1])
+    plan = LowpassPlan(sos, 2, 1000, [0, 10, 20], [0, 0.5, 0], [(0, 999, 0, 3)])
+    with pytest.raises(_lib.LFDUnsupported, match="lattice"):
+        plan.constants()
+    plan.close()
+    # a slowly drifting grid (one phase step per 20 points): a lattice plan
+    lo = np.arange(60) * 100 + np.arange(60) // 20
+    plan = LowpassPlan(sos, 2, 7000, lo, np.full(60, 0.25), [(0, 6999, 0, 60)])
+    with pytest.raises(_lib.LFDUnsupported, match="lattice"):
+        plan.constants()
+    plan.close()
     # more than 32 lattice phases (a jittered grid): the general path
     rng = np.random.default_rng(3)
     lo = np.arange(60) * 100 + rng.integers(-30, 30, 60)
