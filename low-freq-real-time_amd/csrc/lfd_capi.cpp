@@ -1119,9 +1119,11 @@ static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int 
     const int rc = plan_create_uniform(&sub, sos, n_sec, padlen, n_ch, n_t, sl.data(), sw.data(),
                                        (int64_t)sl.size(), sc.data(), (int64_t)sc.size());
     if (rc != LFD_OK) {
+      // (a phase the block plan cannot take: the caller's per-chunk general
+      // path reports any real error of the grid)
       const std::string m = g_err;
       bad(rc);
-      return fail(rc, "phase " + std::to_string(d) + ": " + m);
+      return fail(rc == LFD_EHIP ? rc : LFD_EUNSUPPORTED, "phase " + std::to_string(d) + ": " + m);
     }
     p->subs.push_back(sub);
     p->sub_toff.push_back(p->comp_T);

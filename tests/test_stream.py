@@ -42,6 +42,7 @@ def _edge_cfg_cases():
         (200.0, 10.0, 30, 6, 125.0, 5, 0.0),   # d_t = 10 s (notebook default)
         (100.0, 1.0, 20, 3, 7.3, 9, 2.0),      # ragged files, late start
         (250.0, 1.0, 40, 6, 20.0, 5, 0.0005),  # grid between samples: blended output functional
+        (3000.0, 1.0, 60, 6, 30.0, 5, 0.0),    # 333,333 ns samples: drifting fraction (lattice plans)
     ]
 
 
