@@ -1596,8 +1596,10 @@ int lfd_sos_filtfilt_resample_f32(const float *x, int64_t n_ch, int64_t n_t, int
   for (int64_t j = 0; j < n_out; ++j)
     if (lo[j] < 0 || lo[j] >= n_t || (w[j] != 0.0 && lo[j] + 1 >= n_t))
       return fail(LFD_EINVAL, "interpolation position outside the array");
-  const size_t wsb = lfd_sosfiltfilt_workspace_bytes(n_ch, n_t, pl, n_sec);
-  const size_t yb = align256(sizeof(double) * (size_t)n_ch * n_t);
+  // channel slabs bound the float64 intermediate (<= 16 GB per slab)
+  const int64_t slab = std::max<int64_t>(1, std::min<int64_t>(n_ch, ((int64_t)1 << 31) / std::max<int64_t>(1, n_t)));
+  const size_t wsb = lfd_sosfiltfilt_workspace_bytes(slab, n_t, pl, n_sec);
+  const size_t yb = align256(sizeof(double) * (size_t)slab * n_t);
   const size_t tb = align256((sizeof(int64_t) + sizeof(double)) * (size_t)n_out);
   char *buf = nullptr;
   LFD_HIP(hipMalloc(&buf, wsb + yb + tb));
@@ -1610,9 +1612,12 @@ int lfd_sos_filtfilt_resample_f32(const float *x, int64_t n_ch, int64_t n_t, int
     (void)hipFree(buf);
     return fail(LFD_EHIP, hipGetErrorString(e));
   }
-  rc = lfd_sosfiltfilt_f32(x, n_ch, n_t, s_ch, s_t, sos, n_sec, pl, yf, n_t, 1, buf, stream);
-  if (rc == LFD_OK)
-    rc = lfd_interp_linear_f64(yf, n_ch, n_t, n_t, 1, dlo, dw, n_out, y, ys_ch, ys_t, stream);
+  for (int64_t c0 = 0; c0 < n_ch && rc == LFD_OK; c0 += slab) {
+    const int64_t nc = std::min(slab, n_ch - c0);
+    rc = lfd_sosfiltfilt_f32(x + c0 * s_ch, nc, n_t, s_ch, s_t, sos, n_sec, pl, yf, n_t, 1, buf, stream);
+    if (rc == LFD_OK)
+      rc = lfd_interp_linear_f64(yf, nc, n_t, n_t, 1, dlo, dw, n_out, y + c0 * ys_ch, ys_ch, ys_t, stream);
+  }
   e = hipStreamSynchronize(st);
   (void)hipFree(buf);
   if (rc == LFD_OK && e != hipSuccess) rc = fail(LFD_EHIP, hipGetErrorString(e));
