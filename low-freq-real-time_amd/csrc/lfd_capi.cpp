@@ -1612,6 +1612,7 @@ int lfd_sos_filtfilt_resample_f32(const float *x, int64_t n_ch, int64_t n_t, int
     (void)hipFree(buf);
     return fail(LFD_EHIP, hipGetErrorString(e));
   }
+  rc = LFD_OK;
   for (int64_t c0 = 0; c0 < n_ch && rc == LFD_OK; c0 += slab) {
     const int64_t nc = std::min(slab, n_ch - c0);
     rc = lfd_sosfiltfilt_f32(x + c0 * s_ch, nc, n_t, s_ch, s_t, sos, n_sec, pl, yf, n_t, 1, buf, stream);
