@@ -4145,6 +4145,10 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
         for (int d = 0; d < DM; ++d) ac[d] = an[d];
 #pragma unroll
         for (int si = 0; si < NB; ++si) bd[si] = (double)bn[si];
+        if (diag & 64) {  // (A/B: every conversion issued before the phase's first MFMA)
+#pragma unroll
+          for (int si = 0; si < NB; ++si) asm volatile("" : "+v"(bd[si]));
+        }
         if (v == Q / 2 && pf_next && (diag & 4)) issue((tt + 1) * NO);
         if (v + 1 < Q) {
 #pragma unroll
