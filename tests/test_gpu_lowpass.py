@@ -80,8 +80,9 @@ def test_lfproc_parity(cfg, dc, layout, off_ns):
     assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
-@pytest.mark.parametrize("off_ns", [0, 123_457])
-def test_lfproc_parity_lattice_grid(off_ns):
+@pytest.mark.parametrize("layout,off_ns,null", [("tc", 0, False), ("tc", 123_457, False), ("cc", 123_457, False),
+                                                ("tc", 0, True)])
+def test_lfproc_parity_lattice_grid(layout, off_ns, null):
     """3 kHz data on integer-ns sample times (333,333 ns): the 1 s output grid
     drifts against the samples, so the fraction w varies from point to point
     and the spacing is 3,000 or 3,001 samples.  The plan decomposes the grid
@@ -93,16 +94,20 @@ def test_lfproc_parity_lattice_grid(off_ns):
     rng = np.random.default_rng(5)
     t = np.arange(n) / fs
     x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.02 * t) + 50.0).astype(np.float32)
-    y, ref, sched = _run(x, fs, dt_out, P, B, off_ns=off_ns)
+    if null:  # a NaN in one channel: NaN in every output of the chunks holding it
+        x[3, n // 2] = np.nan
+    y, ref, sched = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
     w = _run.w
     assert len(np.unique(w)) > 100  # a varying fraction
     num = den = 0.0
     for (tt, r), (a, b, oa, ob) in zip(ref, sched):
         assert r.shape == (n_ch, ob - oa)
-        num += float(np.sum((y[:, oa:ob] - r) ** 2))
-        den += float(np.sum(r ** 2))
+        np.testing.assert_array_equal(np.isnan(y[:, oa:ob]), np.isnan(r))
+        f = np.isfinite(r)
+        num += float(np.sum((y[:, oa:ob][f] - r[f]) ** 2))
+        den += float(np.sum(r[f] ** 2))
     assert (num / den) ** 0.5 < 1e-4
-    assert _run.last_kernel == "mfma_runs"
+    assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
 def _plan_cfg(fs, dt_out, P, B, n_ch, n):
