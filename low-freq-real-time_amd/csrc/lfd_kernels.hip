@@ -488,7 +488,7 @@ __constant__ int g_k1_band = 0;
 // parallel.  The per-thread chain is then the 4x4 T recurrence alone: with
 // the outputs inside the chain a 1,250-channel shard spent 2.3 us per run
 // step on one wave per 7 SIMDs.
-template <int NS, bool RUNS, bool DEFER = false>
+template <int NS, bool RUNS, bool DEFER = false, int DFT = SCAN_DF, int DBT = SCAN_DB>
 __global__ __launch_bounds__(256) void k_chunk_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
     const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     // software-pipelined through a ring of SCAN_DF runs: the aggregates and
     // lengths of runs r+1 .. r+SCAN_DF are in flight while run r is applied
     // (the step is ~150 cycles, a load ~1.5 us)
-    constexpr int DF = SCAN_DF;
+    constexpr int DF = DFT;
     const double *agb = F + (((ch >> 4) * rg.n_runs) * 8) * 16 + (ch & 15);
     double agq[DF][N];
     int lenq[DF];
@@ -812,7 +812,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       }
     };
     // ring of SCAN_DB runs (r-1 .. r-SCAN_DB in flight while run r is applied)
-    constexpr int DB = SCAN_DB;
+    constexpr int DB = DBT;
     // q[u] holds run r's inputs, gq[u] run r-DB's geometry (slot u = r mod DB)
     RunIn q[DB];
     RunGeo gq[DB];
@@ -3641,8 +3641,14 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
   if (TR && CR && slot_chunk && defer) {
     const unsigned nb = nblk(n_chunks * g.n_ch, 256);
-    k_chunk_scan<2, true, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP, tp_len,
-                                                    y, ys_ch, ys_t, rg, Y0, TR, CR);
+    // (A/B knob LFD_SCAN_DEEP=1: 16 / 8 runs in flight instead of 4 / 2 —
+    // the deferred scan runs on few waves and waits on memory latency)
+    if (getenv_flag("LFD_SCAN_DEEP"))
+      k_chunk_scan<2, true, true, 16, 8><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
+                                                             tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR);
+    else
+      k_chunk_scan<2, true, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP, tp_len,
+                                                      y, ys_ch, ys_t, rg, Y0, TR, CR);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t waves = ((g.n_ch + 63) / 64) * rg.n_sr;
