@@ -3641,9 +3641,13 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
   if (TR && CR && slot_chunk && defer) {
     const unsigned nb = nblk(n_chunks * g.n_ch, 256);
-    // (A/B knob LFD_SCAN_DEEP=1: 16 / 8 runs in flight instead of 4 / 2 —
-    // the deferred scan runs on few waves and waits on memory latency)
-    if (getenv_flag("LFD_SCAN_DEEP"))
+    // long run chains (>= 128 runs per chunk) keep 16 / 8 runs in flight
+    // instead of 4 / 2: dt = 10 s at 1 kHz 0.401 -> 0.352 ms, bit-identical;
+    // narrow shards measure the same either way (profiles/r03_ab_scan_deep.txt;
+    // A/B knob LFD_SCAN_DEEP=0/1)
+    bool deep = rg.n_sr >= 128 * n_chunks;
+    if (const char *dv = std::getenv("LFD_SCAN_DEEP")) deep = std::atoi(dv) != 0;
+    if (deep)
       k_chunk_scan<2, true, true, 16, 8><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                                              tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR);
     else
