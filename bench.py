@@ -953,7 +953,8 @@ def main():
                        "channels": n_ch_total, "channels_rank0": n_ch, "samples": n, "fs": args.fs,
                        "dt_out": args.dt_out, "chunks": len(sched),
                        "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),
-                       "parallelism": f"channel-shard x{ws}", "io_dtype": "f32"},
+                       "parallelism": (f"channel-shard x{ws}" if args.strong else f"one spool per GPU x{ws} (channel-partitioned job)"),
+                       "io_dtype": "f32"},
             **({"rehearsal": "--one-device: every rank on cuda:0 over gloo; not a scaling number"}
                if args.one_device else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
