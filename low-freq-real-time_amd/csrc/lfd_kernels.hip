@@ -3640,7 +3640,10 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   bool defer = n_chunks * g.n_ch < 40000 || rg.n_sr >= 128 * n_chunks;
   if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
   if (TR && CR && slot_chunk && defer) {
-    const unsigned nb = nblk(n_chunks * g.n_ch, 256);
+    // (A/B knob LFD_SCAN_DEFER_THREADS = 64 / 128 / 256: few waves, one per CU at 64)
+    int dthr = 256;
+    if (const char *tv = std::getenv("LFD_SCAN_DEFER_THREADS")) dthr = std::atoi(tv) == 64 ? 64 : (std::atoi(tv) == 128 ? 128 : 256);
+    const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
     // long run chains (>= 128 runs per chunk) keep 16 / 8 runs in flight
     // instead of 4 / 2: dt = 10 s at 1 kHz 0.401 -> 0.352 ms, bit-identical;
     // narrow shards measure the same either way (profiles/r03_ab_scan_deep.txt;
@@ -3648,11 +3651,11 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     bool deep = rg.n_sr >= 128 * n_chunks;
     if (const char *dv = std::getenv("LFD_SCAN_DEEP")) deep = std::atoi(dv) != 0;
     if (deep)
-      k_chunk_scan<2, true, true, 16, 8><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
-                                                             tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR);
+      k_chunk_scan<2, true, true, 16, 8><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
+                                                              tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR);
     else
-      k_chunk_scan<2, true, true><<<nb, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP, tp_len,
-                                                      y, ys_ch, ys_t, rg, Y0, TR, CR);
+      k_chunk_scan<2, true, true><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP, tp_len,
+                                                       y, ys_ch, ys_t, rg, Y0, TR, CR);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t waves = ((g.n_ch + 63) / 64) * rg.n_sr;

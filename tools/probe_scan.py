@@ -1,5 +1,6 @@
 """Scan-kernel phase times (LFD_SCAN_DIAG bits; results invalid when set) for
-cfg3-sized plans: aligned, off-sample (1.9 ms) and 1 kHz dt = 10 s."""
+cfg3-sized plans: aligned, off-sample (1.9 ms), 1 kHz dt = 10 s, and the
+1,250-channel shard of cfg3 ("narrow", deferred outputs)."""
 import os
 import subprocess
 import sys
@@ -12,7 +13,11 @@ sys.path.insert(0, %r); sys.path.insert(0, os.path.join(%r, "low-freq-real-time_
 import torch, bench
 from lfdas.plan import set_timing
 cfg = sys.argv[1]
-if cfg == "offsample":
+nc = 1250 if cfg == "narrow" else 10000
+if cfg == "narrow":
+    plan, *_ = bench.build_plan(nc, 1_800_000, 500.0, 1.0, 600, 7)
+    n = 1_800_000
+elif cfg == "offsample":
     plan, *_ = bench.build_plan(10000, 1_800_000, 500.0, 1.0, 600, 7, off_ns=1_900_000)
     n = 1_800_000
 elif cfg == "dt10":
@@ -21,9 +26,9 @@ elif cfg == "dt10":
 else:
     plan, *_ = bench.build_plan(10000, 1_800_000, 500.0, 1.0, 600, 7)
     n = 1_800_000
-x = torch.empty((10000, n), dtype=torch.float32, device="cuda")
+x = torch.empty((nc, n), dtype=torch.float32, device="cuda")
 bench.synth_fill(x, 500.0, 1)
-y = torch.empty((10000, plan.n_grid), dtype=torch.float32, device="cuda")
+y = torch.empty((nc, plan.n_grid), dtype=torch.float32, device="cuda")
 ws = plan.alloc_workspace()
 set_timing(True)
 t = []
