@@ -219,3 +219,37 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
                 y[:, out_j(k)] = pk + H0 @ T + G0 @ sf
             T = PhiR @ T + er0[:, :, k] + (corr[n:2 * n] if k == kb else 0) + M @ sf
     return y
+
+
+def fir_decimate_mfma_model(x, taps, q, delay, dm=6):
+    """NumPy model of k_fir_decimate_mfma's arithmetic (lfd_kernels.hip): the
+    polyphase sum y[o] = sum_v sum_u h_v[u] X_v[o - u] evaluated as 4 x 4
+    Toeplitz pieces A_{v,d}[i][k] = h_v[4d + i - k] (o = 4G + i, index
+    n = 4(G - d) + k, d < dm) plus the row-0 epilogue tap h[21 q] X_0[o - 21]
+    that dm = 6 steps do not reach.  X_v[n] = x[n q + delay - v], zero outside
+    the record.  Returns float64 (n_ch, ceil(n_t / q))."""
+    x = np.asarray(x, np.float64)
+    h = np.asarray(taps, np.float64)
+    n_ch, n_t = x.shape
+    n_out = -(-n_t // q)
+    o = np.arange(n_out)
+    G, i = o // 4, o % 4
+
+    def X(v, n):
+        t = n * q + delay - v
+        ok = (t >= 0) & (t < n_t)
+        out = np.zeros((n_ch, len(n)))
+        out[:, ok] = x[:, t[ok]]
+        return out
+
+    y = np.zeros((n_ch, n_out))
+    for v in range(q):
+        for d in range(dm):
+            for k in range(4):
+                u = 4 * d + i - k
+                ti = u * q + v
+                a = np.where((u >= 0) & (ti < h.size), h[np.clip(ti, 0, h.size - 1)], 0.0)
+                y += a * X(v, 4 * (G - d) + k)
+    if 21 * q < h.size:
+        y += np.where(i == 0, h[21 * q], 0.0) * X(0, o - 21)
+    return y

@@ -194,6 +194,32 @@ def test_decimate_fir_device(q, layout):
         assert load().lfd_fir_decimate_last_kernel() == 1
 
 
+@pytest.mark.parametrize("q", [4, 5, 6, 8, 10])
+def test_fir_mfma_toeplitz_model_matches_oracle(q):
+    """CPU model of the matrix-core FIR kernel's decomposition (4 x 4 Toeplitz
+    pieces over the polyphase rows, 6 steps + the row-0 epilogue tap) equals
+    scipy.signal.decimate(ftype='fir') as restated by the oracle (1e-13)."""
+    from emulate import fir_decimate_mfma_model
+    from lfdas.proc import fir_decimate_design
+    rng = np.random.default_rng(q)
+    x = rng.standard_normal((3, 40 * q + 7))
+    taps, delay = fir_decimate_design(q)
+    assert taps.size == 21 * q + 1
+    y = fir_decimate_mfma_model(x, taps, q, delay)
+    assert _rel(y, oracle.decimate_fir(x, q)) < 1e-13
+    # any filter of 21 q + 1 taps (firwin's end taps are ~1e-18, so random
+    # taps exercise the row-0 epilogue tap h[21 q]) vs the direct sum
+    h = rng.standard_normal(21 * q + 1)
+    n_out = -(-x.shape[1] // q)
+    ref = np.zeros((3, n_out))
+    for o in range(n_out):
+        for i in range(h.size):
+            t = o * q + delay - i
+            if 0 <= t < x.shape[1]:
+                ref[:, o] += h[i] * x[:, t]
+    assert _rel(fir_decimate_mfma_model(x, h, q, delay), ref) < 1e-13
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("q", [4, 10])
 def test_decimate_fir_device_nulls_and_ragged(q):
@@ -227,3 +253,11 @@ def test_decimate_fir_device_nulls_and_ragged(q):
     np.testing.assert_array_equal(np.isneginf(y), np.isneginf(ref))
     f = np.isfinite(ref)
     assert _rel(y[f], ref[f]) < 1e-12
+    # a random filter of 21 q + 1 taps (firwin's end taps are ~1e-18): the
+    # row-0 epilogue tap h[21 q] and every Toeplitz slot carry weight
+    from emulate import fir_decimate_mfma_model
+    h = rng.standard_normal(21 * q + 1)
+    xf = np.nan_to_num(x, nan=0.0, posinf=0.0, neginf=0.0)
+    y2 = fir_decimate_device(torch.from_numpy(xf).cuda(), h, q, delay).cpu().numpy()
+    assert load().lfd_fir_decimate_last_kernel() == 1
+    assert _rel(y2, fir_decimate_mfma_model(xf.astype(np.float64), h, q, delay)) < 1e-12
