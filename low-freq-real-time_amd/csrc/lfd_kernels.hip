@@ -3640,8 +3640,10 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   bool defer = n_chunks * g.n_ch < 40000 || rg.n_sr >= 128 * n_chunks;
   if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
   if (TR && CR && slot_chunk && defer) {
-    // (A/B knob LFD_SCAN_DEFER_THREADS = 64 / 128 / 256: few waves, one per CU at 64)
-    int dthr = 256;
+    // narrow shards: 64-thread workgroups (one wave per CU instead of four
+    // sharing one): 1,250 channels 0.150 -> 0.126 ms, bit-identical
+    // (profiles/r03_ab_scan_narrow.txt; A/B knob LFD_SCAN_DEFER_THREADS)
+    int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
     if (const char *tv = std::getenv("LFD_SCAN_DEFER_THREADS")) dthr = std::atoi(tv) == 64 ? 64 : (std::atoi(tv) == 128 ? 128 : 256);
     const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
     // long run chains (>= 128 runs per chunk) keep 16 / 8 runs in flight
