@@ -7,18 +7,19 @@ Butterworth at 0.45 Hz, decimate to 1 Hz, LFProc chunking P = 600, B = 7.
 One step = one pass of the hot path over the whole hour (7 overlapping chunks,
 3,585 outputs per channel), inputs resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--strong]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C] [--weak]
 
 N > 1 runs one rank per GPU: under torch.distributed.run (the driver's
 form; WORLD_SIZE must equal --gpus), or ``python bench.py --gpus N`` starts
 that launcher itself as a child process (and fails, printing no line, when
-the node has fewer than N GPUs).  The path partitions by channel with
-no data-path collective, so the default is weak scaling: every rank owns
-its own 10,000-channel spool and ``value`` = all ranks' channel-samples /
-max-over-ranks time.  With N > 1 the config's "channel-sharded at 1/2/4/8
-GPUs" strong-scaling figure (cfg3's 10,000 channels split into contiguous
-blocks, lfdas.shard.channel_range) is reported beside it as
-``secondary.strong_scaling_cfg3``; ``--strong`` makes it the headline.
+the node has fewer than N GPUs).  The headline is BASELINE configs[2] as
+quoted, "10,000 ch x 1 h @ 500 Hz, channel-sharded at 1/2/4/8 GPUs": strong
+scaling, cfg3's 10,000 channels split into contiguous blocks
+(lfdas.shard.channel_range, 1,250 per GPU at N = 8), no data-path
+collective, ``value`` = 10,000 x 1.8 M channel-samples per step /
+max-over-ranks time.  With N > 1 the weak-scaling figure (every rank its own
+10,000-channel spool) is reported beside it as
+``secondary.weak_scaling_cfg3``; ``--weak`` makes it the headline.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -55,9 +56,10 @@ def _args():
     p.add_argument("--no-stream", action="store_true", help="skip the cfg4 / cfg5 streaming lines")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the extra low-pass lines (off-sample grid, 1 kHz dt = 10 s, time-major)")
-    p.add_argument("--strong", action="store_true",
-                   help="headline = --channels split over the ranks (strong scaling); default: every rank "
-                        "owns --channels channels (weak scaling)")
+    p.add_argument("--weak", action="store_true",
+                   help="headline = every rank owns --channels channels (weak scaling); default: --channels "
+                        "split over the ranks (strong scaling, BASELINE configs[2])")
+    p.add_argument("--strong", action="store_true", help="the default (kept for old command lines)")
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo collectives "
                         "(the line is marked rehearsal; not a scaling measurement)")
@@ -446,6 +448,8 @@ def bench_ooc_cfg5_sharded(dev, ws, rank, barrier, max_over_ranks, n_ch=50_000, 
     except Exception as e:
         err = e
     if max_over_ranks(1.0 if err is not None else 0.0) > 0:  # also the start barrier
+        for p in pins:  # page-locked rows released now, not whenever GC runs
+            p.release()
         if st is not None:
             st.close()
         return {"error": repr(err) if err is not None else "setup failed on another rank"}
@@ -600,8 +604,6 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
     dtype).  Algorithmic bytes 4 + 8 per channel-sample.  The dominant
     kernel is the output pass k_fullrate_wave<4, true> (x read + y written
     over the big blocks, 12 B per sample)."""
-    import os as _os
-
     import torch
     import oracle
     from lfdas.design import pass_filter_sos
@@ -641,8 +643,8 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
     rel = float(np.sqrt(np.sum((y[rows].cpu().numpy() - oracle.sosfiltfilt(sos, xs)) ** 2)
                         / np.sum(oracle.sosfiltfilt(sos, xs) ** 2)))
     # the previous one-thread-per-channel kernel on a tenth of the samples
-    _os.environ["LFD_FULLRATE_SERIAL"] = "1"
-    try:
+    from lfdas._lib import kernel_options
+    with kernel_options(fullrate_serial=1):
         xs10 = x[:, : n // 10]
         ys10 = y[:, : n // 10]
         sosfiltfilt_device(xs10, sos, y=ys10, ws=ws)
@@ -652,8 +654,6 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
         e1.record()
         torch.cuda.synchronize(dev)
         serial_ms = e0.elapsed_time(e1)
-    finally:
-        del _os.environ["LFD_FULLRATE_SERIAL"]
     # CPU: SciPy's sosfiltfilt itself on 24 channels (single core)
     from scipy.signal import sosfiltfilt as sp_sosfiltfilt
     xc = x[:24].cpu().numpy()
@@ -778,7 +778,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from lfdas.shard import channel_range
-    if not args.strong:
+    if args.weak:
         n_ch_total, (c0, c1) = args.channels * ws, (0, args.channels)
     else:
         n_ch_total = args.channels
@@ -854,9 +854,9 @@ def main():
     plan.close()
     torch.cuda.empty_cache()
     if ws > 1:
-        # the other scaling mode beside the headline: strong (cfg3's channels
-        # split over the ranks) under the weak default, weak under --strong
-        if args.strong:
+        # the other scaling mode beside the headline: weak (every rank its own
+        # 10,000 channels) under the strong default, strong under --weak
+        if not args.weak:
             o0, o1, o_tot, o_key = 0, args.channels, ws * args.channels, "weak_scaling_cfg3"
         else:
             (o0, o1), o_tot, o_key = channel_range(args.channels, ws, rank), args.channels, "strong_scaling_cfg3"
@@ -943,17 +943,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (0.5 + sin + N(0,1), generated on device)",
             "config": {"workload": "cfg3: 10,000 ch x 1 h @ 500 Hz fp32 (72 GB), 4th-order Butterworth "
                                    "0.45 Hz zero-phase, decimate to 1 Hz, LFProc P=600 B=7"
-                                   + (", channel-sharded over the GPUs" if args.strong else ", per GPU"),
+                                   + (", per GPU" if args.weak else ", channel-sharded over the GPUs"),
                        "channels": n_ch_total, "channels_rank0": n_ch, "samples": n, "fs": args.fs,
                        "dt_out": args.dt_out, "chunks": len(sched),
                        "outputs_per_channel": int(sum(b - a for _, _, a, b in sched)),
-                       "parallelism": (f"channel-shard x{ws}" if args.strong else f"one spool per GPU x{ws} (channel-partitioned job)"),
+                       "parallelism": (f"one spool per GPU x{ws} (channel-partitioned job)" if args.weak
+                                       else f"channel-shard x{ws}"),
                        "io_dtype": "f32"},
             **({"rehearsal": "--one-device: every rank on cuda:0 over gloo; not a scaling number"}
                if args.one_device else {}),

@@ -54,6 +54,24 @@ int lfd_version(void);
  * the multi-GPU channel sharding of the host). */
 int lfd_device_count(int *count);
 
+/* Kernel-selection overrides (process-wide; 0 = the library's own choice).
+ * Every alternative computes the same outputs within the path's parity
+ * tolerance (most bit-identically); they exist so tests can drive the
+ * fallback kernels on inputs the default would not send there.  The library
+ * reads NO environment variable: its results and kernel choices depend only
+ * on the arguments and these options.  (Tuning and diagnostic A/B knobs exist
+ * only in the separately built liblfdas_diag.so, -DLFD_DIAG, used by tools/.) */
+#define LFD_OPT_NO_RUNS 1         /* block plans: per-block functionals, no run folding   */
+#define LFD_OPT_K1_RECURRENCE 2   /* block plans: recurrence K1 instead of fp64 MFMA      */
+#define LFD_OPT_TM_NO_PAIRS 3     /* time-major MFMA K1: one dword per channel, no pairs  */
+#define LFD_OPT_SCAN_DEFER 4      /* run scan outputs: 1 in the chain, 2 deferred         */
+#define LFD_OPT_FULLRATE_SERIAL 5 /* lfd_sosfiltfilt_f32: one thread per channel          */
+#define LFD_OPT_NO_LATTICE 6      /* drifting grids: LFD_EUNSUPPORTED (per-chunk path)    */
+#define LFD_OPT_NO_HEAD_SKIP 7    /* off-sample grids: walk chunk heads                   */
+#define LFD_OPT_FIR_VALU 8        /* lfd_fir_decimate_f32: VALU kernel, not matrix cores  */
+int lfd_set_option(int option, int64_t value);
+int lfd_get_option(int option, int64_t *value);
+
 /* ------------------------------------------------------------------------
  * Chunked zero-phase Butterworth low-pass + resample
  *   replaces: lf_das.py:219-290 (process_time_range's chunk loop) with its

@@ -41,6 +41,32 @@ std::atomic<int> g_timing{0};
 bool lfd::timing_enabled() { return g_timing.load() != 0; }
 
 namespace {
+constexpr int N_OPT = 9;  // LFD_OPT_* ids are 1 .. N_OPT - 1
+std::atomic<int64_t> g_opt[N_OPT];
+#ifdef LFD_DIAG
+// the A/B environment names the tools/ recipes of rounds 1-3 use
+const char *const k_opt_env[N_OPT] = {nullptr,          "LFD_NO_RUNS",    "LFD_K1_REC",
+                                      "LFD_TM_NO_X2",   "LFD_SCAN_DEFER", "LFD_FULLRATE_SERIAL",
+                                      "LFD_NO_LATTICE", "LFD_NO_HSKIP",   "LFD_FIR_VALU"};
+#endif
+}  // namespace
+
+int64_t lfd::option(int id) {
+  if (id <= 0 || id >= N_OPT) return 0;
+  const int64_t v = g_opt[id].load(std::memory_order_relaxed);
+#ifdef LFD_DIAG
+  if (v == 0 && k_opt_env[id]) {
+    if (const char *e = std::getenv(k_opt_env[id])) {
+      // LFD_SCAN_DEFER=0/1 meant in-chain / deferred
+      if (id == LFD_OPT_SCAN_DEFER) return std::atoi(e) != 0 ? 2 : 1;
+      return std::atoll(e);
+    }
+  }
+#endif
+  return v;
+}
+
+namespace {
 
 #define LFD_HIP(call)                                                      \
   do {                                                                     \
@@ -50,11 +76,6 @@ namespace {
   } while (0)
 
 typedef long double R;
-
-bool env_flag(const char *name) {
-  const char *v = std::getenv(name);
-  return v && v[0] && v[0] != '0';
-}
 
 struct Cascade {
   int ns = 0;
@@ -607,7 +628,7 @@ inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 constexpr int64_t SUB_L_MAX = 504;  // Lp = 512: taps 36.9 KB + 8 run buffers = 2 groups/CU
 int64_t sub_block_step(int64_t Rg, int J, bool off_sample) {
   int64_t lmax = SUB_L_MAX;
-  if (const char *v = std::getenv("LFD_SUBBLOCK")) {
+  if (const char *v = lfd::knob("LFD_SUBBLOCK")) {
     lmax = std::atoll(v);
     if (lmax <= 0) return 1;
   }
@@ -684,6 +705,21 @@ int lfd_version(void) { return 100; }
 int lfd_device_count(int *count) {
   if (!count) return fail(LFD_EINVAL, "count is NULL");
   LFD_HIP(hipGetDeviceCount(count));
+  return LFD_OK;
+}
+
+int lfd_set_option(int option, int64_t value) {
+  if (option <= 0 || option >= N_OPT) return fail(LFD_EINVAL, "unknown option " + std::to_string(option));
+  if (value < 0 || (option == LFD_OPT_SCAN_DEFER ? value > 2 : value > 1))
+    return fail(LFD_EINVAL, "option " + std::to_string(option) + ": value out of range");
+  g_opt[option].store(value);
+  return LFD_OK;
+}
+
+int lfd_get_option(int option, int64_t *value) {
+  if (option <= 0 || option >= N_OPT) return fail(LFD_EINVAL, "unknown option " + std::to_string(option));
+  if (!value) return fail(LFD_EINVAL, "value is NULL");
+  *value = g_opt[option].load();
   return LFD_OK;
 }
 
@@ -792,7 +828,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
       const int64_t nh = G.head_end - G.s0, lo = G.head_end - L, J = 2 * n_sec;
       const int64_t ncorr = G.s0 - lo + J;
       G.hskip = (nh >= J && lo >= 0 && ncorr <= padlen && ncorr <= lfd::HSKIP_MAX &&
-                 !(std::getenv("LFD_NO_HSKIP") && std::atoi(std::getenv("LFD_NO_HSKIP")))) ? 1 : 0;
+                 !lfd::option(LFD_OPT_NO_HEAD_SKIP)) ? 1 : 0;
     }
     bool any_block = false;
     for (int64_t j = ch.g0; j < ch.g1; ++j) {
@@ -901,7 +937,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     // units 7 % longer than with 16-block ones, tools/ab_plan.py --replan)
     int64_t unit_cap = 32;
     int64_t unit_min = 16;
-    if (const char *v = std::getenv("LFD_RUN_UNIT")) {
+    if (const char *v = lfd::knob("LFD_RUN_UNIT")) {
       unit_cap = std::min<int64_t>(32, std::max(lfd::RUN_R, std::atoi(v)));
       unit_min = lfd::RUN_R;
     }
@@ -917,7 +953,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     // off)
     const int64_t n_cg = (n_ch + 15) / 16;
     int64_t tail_rounds = 2;  // LFD_RUN_TAIL=<rounds>, 0: off
-    if (const char *v = std::getenv("LFD_RUN_TAIL")) tail_rounds = std::max(0, std::atoi(v));
+    if (const char *v = lfd::knob("LFD_RUN_TAIL")) tail_rounds = std::max(0, std::atoi(v));
     const int64_t tail_blocks =
         std::min<int64_t>(p->bg.nb / 4, tail_rounds * ((4096 + n_cg - 1) / n_cg) * lfd::RUN_R);
     const int64_t tail_k = unit_blocks <= lfd::RUN_R ? p->bg.nb : p->bg.nb - tail_blocks;  // runs starting at or after this block
@@ -1050,7 +1086,7 @@ static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int 
                                  int64_t n, const lfd_chunk *chunks,
                                  int64_t n_chunks) {
   constexpr int LATTICE_MAX = 32;
-  if (env_flag("LFD_NO_LATTICE")) return fail(LFD_EUNSUPPORTED, "disabled (LFD_NO_LATTICE)");
+  if (lfd::option(LFD_OPT_NO_LATTICE)) return fail(LFD_EUNSUPPORTED, "disabled (LFD_OPT_NO_LATTICE)");
   for (int64_t j = 0; j < n; ++j) {
     if (!(w[j] >= 0.0 && w[j] < 1.0)) return fail(LFD_EINVAL, "grid weights must be in [0, 1)");
     if (j > 0 && lo[j] + w[j] <= lo[j - 1] + w[j - 1]) return fail(LFD_EUNSUPPORTED, "grid not increasing");
@@ -1235,10 +1271,10 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
     return LFD_OK;
   }
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
-  const bool rec = env_flag("LFD_K1_REC");
+  const bool rec = lfd::option(LFD_OPT_K1_RECURRENCE) != 0;
   const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !rec;
-  const bool runs = p->run_ok && !env_flag("LFD_NO_RUNS");
+  const bool runs = p->run_ok && !lfd::option(LFD_OPT_NO_RUNS);
   const bool mfma_runs = runs && mfma && p->run_mfma_ok;
   // (time, channel) rows (the real files' layout): the time-major MFMA kernel
   const bool mfma_tm = runs && !mfma && p->d_taps_tm && (s_ch == 1 || p->n_ch == 1) && s_t > 1 &&
@@ -1497,7 +1533,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
   // the array holds a big block; LFD_FULLRATE_SERIAL=1 (A/B knob) keeps the
   // one-thread-per-channel kernel
   const int64_t nb = fullrate_blocks(n_t);
-  if (nb > 0 && !env_flag("LFD_FULLRATE_SERIAL")) {
+  if (nb > 0 && !lfd::option(LFD_OPT_FULLRATE_SERIAL)) {
     std::shared_ptr<const FrEntry> fe;
     if (int e = fullrate_entry(sos, n_sec, c, &fe)) return e;
     const FrLayout lo = fullrate_layout(n_ch, n_t, padlen, n_sec, nb);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 namespace lfd {
@@ -12,6 +13,28 @@ namespace lfd {
 int fail(int code, const std::string &m);
 // lfd_set_timing() state (HIP-event timing of executes / pushes).
 bool timing_enabled();
+
+// lfd_set_option() value of LFD_OPT_* `id` (0 = the library's choice).  In
+// the diagnostic build an unset option also reads its A/B environment name
+// (LFD_NO_RUNS, LFD_K1_REC, ...), so the round-1..3 recipes under tools/ run
+// unchanged against liblfdas_diag.so.
+int64_t option(int id);
+
+// Tuning / diagnostic A/B knobs.  The production liblfdas.so never reads the
+// environment: knob() is nullptr there and every launcher takes its measured
+// default.  Only the diagnostic build (-DLFD_DIAG -> liblfdas_diag.so,
+// loaded by tools/ through LFDAS_LIB) reads them, and only there are the
+// "timing only, results invalid" kernel modes and the measured-and-rejected
+// variants compiled at all.
+#ifdef LFD_DIAG
+inline const char *knob(const char *name) { return std::getenv(name); }
+#else
+inline const char *knob(const char *) { return nullptr; }
+#endif
+inline bool knob_flag(const char *name) {
+  const char *v = knob(name);
+  return v && v[0] && v[0] != '0';
+}
 
 constexpr int MAX_SEC = 4;            // up to 8th-order cascades
 constexpr int MAX_N = 2 * MAX_SEC;    // state dimension (TDF-II, 2 per section)

@@ -29,6 +29,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "../../include/lfdas.h"
 #include "lfd_internal.h"
 
 namespace lfd {
@@ -478,9 +479,19 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 // LFD_SCAN_DIAG (timing experiments only, results invalid): bit 1 skips the
 // left pad/head, 2 the forward run scan, 4 the right pad and its reverse,
 // 8 the backward run scan.
+#ifdef LFD_DIAG
 __constant__ int g_scan_diag = 0;
 // K1 unit order (see k_block_runs_mfma; 0 = channel-group-major)
 __constant__ int g_k1_band = 0;
+#endif
+// LFD_DG(v): a diagnostic / A/B value, the constant 0 in the production
+// build (-DLFD_DIAG builds liblfdas_diag.so for tools/), so every branch it
+// guards is compiled out of liblfdas.so
+#ifdef LFD_DIAG
+#define LFD_DG(v) (v)
+#else
+#define LFD_DG(v) 0
+#endif
 
 // DEFER (run mode): the backward run scan only carries T and stores the T
 // entering every run (TR, laid out like SR) and the chunk's p0 correction
@@ -547,7 +558,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   const int64_t lo_h = G.head_end - g.L;
   bool hs = false;
   if constexpr (RUNS) {
-    if (G.hskip && E > 0 && !(g_scan_diag & 1)) {
+    if (G.hskip && E > 0 && !(LFD_DG(g_scan_diag) & 1)) {
       hs = true;
       for (int64_t t = lo_h; t < G.s0; ++t) hs = hs && __builtin_isfinite(xc[t * s_t]);
     }
@@ -558,7 +569,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     R.steady(S, e0, true);
 #pragma unroll
     for (int j = 0; j < J; ++j) h[j] = e0;
-    for (int i = 0; i < n_pad && !(g_scan_diag & 1); ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
+    for (int i = 0; i < n_pad && !(LFD_DG(g_scan_diag) & 1); ++i) R.fwd(S, h, (double)(2.0f * xl - xc[(G.s0 + E - i) * s_t]));
   }
   if constexpr (RUNS) {
     if (hs) {
@@ -593,7 +604,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // load left every step waiting on memory latency: the off-sample grids'
   // heads and tails are up to L - 1 samples)
   constexpr int SB = 8;
-  if (!(g_scan_diag & 1) && !hs) {
+  if (!(LFD_DG(g_scan_diag) & 1) && !hs) {
     int64_t t = G.s0;
     for (; t + SB <= G.head_end; t += SB) {
       float xv[SB];
@@ -653,7 +664,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
       for (int i = 0; i < N; ++i) agq[u][i] = r < G.r1 ? agb[(r * 8 + i) * 16] : 0.0;
     }
-    for (int64_t rb = G.r0; rb < G.r1 && !(g_scan_diag & 2); rb += DF) {
+    for (int64_t rb = G.r0; rb < G.r1 && !(LFD_DG(g_scan_diag) & 2); rb += DF) {
 #pragma unroll
       for (int u = 0; u < DF; ++u) {
         const int64_t r = rb + u;
@@ -712,7 +723,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   double *tp = TP + tid;
   int64_t ntp = 0;
   double ylast = 0.0;
-  if (!(g_scan_diag & 4)) {
+  if (!(LFD_DG(g_scan_diag) & 4)) {
     int64_t t = G.tail_begin;
     for (; t + SB <= G.s1 + 1; t += SB) {
       float xv[SB];
@@ -731,7 +742,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     }
   }
   const float xr = xc[G.s1 * s_t];
-  for (int i = 0; i < E && !(g_scan_diag & 4); ++i) {
+  for (int i = 0; i < E && !(LFD_DG(g_scan_diag) & 4); ++i) {
     ylast = R.fwd(S, h, (double)(2.0f * xr - xc[(G.s1 - 1 - i) * s_t]));
     tp[(ntp++) * n_thr] = ylast;
   }
@@ -828,7 +839,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     // when run r = r1 - 1 - u is applied)
 #pragma unroll
     for (int u = 0; u < DB; ++u) load_geo(max(G.r1 - 1 - u - DB, G.r0), gq[u]);
-    for (int64_t rb = G.r1 - 1; rb >= G.r0 && !(g_scan_diag & 8); rb -= DB)
+    for (int64_t rb = G.r1 - 1; rb >= G.r0 && !(LFD_DG(g_scan_diag) & 8); rb -= DB)
 #pragma unroll
     for (int u = 0; u < DB; ++u) {
       const int64_t r = rb - u;
@@ -952,7 +963,9 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 // ---------------------------------------------------------------------------
 typedef double fr_d4v __attribute__((ext_vector_type(4)));
 // LFD_FR_STAGE_OLD=1 (A/B knob): the big block's loads in groups of 8 dwords
+#ifdef LFD_DIAG
 __constant__ int g_fr_stage_old = 0;
+#endif
 #ifndef FRS_Q
 // k_fullrate_scan: big blocks per load batch (8: 0.83 ms vs 0.91 at 4 on the
 // 2,000 x 600,000 band-pass; a software-pipelined next batch spills and is
@@ -986,7 +999,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     // per wave in flight, one memory latency per block); time-contiguous,
     // 16-B aligned rows as float4 (1 KB per instruction)
     const float *row = x + ch * s_ch + a * s_t;
-    if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !g_fr_stage_old) {
+    if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !LFD_DG(g_fr_stage_old)) {
       float4 v[L / 256];
 #pragma unroll
       for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
@@ -2430,8 +2443,8 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   // g_k1_band > 0 (A/B knob LFD_K1_BAND) walks bands of that many channel
   // groups, time groups inside a band, so fewer pages are in flight at once
   int64_t cg, grp;
-  if (g_k1_band > 0) {
-    const int64_t band = g_k1_band;
+  if (LFD_DG(g_k1_band) > 0) {
+    const int64_t band = LFD_DG(g_k1_band);
     const int64_t b = unit / (band * rg.n_groups);
     const int64_t base = b * band;
     const int64_t bw = min(band, n_cg - base);
@@ -3136,20 +3149,15 @@ __global__ __launch_bounds__(NT, NTILE == 1 ? 4 : (SEPI ? 2 : 1)) void k_block_r
 
 inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-inline bool getenv_flag(const char *name) {
-  const char *v = std::getenv(name);
-  return v && v[0] && v[0] != '0';
-}
-
 template <int NS, bool FIR32>
 hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
                                 const BlockConst &kc, double *F, hipStream_t st) {
   const bool lds = (s_t == 1) && (g.L % 4 == 0) && (g.base % 4 == 0) && (s_ch % 4 == 0) &&
-                   ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && !getenv_flag("LFD_K1_NOLDS");
+                   ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && !knob_flag("LFD_K1_NOLDS");
   if (lds) {
     const int64_t tiles = ((g.n_ch + 15) / 16) * ((g.nb + 15) / 16);
     k_block_functionals_lds<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(
-        x, s_ch, g, kc, F, getenv_flag("LFD_K1_CHAN_FAST") ? 1 : 0);
+        x, s_ch, g, kc, F, knob_flag("LFD_K1_CHAN_FAST") ? 1 : 0);
   } else {
     const int64_t tiles = ((g.n_ch + 63) / 64) * ((g.nb + 3) / 4);
     k_block_functionals_gen<NS, FIR32><<<dim3((unsigned)tiles), 256, 0, st>>>(x, s_ch, s_t, g,
@@ -3160,7 +3168,8 @@ hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t, const
 
 }  // namespace
 
-hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
+#ifdef LFD_DIAG
+hipError_t launch_block_runs_mfma_tm_ab(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
                                      const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
                                      double *AG, hipStream_t st) {
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || tg.nvar != 1 || tg.v0 != 0 || rg.n_groups < 1)
@@ -3169,10 +3178,10 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   // measured on cfg3 stored time-major (tools/tm_bench.py): no-swap loads at
   // 512 threads / depth 2 14.28 ms, 768 / 1 14.46; permlane loads 14.74-14.89
   int nt = 512, pf = 2;
-  if (const char *v = std::getenv("LFD_TM_NT")) nt = std::atoi(v);
-  if (const char *v = std::getenv("LFD_TM_PF")) pf = std::atoi(v);
+  if (const char *v = knob("LFD_TM_NT")) nt = std::atoi(v);
+  if (const char *v = knob("LFD_TM_PF")) pf = std::atoi(v);
   int ntile = 2;
-  if (const char *v = std::getenv("LFD_TM_NTILE")) ntile = std::atoi(v) == 1 ? 1 : 2;
+  if (const char *v = knob("LFD_TM_NTILE")) ntile = std::atoi(v) == 1 ? 1 : 2;
   size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * ntile * RUN_WB;
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   auto go = [&](auto kern, int NT) -> hipError_t {
@@ -3187,29 +3196,29 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
     return hipGetLastError();
   };
   bool swap = false;
-  if (const char *v = std::getenv("LFD_TM_SWAP")) swap = std::atoi(v) != 0;
+  if (const char *v = knob("LFD_TM_SWAP")) swap = std::atoi(v) != 0;
   // channel-pair loads: need 8-B aligned pairs (even n_ch and row stride)
   const bool x2_ok = g.n_ch % 2 == 0 && s_t % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
-  bool x2 = x2_ok;
-  if (const char *v = std::getenv("LFD_TM_X2")) x2 = x2_ok && std::atoi(v) != 0;
+  bool x2 = x2_ok && !option(LFD_OPT_TM_NO_PAIRS);
+  if (const char *v = knob("LFD_TM_X2")) x2 = x2_ok && std::atoi(v) != 0;
   bool m4 = false;
-  if (const char *v = std::getenv("LFD_TM_M4")) m4 = std::atoi(v) != 0;
-  if (m4 && x2 && !swap && ntile == 2 && (std::getenv("LFD_TM_PF") || std::getenv("LFD_TM_NT"))) {
+  if (const char *v = knob("LFD_TM_M4")) m4 = std::atoi(v) != 0;
+  if (m4 && x2 && !swap && ntile == 2 && (knob("LFD_TM_PF") || knob("LFD_TM_NT"))) {
     if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, true>, 512);
     if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true>, 512);
     return hipErrorInvalidValue;
   }
   // buffer loads at prefetch depth 1: 14.01 vs 14.18 ms on cfg3 stored
   // time-major (in-process A/B, tools/ab_plan.py --tm; bit-identical)
-  bool buf = !std::getenv("LFD_TM_PF") && !std::getenv("LFD_TM_NT");
-  if (const char *v = std::getenv("LFD_TM_BUF")) buf = std::atoi(v) != 0;
+  bool buf = !knob("LFD_TM_PF") && !knob("LFD_TM_NT");
+  if (const char *v = knob("LFD_TM_BUF")) buf = std::atoi(v) != 0;
   if (buf && x2 && !swap && ntile == 2 && s_t < (int64_t)1 << 22) {
-    const int pfb = std::getenv("LFD_TM_PF") ? pf : 1;
+    const int pfb = knob("LFD_TM_PF") ? pf : 1;
     int mode = 0;
-    if (const char *v = std::getenv("LFD_TM_MODE")) mode = std::atoi(v);
+    if (const char *v = knob("LFD_TM_MODE")) mode = std::atoi(v);
     // (LFD_TM_DIAG_LDS=1: the diagnostics allocate only the tap table, so
     // their occupancy is set by registers, not by the run buffers)
-    if (mode >= 3 && getenv_flag("LFD_TM_DIAG_LDS")) lds = tab;
+    if (mode >= 3 && knob_flag("LFD_TM_DIAG_LDS")) lds = tab;
     if (mode == 3 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 3>, 512);
     if (mode == 3) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 3>, 512);
     if (mode == 4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 4>, 512);
@@ -3217,7 +3226,7 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
     // on cfg3 stored time-major (in-process A/B on one allocation,
     // profiles/r03_ab_tm_sepi.txt; A/B knob LFD_TM_SEPI=0)
     bool sepi = true;
-    if (const char *v = std::getenv("LFD_TM_SEPI")) sepi = std::atoi(v) != 0;
+    if (const char *v = knob("LFD_TM_SEPI")) sepi = std::atoi(v) != 0;
     if (sepi && nt == 512) {
       lds = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
       // (LFD_TM_M4=1: v_mfma_f64_4x4x4 steps, a third less matrix-core issue time)
@@ -3250,6 +3259,40 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   }
   return hipErrorInvalidValue;  // no instantiation for this A/B knob combination
 }
+#endif  // LFD_DIAG
+
+hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
+                                     const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
+                                     double *AG, hipStream_t st) {
+#ifdef LFD_DIAG
+  return launch_block_runs_mfma_tm_ab(x, s_t, n_t, g, taps, tg, rg, Y0, AG, st);
+#else
+  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || tg.nvar != 1 || tg.v0 != 0 || rg.n_groups < 1)
+    return hipErrorInvalidValue;
+  const size_t tab = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST);
+  auto go = [&](auto kern, size_t lds) -> hipError_t {
+    if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
+    if (e != hipSuccess) return e;
+    const int64_t units = ((g.n_ch + 31) / 32) * rg.n_groups;  // two 16-channel tiles per wave
+    kern<<<(unsigned)((units + 7) / 8), 512, lds, st>>>(x, s_t, n_t, g, taps, tg, rg, Y0, AG);
+    return hipGetLastError();
+  };
+  // channel-pair loads need 8-B aligned pairs (even n_ch and row stride)
+  const bool x2 = g.n_ch % 2 == 0 && s_t % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
+                  !option(LFD_OPT_TM_NO_PAIRS);
+  if (x2 && s_t < (int64_t)1 << 22)
+    // buffer loads at prefetch depth 1 (14.01 vs 14.18 ms) with the streaming
+    // run epilogue, taps + constants only in LDS (13.85 vs 14.35 ms) on cfg3
+    // stored time-major (profiles/r03_ab_tm_sepi.txt)
+    return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>,
+              sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S));
+  const size_t lds = tab + sizeof(double) * 8 * 2 * RUN_WB;  // + 8 waves x 2 tiles of run buffers
+  if (x2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, lds);
+  return go(&k_block_runs_mfma_tm<2, 512, false>, lds);
+#endif
+}
 
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g, const BlockConst &kc,
@@ -3277,11 +3320,14 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<1, 0>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
+    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
+#ifdef LFD_DIAG
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<1, 0>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6>)}) {
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6>),
+#endif
+                           }) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          TAP_LDS_MAX);
       if (e != hipSuccess) return e;
@@ -3291,23 +3337,24 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   // 16 waves per CU whatever the table size: 4 x 256, 2 x 512 or 1 x 1024 threads
   // share one LDS tap table each
   int threads = lds <= 40 * 1024 ? 256 : (lds <= 80 * 1024 ? 512 : 1024);
-  if (const char *v = std::getenv("LFD_MF_THREADS")) threads = std::max(threads, std::atoi(v));
+  if (const char *v = knob("LFD_MF_THREADS")) threads = std::max(threads, std::atoi(v));
   threads = std::min(threads, 1024);
   int pf = 2, mode = 0;
-  if (const char *v = std::getenv("LFD_MF_PF")) pf = std::atoi(v);
-  if (const char *v = std::getenv("LFD_MF_MODE")) mode = std::atoi(v);
+  if (const char *v = knob("LFD_MF_PF")) pf = std::atoi(v);
+  if (const char *v = knob("LFD_MF_MODE")) mode = std::atoi(v);  // diagnostics (results invalid)
   // blocks per wave: MF_RUN when the array is wide; narrow arrays (the
   // real-time edge runs: 2,000 channels, 44 blocks of 2,000 samples) get
   // fewer so that >= ~4,096 waves (16 per CU) cover the chip
   const int64_t n_cg = (g.n_ch + 15) / 16;
   int bpw = (int)std::max<int64_t>(1, std::min<int64_t>(MF_RUN, n_cg * g.nb / 4096));
-  if (const char *v = std::getenv("LFD_MF_BPW")) bpw = std::max(1, std::min(MF_RUN, std::atoi(v)));
+  if (const char *v = knob("LFD_MF_BPW")) bpw = std::max(1, std::min(MF_RUN, std::atoi(v)));
   const int64_t n_runs = (g.nb + bpw - 1) / bpw;
   const int64_t units = n_cg * n_runs;
   const unsigned grid = nblk(units, threads / 64);
 #define LFD_MF(PF_, MODE_)                                                                      \
   k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
                                                                    n_runs, bpw)
+#ifdef LFD_DIAG
   if (mode == 1)
     LFD_MF(2, 1);
   else if (mode == 3)
@@ -3318,6 +3365,11 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
     LFD_MF(1, 0);
   else
     LFD_MF(2, 0);
+#else
+  (void)pf;
+  (void)mode;
+  LFD_MF(2, 0);
+#endif
 #undef LFD_MF
   return hipGetLastError();
 }
@@ -3343,7 +3395,8 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   return hipGetLastError();
 }
 
-hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+#ifdef LFD_DIAG
+hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
                                   double *Y0, double *AG, hipStream_t st) {
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
@@ -3360,7 +3413,7 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   int mode = 0, pf = 1, nt = 512;
   {
     static int band_set = 0;
-    const char *v = std::getenv("LFD_K1_BAND");
+    const char *v = knob("LFD_K1_BAND");
     const int band = v ? std::max(0, std::atoi(v)) : 0;
     if (band != band_set) {
       hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_k1_band), &band, sizeof(int), 0,
@@ -3371,16 +3424,16 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
       band_set = band;
     }
   }
-  if (const char *v = std::getenv("LFD_RUN_MODE")) mode = std::atoi(v);
-  if (const char *v = std::getenv("LFD_RUN_PF")) pf = std::atoi(v);
-  if (const char *v = std::getenv("LFD_RUN_NT")) nt = std::atoi(v);
+  if (const char *v = knob("LFD_RUN_MODE")) mode = std::atoi(v);
+  if (const char *v = knob("LFD_RUN_PF")) pf = std::atoi(v);
+  if (const char *v = knob("LFD_RUN_NT")) nt = std::atoi(v);
   // three v_mfma_f64_4x4x4_4b per step instead of one 16x16x4 (mf_iter4)
   bool m4 = false;
-  if (const char *v = std::getenv("LFD_RUN_M4")) m4 = std::atoi(v) != 0;
+  if (const char *v = knob("LFD_RUN_M4")) m4 = std::atoi(v) != 0;
   int minw = 4;  // LFD_RUN_MINW=0: the compiler's register allocation
-  if (const char *v = std::getenv("LFD_RUN_MINW")) minw = std::atoi(v);
+  if (const char *v = knob("LFD_RUN_MINW")) minw = std::atoi(v);
   bool bufl = false;  // LFD_RUN_BUF=1: buffer loads (A/B knob)
-  if (const char *v = std::getenv("LFD_RUN_BUF")) bufl = std::atoi(v) != 0;
+  if (const char *v = knob("LFD_RUN_BUF")) bufl = std::atoi(v) != 0;
   if (bufl && 16 * s_ch + 64 < ((int64_t)1 << 29) && mode == 0 && nt == 512 && minw == 4 && !m4) {
     if (pf == 2) return run_k1<2, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     if (pf == 1) return run_k1<1, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
@@ -3391,7 +3444,7 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   // on a 1,250-channel shard; profiles/r03_ab_cm_sepi.txt), where 16 waves
   // per CU already hide the run-end sweep
   bool sepi = false;
-  if (const char *v = std::getenv("LFD_RUN_SEPI")) sepi = std::atoi(v) != 0;
+  if (const char *v = knob("LFD_RUN_SEPI")) sepi = std::atoi(v) != 0;
   if (sepi && mode == 0 && nt == 512 && !m4 && !bufl) {
     if (minw == 4 && pf == 1) return run_k1<1, 0, 512, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     if (minw == 4 && pf == 2) return run_k1<2, 0, 512, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
@@ -3425,6 +3478,22 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   // an A/B knob combination without an instantiation: refuse rather than run
   // (and let a record label) a configuration that never ran
   return hipErrorInvalidValue;
+}
+#endif  // LFD_DIAG
+
+hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+                                  const double *taps, const TapGeom &tg, const RunGeom &rg,
+                                  double *Y0, double *AG, hipStream_t st) {
+#ifdef LFD_DIAG
+  return launch_block_runs_mfma_ab(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, st);
+#else
+  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
+  const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
+  // 512-thread workgroups (2 per CU: 16 waves), prefetch depth 1, registers
+  // capped for 4 waves per SIMD: 12.77 ms vs 13.09-13.12 for depth 2 at the
+  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt)
+  return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3636,22 +3705,22 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   // cfg3) 0.247 -> 0.152 ms, 2,500 ch 0.263 -> 0.191, 5,000 ch equal, 10,000
   // ch 0.339 -> 0.431 (the TR round trip); and when the chunks hold long
   // run chains (dt = 10 s at 1 kHz: ~300 runs per chunk, 0.79 -> 0.67 ms);
-  // A/B knob LFD_SCAN_DEFER=0/1
+  // option LFD_OPT_SCAN_DEFER = 1 / 2 forces in-chain / deferred outputs
   bool defer = n_chunks * g.n_ch < 40000 || rg.n_sr >= 128 * n_chunks;
-  if (const char *dv = std::getenv("LFD_SCAN_DEFER")) defer = std::atoi(dv) != 0;
+  if (const int64_t o = option(LFD_OPT_SCAN_DEFER)) defer = o == 2;
   if (TR && CR && slot_chunk && defer) {
     // narrow shards: 64-thread workgroups (one wave per CU instead of four
     // sharing one): 1,250 channels 0.150 -> 0.126 ms, bit-identical
     // (profiles/r03_ab_scan_narrow.txt; A/B knob LFD_SCAN_DEFER_THREADS)
     int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
-    if (const char *tv = std::getenv("LFD_SCAN_DEFER_THREADS")) dthr = std::atoi(tv) == 64 ? 64 : (std::atoi(tv) == 128 ? 128 : 256);
+    if (const char *tv = knob("LFD_SCAN_DEFER_THREADS")) dthr = std::atoi(tv) == 64 ? 64 : (std::atoi(tv) == 128 ? 128 : 256);
     const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
     // long run chains (>= 128 runs per chunk) keep 16 / 8 runs in flight
     // instead of 4 / 2: dt = 10 s at 1 kHz 0.401 -> 0.352 ms, bit-identical;
     // narrow shards measure the same either way (profiles/r03_ab_scan_deep.txt;
     // A/B knob LFD_SCAN_DEEP=0/1)
     bool deep = rg.n_sr >= 128 * n_chunks;
-    if (const char *dv = std::getenv("LFD_SCAN_DEEP")) deep = std::atoi(dv) != 0;
+    if (const char *dv = knob("LFD_SCAN_DEEP")) deep = std::atoi(dv) != 0;
     if (deep)
       k_chunk_scan<2, true, true, 16, 8><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                                               tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR);
@@ -3664,18 +3733,22 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     k_run_outputs<<<nblk(waves, 4), 256, 0, st>>>(g, cg, rg, slot_chunk, Y0, SR, TR, CR, y, ys_ch, ys_t);
     return hipGetLastError();
   }
-  static int diag = -1, threads = 256;
+  int threads = 256;
+#ifdef LFD_DIAG
+  static int diag = -1, threads_ab = 256;
   if (diag < 0) {
-    const char *v = std::getenv("LFD_SCAN_DIAG");
+    const char *v = knob("LFD_SCAN_DIAG");
     diag = v ? std::atoi(v) : 0;
     if (diag) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_scan_diag), &diag, sizeof(int));
     // workgroup size A/B knob (64, 128 or 256 threads; the kernel's LDS
     // staging is per wave and its launch bound is 256)
-    if (const char *t = std::getenv("LFD_SCAN_THREADS")) {
+    if (const char *t = knob("LFD_SCAN_THREADS")) {
       const int w = std::atoi(t);
-      if (w == 64 || w == 128 || w == 256) threads = w;
+      if (w == 64 || w == 128 || w == 256) threads_ab = w;
     }
   }
+  threads = threads_ab;
+#endif
   const unsigned nb = nblk(n_chunks * g.n_ch, threads);
   k_chunk_scan<2, true><<<nb, threads, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                             tp_len, y, ys_ch, ys_t, rg, Y0);
@@ -3709,11 +3782,13 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
                                   hipStream_t st) {
   const int64_t n_wg = n_ch * nb;
   if (n_wg < 1 || n_wg > INT32_MAX) return hipErrorInvalidValue;
+#ifdef LFD_DIAG
   static int stage_old = -1;
   if (stage_old < 0) {
-    stage_old = getenv_flag("LFD_FR_STAGE_OLD") ? 1 : 0;
+    stage_old = knob_flag("LFD_FR_STAGE_OLD") ? 1 : 0;
     if (stage_old) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stage_old), &stage_old, sizeof(int));
   }
+#endif
 #define LFD_FR(NS, OUT)                                                                                \
   k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
                                                          ys_t)
@@ -3792,7 +3867,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
   // directly reads it W/S times from L2/L1 (W/S = 4: 5.25 ms vs 3.81 ms on
   // cfg2), so the scan takes every W > 2S (A/B knob LFD_ROLL_DIRECT_MAX)
   int64_t direct_max = 2;
-  if (const char *v = std::getenv("LFD_ROLL_DIRECT_MAX")) direct_max = std::atoll(v);
+  if (const char *v = knob("LFD_ROLL_DIRECT_MAX")) direct_max = std::atoll(v);
   // segment prefix sums (k_rolling_seg) when g = gcd(W, S) >= 16 and the
   // prefix ring fits: no per-position running sum (A/B knob LFD_ROLL_SEGSUM=0)
   {
@@ -3807,10 +3882,10 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     while (ring < W / g + RG_P / g + 3) ring *= 2;
     bool seg = s_t == 1 && S > 1 && S < W && g >= 16 && ring <= 1024 && n_t < (int64_t)INT32_MAX - 2 * RG_P &&
                (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
-    if (const char *v = std::getenv("LFD_ROLL_SEGSUM")) seg = seg && std::atoi(v) != 0;
+    if (const char *v = knob("LFD_ROLL_SEGSUM")) seg = seg && std::atoi(v) != 0;
     if (seg) {
       int64_t span = std::max<int64_t>(32768, 8 * W);
-      if (const char *v = std::getenv("LFD_ROLL_SEG")) span = std::max<int64_t>(4 * W, std::atoll(v));
+      if (const char *v = knob("LFD_ROLL_SEG")) span = std::max<int64_t>(4 * W, std::atoll(v));
       while (span > std::max<int64_t>(4096, 4 * W) && n_ch * ((n_t + span - 1) / span) < 16384) span /= 2;
       const int64_t seg_out = std::max<int64_t>(1, span / S);
       const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
@@ -3841,7 +3916,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // overlapping windows: running sum over segments of >= max(32768, 4W)
     // positions (halo W per segment), fewer when that leaves the chip idle
     int64_t seg_pos = std::max<int64_t>(32768, 4 * W);
-    if (const char *v = std::getenv("LFD_ROLL_SEG")) seg_pos = std::max<int64_t>(4 * W, std::atoll(v));
+    if (const char *v = knob("LFD_ROLL_SEG")) seg_pos = std::max<int64_t>(4 * W, std::atoll(v));
     while (seg_pos > std::max<int64_t>(4096, 4 * W) && n_ch * ((n_t + seg_pos - 1) / seg_pos) < 16384)
       seg_pos /= 2;
     const int64_t seg_out = std::max<int64_t>(1, seg_pos / S);
@@ -3854,18 +3929,18 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // LDS as coalesced float4 stores) measured best on cfg2 at S = 1: 4.77 ms
     // vs 5.93 (0), 5.99 (1), 5.54 (3)
     int stage = 2;
-    if (const char *v = std::getenv("LFD_ROLL_STAGE")) stage = std::atoi(v) & 3;
+    if (const char *v = knob("LFD_ROLL_STAGE")) stage = std::atoi(v) & 3;
     int npf = 1, minw = 3;
-    if (const char *v = std::getenv("LFD_ROLL_PF")) npf = std::atoi(v);
-    if (const char *v = std::getenv("LFD_ROLL_MINW")) minw = std::atoi(v);
+    if (const char *v = knob("LFD_ROLL_PF")) npf = std::atoi(v);
+    if (const char *v = knob("LFD_ROLL_MINW")) minw = std::atoi(v);
     // the per-step wave scan on DPP lane moves (A/B knob LFD_ROLL_DPP=0: shuffles)
     bool dpp = true;
-    if (const char *v = std::getenv("LFD_ROLL_DPP")) dpp = std::atoi(v) != 0;
+    if (const char *v = knob("LFD_ROLL_DPP")) dpp = std::atoi(v) != 0;
     // LDS ring for x[t - W] (vector rows, W + 512 <= 4096): A/B knob LFD_ROLL_RING
     int ring = 0;
     while (ring < W + RS_P) ring = ring ? 2 * ring : 1024;
     bool use_ring = vec && ring <= 4096 && stage == 2 && npf == 1 && minw == 3;
-    if (const char *v = std::getenv("LFD_ROLL_RING")) use_ring = use_ring && std::atoi(v) != 0;
+    if (const char *v = knob("LFD_ROLL_RING")) use_ring = use_ring && std::atoi(v) != 0;
     if (use_ring) {
       static bool attr = false;
       if (!attr) {
@@ -3883,6 +3958,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                                              ys_t, (int)seg_out, V && vec_out, 0, dpp)
     if (!vec)
       LFD_ROLL(false, 0, 1);
+#ifdef LFD_DIAG
     else if (stage == 2 && npf == 1 && minw == 4)
       k_rolling_scan_tc<true, 2, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
                                                                       ys_ch, ys_t, (int)seg_out, vec_out, 0, dpp);
@@ -3897,10 +3973,11 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
       LFD_ROLL(true, 0, 1);
     else if (stage == 1)
       LFD_ROLL(true, 1, 1);
-    else if (stage == 2)
-      LFD_ROLL(true, 2, 1);
-    else
+    else if (stage == 3)
       LFD_ROLL(true, 3, 1);
+#endif
+    else
+      LFD_ROLL(true, 2, 1);
 #undef LFD_ROLL
   } else {
     const int64_t seg_out = S >= W ? 64 : std::max<int64_t>(1, std::max<int64_t>(4096, 4 * W) / S);
@@ -4043,6 +4120,7 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
                                                           double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
                                                           int diag) {
   constexpr int DM = FDM_DM, NO = FDM_NO, NN = FDM_NN, RL = fdm_rl();
+  diag = LFD_DG(diag);                     // production: 0, the diagnostics compile out
   constexpr int SPAN = NN * Q;             // samples per channel and tile
   constexpr int NR = (SPAN + 63) / 64;     // staging loads per lane
   constexpr int JB = Q * RL + 32;          // j-block stride (floats)
@@ -4211,15 +4289,15 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
   const int U = (int)((n_taps + q - 1) / q);  // taps per polyphase branch
   // matrix-core path (time-contiguous rows, q in {4, 5, 6, 8, 10}, phase 0
   // at most 22 taps, the others 21: n_taps <= 21 q + 1)
-  if (s_t == 1 && n_taps <= 21 * q + 1 && !getenv_flag("LFD_FIR_VALU")) {
+  if (s_t == 1 && n_taps <= 21 * q + 1 && !option(LFD_OPT_FIR_VALU)) {
     const int64_t tiles_o = (n_out + FDM_NO - 1) / FDM_NO;
     int strip = 8;
-    if (const char *sv = std::getenv("LFD_FIR_STRIP")) strip = std::max(1, std::atoi(sv));
+    if (const char *sv = knob("LFD_FIR_STRIP")) strip = std::max(1, std::atoi(sv));
     if (strip > tiles_o) strip = (int)tiles_o;
     const int64_t grid = (n_ch + 3) / 4 * ((tiles_o + strip - 1) / strip);
     int diag = 0;
-    if (const char *dv = std::getenv("LFD_FIR_DIAG")) diag = std::atoi(dv);
-    const bool db = getenv_flag("LFD_FIR_DB");
+    if (const char *dv = knob("LFD_FIR_DIAG")) diag = std::atoi(dv);
+    const bool db = knob_flag("LFD_FIR_DB");  // double-buffered staging (measured, not kept)
     bool launched = false;
     hipError_t e = hipSuccess;
 #define LFD_FDM1(QV, DBV)                                                                                    \
@@ -4234,6 +4312,7 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     k_fir_decimate_mfma<QV, DBV><<<(unsigned)grid, 256, fdm_lds_bytes<QV, DBV>(), st>>>(                    \
         x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, diag);                  \
   }
+#ifdef LFD_DIAG
 #define LFD_FDM(QV)          \
   case QV: {                 \
     if (db)                  \
@@ -4243,6 +4322,15 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     launched = true;         \
     break;                   \
   }
+#else
+#define LFD_FDM(QV)          \
+  case QV: {                 \
+    (void)db;                \
+    LFD_FDM1(QV, false)      \
+    launched = true;         \
+    break;                   \
+  }
+#endif
     if (grid <= (int64_t)INT32_MAX) {
       switch (q) {
         LFD_FDM(4)

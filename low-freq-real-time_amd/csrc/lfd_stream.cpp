@@ -485,7 +485,7 @@ int lfd_stream_open(lfd_stream **out, const lfd_stream_config *cfg, const double
   s->out_ns = out_ns;
   s->dry = (cfg->flags & LFD_STREAM_DRY_RUN) != 0;
   {
-    const char *v = std::getenv("LFD_STREAM_DIRECT2D");
+    const char *v = lfd::knob("LFD_STREAM_DIRECT2D");
     s->direct2d = v && v[0] && v[0] != '0';
   }
   if (cfg->mode == LFD_STREAM_CONTINUOUS) {

@@ -7,6 +7,7 @@ g.build()"`` (or ``make -C low-freq-real-time_amd/csrc``).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -114,6 +115,8 @@ def load():
         "lfd_version": ([], i32),
         "lfd_device_count": ([P(i32)], i32),
         "lfd_set_timing": ([i32], i32),
+        "lfd_set_option": ([i32, i64], i32),
+        "lfd_get_option": ([i32, P(i64)], i32),
         "lfd_lowpass_plan_create": ([P(vp), vp, i32, i32, i64, i64, vp, vp, i64,
                                      vp, i64], i32),
         "lfd_lowpass_plan_info": ([vp, P(sz), P(i64), P(i64)], i32),
@@ -166,7 +169,7 @@ def load():
 
 
 EXPORTED = (
-    "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing",
+    "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing", "lfd_set_option", "lfd_get_option",
     "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute",
     "lfd_lowpass_last_timing", "lfd_lowpass_timings", "lfd_lowpass_plan_destroy",
     "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_debug_runs",
@@ -178,6 +181,32 @@ EXPORTED = (
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
     "lfd_host_alloc", "lfd_host_free", "lfd_host_register", "lfd_host_unregister", "lfd_demean_scale_f64", "lfd_median_filter_f64",
 )
+
+
+# include/lfdas.h LFD_OPT_*: result-neutral kernel-selection overrides (the
+# library reads no environment variable; tests drive the fallback kernels
+# through these)
+OPTIONS = {"no_runs": 1, "k1_recurrence": 2, "tm_no_pairs": 3, "scan_defer": 4, "fullrate_serial": 5,
+           "no_lattice": 6, "no_head_skip": 7, "fir_valu": 8}
+
+
+@contextlib.contextmanager
+def kernel_options(**kw):
+    """Set LFD_OPT_* overrides (``no_runs=1``, ``scan_defer=2`` ...) for the
+    body of a ``with`` block, restoring the previous values afterwards."""
+    lib = load()
+    old = {}
+    try:
+        for name, v in kw.items():
+            oid = OPTIONS[name]
+            cur = ctypes.c_int64()
+            check(lib.lfd_get_option(oid, ctypes.byref(cur)))
+            old[oid] = cur.value
+            check(lib.lfd_set_option(oid, int(v)))
+        yield
+    finally:
+        for oid, v in old.items():
+            lib.lfd_set_option(oid, v)
 
 
 def check(rc: int):

@@ -127,7 +127,7 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
     para = LFProc(None)._default_process_parameters()
     para.update({k: v for k, v in params.items() if k in para})
     tg = S.time_grid(bgtime, edtime, para["output_sample_interval"])
-    sched = S.lfproc_chunks(len(tg), para["process_patch_size"], para["edge_buff_size"])
+    sched, kinds = S.lfproc_chunks(len(tg), para["process_patch_size"], para["edge_buff_size"], with_kind=True)
     counts = [ob - oa for _, _, oa, ob in sched]
     sub, (c0, c1) = shard_spool(sp, world, rank)
     run_shard = run_shard or (lambda s, a, b, p: lfproc_shard(s, a, b, p, device))
@@ -178,8 +178,11 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
                     attrs=attrs).update_attrs(d_time=para["output_sample_interval"])
         res.append(out)
         if rank == 0 and output_folder and (world == 1 or gather):
-            if verbose:
-                print("Processing patch ", str(i))
+            if verbose:  # the reference's messages (lf_das.py:263,276,290)
+                if kinds[i - 1] == "tail":
+                    print(f"Processing patch {i} (Last portion of data)")
+                else:
+                    print("Processing patch ", str(i))
             os.makedirs(output_folder, exist_ok=True)
             out.io.write(os.path.join(output_folder, _get_filename(out.attrs["time_min"], out.attrs["time_max"])),
                          "dasdae")

@@ -230,3 +230,15 @@ def test_bench_refuses_more_gpus_than_present_and_launcher_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr and "{" not in r.stdout
+
+
+def test_sharded_driver_prints_reference_messages(tmp_path, capsys):
+    """Rank 0 prints the reference's per-chunk messages, the tail chunk as
+    ``Processing patch {i} (Last portion of data)`` (lf_das.py:263,276,290)."""
+    import lfdas.dc as dc
+    from lfdas.shard import process_time_range_sharded
+    process_time_range_sharded(dc.get_example_spool(), T1, T2, PARAMS, output_folder=str(tmp_path / "o"),
+                               run_shard=_oracle_shard, verbose=True)
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("Processing patch")]
+    assert lines == ["Processing patch  1", "Processing patch  2", "Processing patch  3",
+                     "Processing patch 4 (Last portion of data)"]

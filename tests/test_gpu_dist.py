@@ -118,3 +118,120 @@ def test_sharded_device_compute_world2_gap_raises_on_every_rank(tmp_path):
     got = _run(2, str(tmp_path / "o"), gap=2.0)
     assert [g[1] for g in got] == ["error", "error"]
     assert all("patch merge failed! Gap in data exists" in g[3] for g in got)
+
+
+# --- the out-of-core form (cfg5 across GPUs: shard_stream + push_rows) ------
+
+S_T0 = 1_679_464_800_000_000_000  # 2023-03-22T06:00:00 (the edge notebook's start)
+S_FS, S_DT_NS = 200.0, 5_000_000  # cfg5: 200 Hz, dt = 10 s, P = 120, B = 6
+S_NCH, S_PUSH, S_NPUSH = 37, 12_000, 48  # ragged 19 + 18 channels, 60 s pushes, 48 min
+
+
+def _stream_block(k, time_major):
+    """Full-width host block k of the synthetic spool (every rank makes the
+    same one; only its own rows are pinned and pushed)."""
+    import synth
+    b = synth.noise_sine(S_NCH, S_PUSH, S_FS, seed=500 + k, dc=3.0)
+    return np.ascontiguousarray(b.T) if time_major else b
+
+
+def _stream_rank(rank, world, port, time_major, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from lfdas.shard import pin_rows, push_rows, shard_stream
+        t_end = S_T0 + (S_PUSH * S_NPUSH - 1) * S_DT_NS
+        st, (c0, c1) = shard_stream(S_NCH, S_DT_NS, output_sample_interval=10.0, process_patch_size=120,
+                                    edge_buff_size=6, mode="continuous", t_start=S_T0, t_end=t_end,
+                                    capacity=int(1300 * S_FS) + 2 * S_PUSH, device="cuda:0")
+        st.reserve(S_PUSH)
+        ys, ts, counts = [], [], []
+        tax = 0 if time_major else 1
+        pins = []
+        try:
+            for k in range(S_NPUSH):
+                blk = _stream_block(k, time_major)
+                if not time_major:  # this rank's rows page-locked in place: one direct DMA
+                    pins.append(pin_rows(blk, (c0, c1)))
+                o = push_rows(st, blk, (c0, c1), S_T0 + k * S_PUSH * S_DT_NS, time_axis=tax)
+                if o.n_out:
+                    ys.append(st.fetch())
+                    ts.append(o.times_ns)
+                    counts.extend(c for c in o.chunk_counts if c > 0)
+                else:
+                    st.wait_copy()
+                for p in pins:
+                    p.release()
+                pins.clear()
+            o = st.flush()
+            if o.n_out:
+                ys.append(st.fetch())
+                ts.append(o.times_ns)
+                counts.extend(c for c in o.chunk_counts if c > 0)
+            st.synchronize()
+        finally:
+            for p in pins:
+                p.release()
+            st.close()
+        q.put((rank, (c0, c1), np.concatenate(ys, axis=1), np.concatenate(ts), counts))
+    except Exception as e:  # reported, so the test fails with the rank's error
+        q.put((rank, None, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("time_major", [False, True])
+def test_shard_stream_world2_device_matches_oracle(time_major):
+    """cfg5 geometry (200 Hz, dt = 10 s, P = 120, B = 6) streamed in 60 s
+    pushes through ``shard_stream`` + ``push_rows`` on two gloo ranks sharing
+    cuda:0: each rank's device outputs for its channel block (19 + 18 of 37)
+    equal the oracle's process_time_range over the whole spool (relRMS <=
+    1e-4 per rank, on every channel incl. each block's first and last),
+    with identical output times and chunk (file) boundaries."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, os.path.dirname(here),
+                                                os.path.join(os.path.dirname(here), "low-freq-real-time_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_rank, args=(r, 2, port, time_major, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = []
+    try:
+        for _ in range(2):
+            got.append(q.get(timeout=100))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    except queue.Empty:
+        pytest.fail("a rank did not report within 100 s")
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    got = sorted(got, key=lambda g: g[0])
+    for g in got:
+        assert g[1] is not None, g[2]
+    import oracle
+    x = np.concatenate([_stream_block(k, False) for k in range(S_NPUSH)], axis=1)
+    ref = oracle.lfproc_process(x, S_T0, S_DT_NS, S_T0, S_T0 + (S_PUSH * S_NPUSH - 1) * S_DT_NS, 10.0, 120, 6)
+    want = np.concatenate([r for _, r in ref], axis=1)
+    want_t = np.concatenate([t for t, _ in ref])
+    assert [g[1] for g in got] == [(0, 19), (19, 37)]
+    for _, (c0, c1), y, t, counts in got:
+        np.testing.assert_array_equal(t, want_t)
+        assert counts == [len(tt) for tt, _ in ref if len(tt)]
+        assert y.shape == (c1 - c0, want.shape[1])
+        w = want[c0:c1]
+        rel = float(np.sqrt(np.sum((y.astype(np.float64) - w) ** 2) / np.sum(w ** 2)))
+        assert rel < 1e-4, rel
+        for r in (0, c1 - c0 - 1):  # the block's first and last channel alone
+            rr = float(np.sqrt(np.sum((y[r].astype(np.float64) - w[r]) ** 2) / np.sum(w[r] ** 2)))
+            assert rr < 1e-4, (c0 + r, rr)

@@ -6,6 +6,7 @@ import pytest
 
 import oracle
 from lfdas import schedule as S
+from lfdas._lib import kernel_options
 
 pytestmark = pytest.mark.gpu
 
@@ -127,7 +128,7 @@ def _plan_cfg(fs, dt_out, P, B, n_ch, n):
     (200.0, 10.0, 100, 7, 5, 600_000),  # R = 2000: 4 sub-blocks of 500
     (1000.0, 0.5, 40, 4, 18, 100_003),  # L = 500, odd n_t (channel stride % 4 != 0 -> recurrence)
 ])
-def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
+def test_k1_mfma_matches_recurrence(cfg):
     """Both block-functional kernels feed the same scan: outputs agree to
     float32 rounding; the dispatch picks MFMA only for aligned rows."""
     import torch
@@ -138,15 +139,12 @@ def test_k1_mfma_matches_recurrence(cfg, monkeypatch):
     xd = torch.from_numpy(x).cuda()
     ws = plan.alloc_workspace()
     out = {}
+    opts = {"default": {}, "noruns": {"no_runs": 1}, "rec": {"no_runs": 1, "k1_recurrence": 1},
+            "recfold": {"k1_recurrence": 1}}
     for mode in ("default", "noruns", "rec", "recfold"):
-        if mode == "noruns":
-            monkeypatch.setenv("LFD_NO_RUNS", "1")
-        if mode == "rec":
-            monkeypatch.setenv("LFD_K1_REC", "1")
-        if mode == "recfold":
-            monkeypatch.delenv("LFD_NO_RUNS")
         yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
-        plan.execute(xd, yd, ws)
+        with kernel_options(**opts[mode]):
+            plan.execute(xd, yd, ws)
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
     aligned = n % 4 == 0
@@ -443,7 +441,7 @@ def test_nonfinite_samples_poison_their_chunk_only(where, layout):
     (1000.0, 0.5, 40, 4, 18, 100_003, 18),  # odd n_t
     (250.0, 0.2, 40, 6, 70, 6000, 72),      # even channels (channel-pair loads), ragged last wave
 ])
-def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
+def test_k1_time_major_fold_matches_blocks(cfg):
     """(time, channel) storage viewed as (channel, time) (s_ch = 1, s_t =
     row width): the time-major MFMA run kernel and the recurrence K1 + run
     fold agree with the per-block scan and with the oracle, nulls included."""
@@ -457,15 +455,13 @@ def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
     assert xd.stride() == (1, width)
     ws = plan.alloc_workspace()
     out = {}
+    # nox2: one dword load per channel instead of channel pairs
+    opts = {"default": {}, "nox2": {"tm_no_pairs": 1}, "recfold": {"tm_no_pairs": 1, "k1_recurrence": 1},
+            "blocks": {"tm_no_pairs": 1, "k1_recurrence": 1, "no_runs": 1}}
     for mode in ("default", "nox2", "recfold", "blocks"):
-        if mode == "nox2":  # one dword load per channel instead of channel pairs
-            monkeypatch.setenv("LFD_TM_X2", "0")
-        if mode == "recfold":
-            monkeypatch.setenv("LFD_K1_REC", "1")
-        if mode == "blocks":
-            monkeypatch.setenv("LFD_NO_RUNS", "1")
         yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
-        plan.execute(xd, yd, ws)
+        with kernel_options(**opts[mode]):
+            plan.execute(xd, yd, ws)
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
     assert out["default"][1] == "mfma_runs_tm"
@@ -495,16 +491,16 @@ def test_k1_time_major_fold_matches_blocks(cfg, monkeypatch):
 
 
 @pytest.mark.parametrize("off_ns", [0, 1_900_000])
-def test_scan_deferred_outputs_bit_identical(off_ns, monkeypatch):
+def test_scan_deferred_outputs_bit_identical(off_ns):
     """Run-mode scan with the outputs inside the backward chain
-    (LFD_SCAN_DEFER=0) and deferred to k_run_outputs (=1): same arithmetic,
-    bit-identical outputs, both against the oracle."""
+    (option scan_defer=1) and deferred to k_run_outputs (=2): same
+    arithmetic, bit-identical outputs, both against the oracle."""
     fs, dt_out, P, B, n_ch, dur = 500.0, 1.0, 60, 7, 70, 400.0
     x = (np.random.default_rng(3).standard_normal((n_ch, int(dur * fs))) + 5.0).astype(np.float32)
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("LFD_SCAN_DEFER", mode)
-        out[mode] = _run(x, fs, dt_out, P, B, "tc", off_ns=off_ns)
+        with kernel_options(scan_defer=1 + int(mode)):
+            out[mode] = _run(x, fs, dt_out, P, B, "tc", off_ns=off_ns)
         assert _run.last_kernel == "mfma_runs"
     np.testing.assert_array_equal(out["0"][0], out["1"][0])
     y, ref, sched = out["1"]

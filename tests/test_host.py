@@ -29,6 +29,52 @@ def test_library_exports_every_header_symbol():
     assert lib.lfd_version() >= 100
 
 
+def test_production_library_reads_no_environment():
+    """liblfdas.so (the product) holds no getenv call site and no LFD_* knob
+    name: its outputs and kernel choices cannot depend on the environment.
+    The A/B knobs and the "timing only" diagnostic modes exist only in
+    liblfdas_diag.so (-DLFD_DIAG), which tools/ load through LFDAS_LIB."""
+    import subprocess
+    so = os.path.join(os.path.dirname(_lib.__file__), "liblfdas.so")
+    blob = open(so, "rb").read()
+    assert [m for m in re.findall(rb"LFD_[A-Z0-9_]{3,}", blob) if not m.startswith(b"LFD_OPT_")] == []
+    und = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True).stdout
+    assert "getenv" not in und
+    diag = os.path.join(os.path.dirname(_lib.__file__), "liblfdas_diag.so")
+    assert b"LFD_TM_MODE" in open(diag, "rb").read()
+    # the sources: every getenv sits behind LFD_DIAG
+    for f in ("lfd_kernels.hip", "lfd_capi.cpp", "lfd_stream.cpp", "lfd_internal.h"):
+        src = open(os.path.join(ROOT, "low-freq-real-time_amd", "csrc", f)).read()
+        guarded = []  # per open #if: is it the LFD_DIAG branch
+        for ln in src.splitlines():
+            t = ln.strip()
+            if t.startswith("#if"):
+                guarded.append(t.startswith("#ifdef LFD_DIAG") or t == "#if defined(LFD_DIAG)")
+            elif t.startswith("#el") and guarded:
+                guarded[-1] = False
+            elif t.startswith("#endif") and guarded:
+                guarded.pop()
+            if "getenv(" in t and not t.startswith("//"):
+                assert any(guarded), (f, ln)
+        assert guarded == [], f
+
+
+def test_kernel_options_roundtrip_and_validation():
+    lib = _lib.load()
+    import ctypes
+    v = ctypes.c_int64(-1)
+    for name, oid in _lib.OPTIONS.items():
+        assert lib.lfd_get_option(oid, ctypes.byref(v)) == 0 and v.value == 0, name
+    with _lib.kernel_options(no_runs=1, scan_defer=2):
+        lib.lfd_get_option(_lib.OPTIONS["scan_defer"], ctypes.byref(v))
+        assert v.value == 2
+    lib.lfd_get_option(_lib.OPTIONS["scan_defer"], ctypes.byref(v))
+    assert v.value == 0
+    assert lib.lfd_set_option(99, 1) == _lib.LFD_EINVAL
+    assert lib.lfd_set_option(_lib.OPTIONS["no_runs"], 3) == _lib.LFD_EINVAL
+    assert lib.lfd_set_option(_lib.OPTIONS["scan_defer"], 3) == _lib.LFD_EINVAL
+
+
 def test_design_matches_oracle():
     for fs, fc in [(250.0, 1.0), (500.0, 0.45), (200.0, 0.045), (2000.0, 0.45)]:
         np.testing.assert_array_equal(lowpass_sos(fs, fc), oracle.butter_sos(4, fc / (fs / 2)))
