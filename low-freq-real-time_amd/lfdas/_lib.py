@@ -108,6 +108,10 @@ def load():
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover
         raise LFDLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    if os.path.basename(LIB_PATH) != "liblfdas.so":
+        import sys
+        print(f"lfdas: loaded {LIB_PATH} (not the product library: in the diagnostic build LFD_* "
+              "environment knobs change kernels, some into timing-only modes)", file=sys.stderr)
     i64, i32, vp, sz = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
     P = ctypes.POINTER
     sig = {

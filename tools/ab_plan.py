@@ -8,12 +8,16 @@ slower), so variants are compared on the same tensor, alternating.
         [--ch 10000] [--off-ns 0] [--reps 4] "SPEC" "SPEC" ...
 
 SPEC = space-separated NAME=VALUE env settings ("" = defaults). Outputs of
-every spec are compared bit for bit with the first spec's."""
+every spec are compared bit for bit with the first spec's (y is filled with
+NaN before every compared execute, so a variant that writes nothing cannot
+pass as identical).  The knobs exist only in the diagnostic build: this tool
+loads liblfdas_diag.so (LFDAS_LIB), never the product library."""
 import argparse
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("LFDAS_LIB", os.path.join(ROOT, "low-freq-real-time_amd", "lfdas", "liblfdas_diag.so"))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "low-freq-real-time_amd"))
 
@@ -71,6 +75,7 @@ for rep in range(a.reps):
             plan, *_ = bench.build_plan(a.ch, n, a.fs, a.dt, a.P, a.B, a.off_ns)
             del wsb
             wsb = plan.alloc_workspace(dev)
+        y.fill_(float("nan"))
         plan.execute(x, y, wsb, st)
         torch.cuda.synchronize()
         if ref is None:
