@@ -336,6 +336,11 @@ int lfd_stream_last_timing(const lfd_stream *s, float *ms_copy, float *ms_run);
 int lfd_stream_info(const lfd_stream *s, int64_t *capacity, int64_t *held_samples,
                     int64_t *t_first_held_ns);
 void lfd_stream_close(lfd_stream *s);
+/* Testing hook: low-pass plans this stream has built and plan-cache hits.
+ * Uniform grids are cached by (first point, spacing, fraction); lattice grids
+ * (3 kHz on integer-ns times) by their structure alone, the fractions being
+ * computed on device per run, so a steady stream builds only a few plans. */
+int lfd_debug_stream_plans(const lfd_stream *s, int64_t *created, int64_t *hits);
 
 /* Pinned host memory for pushes (hipHostMalloc). */
 int lfd_host_alloc(void **p, size_t bytes);

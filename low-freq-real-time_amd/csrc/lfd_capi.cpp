@@ -1224,6 +1224,12 @@ int lfd_lowpass_plan_info(const lfd_lowpass_plan *p, size_t *ws, int64_t *nb, in
 int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
                         int64_t s_t, float *y, int64_t ys_ch, int64_t ys_t,
                         void *workspace, void *stream) {
+  return lfd::lowpass_execute_gen(p, x, s_ch, s_t, y, ys_ch, ys_t, workspace, stream, lfd::GridGen{});
+}
+}  // extern "C"
+
+int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
+                             int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const lfd::GridGen &gen) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
   if (!x || !y || !workspace) return fail(LFD_EINVAL, "x, y and workspace must be device pointers");
   if (s_t == 0 || (p->n_ch > 1 && s_ch == 0)) return fail(LFD_EINVAL, "zero stride");
@@ -1266,7 +1272,7 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
     }
     if (timed) LFD_HIP(hipEventRecord(ev[1], st));
     LFD_HIP(lfd::launch_blend_grid(tmp, p->comp_T, p->n_ch, p->d_bj, p->d_bi, p->d_bw, p->n_blend, y, ys_ch,
-                                   ys_t, st));
+                                   ys_t, st, gen));
     if (timed) LFD_HIP(hipEventRecord(ev[2], st));
     p->last_k1 = p->subs[0]->last_k1;
     return LFD_OK;
@@ -1321,6 +1327,7 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
   return LFD_OK;
 }
 
+extern "C" {
 int lfd_lowpass_last_timing(const lfd_lowpass_plan *p, float *ms_blocks, float *ms_scan) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
   if (!p->timed) return fail(LFD_EINVAL, "timing was not enabled for the last execute");

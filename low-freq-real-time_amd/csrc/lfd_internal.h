@@ -7,6 +7,8 @@
 #include <cstdlib>
 #include <string>
 
+struct lfd_lowpass_plan;  // include/lfdas.h
+
 namespace lfd {
 
 // Sets the calling thread's lfd_last_error() message; returns `code`.
@@ -292,8 +294,19 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
                                int64_t ys_t, hipStream_t st, int *kernel_used);
 // Lattice (composite) plans: y[ch, bj[i]] = (1 - bw[i]) tmp[ch, bi[2i]] +
 // bw[i] tmp[ch, bi[2i+1]] (bi[2i+1] < 0: tmp[ch, bi[2i]]), tmp rows of T.
+// GridGen (dts > 0): the weights of a regular time grid computed on device
+// from integer ns (point j at rel0 + j*step ns after the input's sample 0,
+// sampled every dts ns) instead of bw.
+struct GridGen {
+  int64_t rel0 = 0, step = 0, dts = 0;
+};
 hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
-                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st);
+                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+                             const GridGen &gen = GridGen{});
+// lfd_lowpass_execute with a generated grid (a lattice plan's weights from
+// `gen`; the stream caches lattice plans by structure).  Other plans ignore it.
+int lowpass_execute_gen(const ::lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
+                        int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const GridGen &gen);
 // dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.
 hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
                             int64_t dp, hipStream_t st);

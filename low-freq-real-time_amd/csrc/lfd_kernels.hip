@@ -4416,10 +4416,15 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
 // Lattice-plan blend (lfd_capi.cpp plan_create_composite): linear interp1d
 // between the two lattice phases' outputs y[lo] and y[lo + 1] of every grid
 // point; one thread per (channel, point), points fastest.
+// gen.dts > 0: the weights come from the grid's own integer time arithmetic
+// instead of bw: point j sits rel = gen.rel0 + j gen.step ns after sample 0,
+// w = (rel - floor(rel / dts) dts) / dts — the host's formula (lfd_stream.cpp
+// run_chunks), so a stream's lattice plan serves every push whose grid has
+// the same lattice structure, whatever its fractions.
 __global__ __launch_bounds__(256) void k_blend_grid(const float *__restrict__ tmp, int64_t T, int64_t n_ch,
                                                     const int64_t *__restrict__ bj, const int64_t *__restrict__ bi,
                                                     const double *__restrict__ bw, int64_t nb, float *__restrict__ y,
-                                                    int64_t ys_ch, int64_t ys_t) {
+                                                    int64_t ys_ch, int64_t ys_t, GridGen gen) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nb * n_ch) return;
   const int64_t ch = idx / nb, i = idx - ch * nb;
@@ -4427,16 +4432,25 @@ __global__ __launch_bounds__(256) void k_blend_grid(const float *__restrict__ tm
   const int64_t ia = bi[2 * i], ib = bi[2 * i + 1];
   double v = (double)row[ia];
   if (ib >= 0) {
-    const double wv = bw[i];
+    double wv;
+    if (gen.dts > 0) {
+      const int64_t rel = gen.rel0 + bj[i] * gen.step;
+      int64_t lo = rel / gen.dts;
+      if (rel % gen.dts != 0 && rel < 0) --lo;
+      wv = (double)(rel - lo * gen.dts) / (double)gen.dts;
+    } else {
+      wv = bw[i];
+    }
     v = fma(wv, (double)row[ib] - v, v);
   }
   y[ch * ys_ch + bj[i] * ys_t] = (float)v;
 }
 
 hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
-                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+                             const GridGen &gen) {
   if (nb <= 0 || n_ch <= 0) return hipSuccess;
-  k_blend_grid<<<nblk(nb * n_ch, 256), 256, 0, st>>>(tmp, T, n_ch, bj, bi, bw, nb, y, ys_ch, ys_t);
+  k_blend_grid<<<nblk(nb * n_ch, 256), 256, 0, st>>>(tmp, T, n_ch, bj, bi, bw, nb, y, ys_ch, ys_t, gen);
   return hipGetLastError();
 }
 

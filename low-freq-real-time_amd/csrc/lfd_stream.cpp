@@ -129,6 +129,7 @@ struct lfd_stream {
   lfd_stream_output last{};
   std::vector<int64_t> last_counts;
   std::map<std::vector<int64_t>, lfd_lowpass_plan *> plans;
+  int64_t plans_created = 0, plan_hits = 0;  // lfd_debug_stream_plans
   void *ws = nullptr;
   size_t ws_bytes = 0;
   int64_t n_runs = 0;
@@ -345,22 +346,27 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
   float *y = s->out[oi];
   const float *x = s->arena[s->cur] + x0;
   lfd_lowpass_plan *plan = nullptr;
+  // grid weights from the grid's integer times on device (lattice plans):
+  // the same formula as w[] above, relative to the run's first output
+  const lfd::GridGen gen{t_grid0 + j0 * s->out_ns - s->t_col0, s->out_ns, dts};
   if (n_out >= 2) {
-    // uniform grids: keyed by (first point, spacing, fraction); other grids
-    // (varying fraction or spacing) become lattice plans keyed by every point
+    // uniform grids: keyed by (first point, spacing, fraction): the fraction
+    // is part of the block plan's output functional.  Other grids (varying
+    // fraction or spacing: lattice plans) are keyed by their STRUCTURE only —
+    // every point's sample lo relative to the row start and whether it
+    // blends (w != 0) — and take the fractions from `gen` at execute time, so
+    // a steady 3 kHz stream reuses its few lattice plans instead of building
+    // one per push
     int64_t wbits = 0;
     std::memcpy(&wbits, &w[0], sizeof(wbits));
-    std::vector<int64_t> key = {nt, aligned ? 1 : 0, lo[0] - x0, lo[1] - lo[0], n_out, wbits};
+    std::vector<int64_t> key = {nt, aligned ? 1 : 0, lo[0] - x0, lo[1] - lo[0], n_out, aligned ? wbits : 0};
     if (!aligned)
-      for (int64_t j = 0; j < n_out; ++j) {
-        int64_t wb = 0;
-        std::memcpy(&wb, &w[j], sizeof(wb));
-        key.insert(key.end(), {lo[j] - x0, wb});
-      }
+      for (int64_t j = 0; j < n_out; ++j) key.insert(key.end(), {lo[j] - x0, w[j] != 0.0 ? 1 : 0});
     for (auto &c : cs) key.insert(key.end(), {c[0] - x0, c[1] - x0, c[2] - j0, c[3] - j0});
     auto it = s->plans.find(key);
     if (it != s->plans.end()) {
       plan = it->second;
+      s->plan_hits++;
     } else {
       if (s->plans.size() >= PLAN_CACHE_MAX) {
         LFD_HIP(hipStreamSynchronize(s->s_comp));  // in-flight runs use plan constants
@@ -376,6 +382,7 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
       if (rc != LFD_OK && rc != LFD_EUNSUPPORTED) return rc;
       if (rc != LFD_OK) plan = nullptr;
       s->plans[key] = plan;
+      s->plans_created++;
     }
   }
   if (s->timed) LFD_HIP(hipEventRecord(s->tm[2], s->s_comp));
@@ -383,7 +390,8 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
     size_t need = 0;
     LFD_TRY(lfd_lowpass_plan_info(plan, &need, nullptr, nullptr));
     LFD_TRY(ensure_dev(&s->ws, &s->ws_bytes, std::max<size_t>(need, 256), s->s_comp));
-    LFD_TRY(lfd_lowpass_execute(plan, x, s->cap, 1, y, n_out, 1, s->ws, s->s_comp));
+    LFD_TRY(lfd::lowpass_execute_gen(plan, x, s->cap, 1, y, n_out, 1, s->ws, s->s_comp,
+                                     aligned ? lfd::GridGen{} : gen));
   } else {
     // single-point output, or a grid no block plan takes (more than 32
     // lattice phases): per-chunk general path (still on device)
@@ -662,6 +670,13 @@ int lfd_stream_info(const lfd_stream *s, int64_t *capacity, int64_t *held, int64
   if (capacity) *capacity = s->cap;
   if (held) *held = s->a_hi - s->a_lo;
   if (t_first_held_ns) *t_first_held_ns = s->t_col0 + s->a_lo * s->cfg.sample_ns;
+  return LFD_OK;
+}
+
+int lfd_debug_stream_plans(const lfd_stream *s, int64_t *created, int64_t *hits) {
+  if (!s) return fail(LFD_EINVAL, "stream is NULL");
+  if (created) *created = s->plans_created;
+  if (hits) *hits = s->plan_hits;
   return LFD_OK;
 }
 

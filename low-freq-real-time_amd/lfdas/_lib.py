@@ -159,6 +159,7 @@ def load():
         "lfd_stream_last_timing": ([vp, P(ctypes.c_float), P(ctypes.c_float)], i32),
         "lfd_stream_info": ([vp, P(i64), P(i64), P(i64)], i32),
         "lfd_stream_close": ([vp], None),
+        "lfd_debug_stream_plans": ([vp, P(i64), P(i64)], i32),
         "lfd_host_alloc": ([P(vp), sz], i32),
         "lfd_host_free": ([vp], None),
         "lfd_host_register": ([vp, sz], i32),
@@ -183,6 +184,7 @@ EXPORTED = (
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
+    "lfd_debug_stream_plans",
     "lfd_host_alloc", "lfd_host_free", "lfd_host_register", "lfd_host_unregister", "lfd_demean_scale_f64", "lfd_median_filter_f64",
 )
 

@@ -241,6 +241,12 @@ class LowpassStream:
         check(self._lib.lfd_stream_info(self._h, ctypes.byref(c), ctypes.byref(h), ctypes.byref(t)))
         return int(c.value), int(h.value), int(t.value)
 
+    def plan_stats(self):
+        """(plans built, plan-cache hits) of this stream (``lfd_debug_stream_plans``)."""
+        c, h = ctypes.c_int64(), ctypes.c_int64()
+        check(self._lib.lfd_debug_stream_plans(self._h, ctypes.byref(c), ctypes.byref(h)))
+        return int(c.value), int(h.value)
+
     def close(self):
         if getattr(self, "_h", None):
             self._lib.lfd_stream_close(self._h)
