@@ -6,6 +6,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("LFDAS_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "low-freq-real-time_amd", "lfdas", "liblfdas_diag.so"))  # A/B knobs: diagnostic build only
 sys.path.insert(0, os.path.join(ROOT, "low-freq-real-time_amd"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
