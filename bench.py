@@ -665,7 +665,8 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
     return {"value": n_ch * n / (ms * 1e-3), "unit": "channel-samples/s", "ms": ms,
             "config": f"{n_ch:,} ch x {n:,} @ {fs:g} Hz fp32 -> f64, Butterworth band-pass {band} Hz "
                       f"(corners=4, {sos.shape[0]} sections), zero-phase, full rate",
-            "kernels_ms": {"k_fullrate_wave<4,false> (functionals)": kt[0], "k_fullrate_scan<4>": kt[1],
+            "kernels_ms": {"k_block_functionals_mfma (medium-block functionals, fp64 MFMA)": kt[0],
+                           "k_fullrate_scan_seg<4> (segmented scan)": kt[1],
                            "k_fullrate_wave<4,true> (output)": kt[2]},
             "roofline": {"bound": "hbm", "kernel": "k_fullrate_wave<4,true>", "achieved": gbs_out,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs_out / HBM_PEAK_GBS,

@@ -69,6 +69,7 @@ int lfd_device_count(int *count);
 #define LFD_OPT_NO_LATTICE 6      /* drifting grids: LFD_EUNSUPPORTED (per-chunk path)    */
 #define LFD_OPT_NO_HEAD_SKIP 7    /* off-sample grids: walk chunk heads                   */
 #define LFD_OPT_FIR_VALU 8        /* lfd_fir_decimate_f32: VALU kernel, not matrix cores  */
+#define LFD_OPT_FULLRATE_BIGBLOCK 9 /* lfd_sosfiltfilt_f32: big-block functionals + serial scan */
 int lfd_set_option(int option, int64_t value);
 int lfd_get_option(int option, int64_t *value);
 

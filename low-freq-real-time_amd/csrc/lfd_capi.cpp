@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -41,13 +42,14 @@ std::atomic<int> g_timing{0};
 bool lfd::timing_enabled() { return g_timing.load() != 0; }
 
 namespace {
-constexpr int N_OPT = 9;  // LFD_OPT_* ids are 1 .. N_OPT - 1
+constexpr int N_OPT = 10;  // LFD_OPT_* ids are 1 .. N_OPT - 1
 std::atomic<int64_t> g_opt[N_OPT];
 #ifdef LFD_DIAG
 // the A/B environment names the tools/ recipes of rounds 1-3 use
 const char *const k_opt_env[N_OPT] = {nullptr,          "LFD_NO_RUNS",    "LFD_K1_REC",
                                       "LFD_TM_NO_X2",   "LFD_SCAN_DEFER", "LFD_FULLRATE_SERIAL",
-                                      "LFD_NO_LATTICE", "LFD_NO_HSKIP",   "LFD_FIR_VALU"};
+                                      "LFD_NO_LATTICE", "LFD_NO_HSKIP",   "LFD_FIR_VALU",
+                                      "LFD_FULLRATE_BIGBLOCK"};
 #endif
 }  // namespace
 
@@ -348,6 +350,9 @@ void fullrate_constants(const Cascade &cs, lfd::FRConst &fc) {
     R t[MAX_N] = {0};
     for (int i = lfd::FR_L - 1; i >= 0; --i) (void)tdf2_step(cs, t, yv[i]);
     for (int r = 0; r < n; ++r) fc.M[r * MAX_N + c] = (double)t[r];
+    R tb[MAX_N] = {0};
+    for (int i = lfd::FR_LB - 1; i >= 0; --i) (void)tdf2_step(cs, tb, yv[i]);
+    for (int r = 0; r < n; ++r) fc.MB[r * MAX_N + c] = (double)tb[r];
     R u[MAX_N] = {0};
     for (int i = lfd::FR_LS - 1; i >= 0; --i) fc.Rh[i][c] = (double)tdf2_step(cs, u, yv[i]);
     for (int r = 0; r < n; ++r) fc.M32[r * MAX_N + c] = (double)u[r];
@@ -373,6 +378,69 @@ void fullrate_constants(const Cascade &cs, lfd::FRConst &fc) {
         const int i = 16 * mt + (l & 15), kk = 4 * ks + (l >> 4);
         fc.QA[mt][ks][l] = kk < n ? fc.Rh[i][kk] : (kk < 2 * n ? fc.H[lfd::FR_LS - 1 - i][kk - n] : 0.0);
       }
+}
+
+// Taps of the medium-block functionals (lfd_internal.h FR_LB), packed as the
+// MFMA kernel's tap table (TapGeom{FR_LB, 0, 2N, 1, 0}):  for a unit sample at
+// p, A = the forward exit state after the block = st[LB-1-p] (st[i]: state
+// after i + 1 steps of the impulse response h), Z = the zero-state reverse
+// exit over the forward output h[i - p] = sum_{i >= p} st[i] h[i - p] (the
+// reverse pass runs the same cascade).
+std::vector<double> fullrate_medium_taps(const Cascade &cs) {
+  const int n = 2 * cs.ns, LB = lfd::FR_LB;
+  std::vector<R> h(LB);
+  std::vector<std::array<R, MAX_N>> st(LB);
+  {
+    R z[MAX_N] = {0};
+    for (int i = 0; i < LB; ++i) {
+      h[i] = tdf2_step(cs, z, i == 0 ? 1.0L : 0.0L);
+      for (int c = 0; c < MAX_N; ++c) st[i][c] = z[c];
+    }
+  }
+  std::vector<R> K((size_t)2 * n * LB, 0.0L);  // K[c][p]
+  for (int p = 0; p < LB; ++p)
+    for (int c = 0; c < n; ++c) {
+      K[(size_t)c * LB + p] = st[LB - 1 - p][c];
+      R acc = 0;
+      for (int i = p; i < LB; ++i) acc += st[i][c] * h[i - p];
+      K[(size_t)(n + c) * LB + p] = acc;
+    }
+  const int nc = 2 * n;
+  std::vector<double> dev((size_t)LB * nc, 0.0);
+  for (int t = 0; t < LB / 16; ++t)
+    for (int q = 0; q < 4; ++q)
+      for (int c = 0; c < nc; ++c)
+        for (int el = 0; el < 4; ++el)
+          dev[((size_t)(t * 4 + q) * nc + c) * 4 + el] = (double)K[(size_t)c * LB + 16 * t + 4 * q + el];
+  return dev;
+}
+
+// Segment plan of k_fullrate_scan_seg for M medium blocks: G segments of
+// seglen blocks (Gu non-empty), PhiB^seglen and PhiB^lastlen in extended
+// precision.
+lfd::FRSeg fullrate_segments(const Cascade &cs, int64_t M) {
+  lfd::FRSeg sg{};
+  const int n = 2 * cs.ns;
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(64, M / 4));
+  sg.seglen = (int)((M + G - 1) / G);
+  sg.Gu = (int)((M + sg.seglen - 1) / sg.seglen);
+  sg.G = (int)G;
+  sg.lastlen = (int)(M - (int64_t)(sg.Gu - 1) * sg.seglen);
+  Mat P1(n);
+  for (int c = 0; c < n; ++c) {
+    R z[MAX_N] = {0};
+    z[c] = 1;
+    (void)tdf2_step(cs, z, 0);
+    for (int r = 0; r < n; ++r) P1.a[r][c] = z[r];
+  }
+  const Mat PB = mpow(P1, lfd::FR_LB);
+  const Mat ps = mpow(PB, sg.seglen), pl = mpow(PB, sg.lastlen);
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) {
+      sg.pseg[r * MAX_N + c] = (double)ps.a[r][c];
+      sg.plast[r * MAX_N + c] = (double)pl.a[r][c];
+    }
+  return sg;
 }
 
 // Fill the block-functional and scan constants for block length L and output
@@ -1447,12 +1515,25 @@ int64_t fullrate_blocks(int64_t n_t) {  // the tail keeps >= 1 sample
 
 struct FrLayout {
   size_t off_F, off_SF, off_ST, off_TP, bytes;
+  size_t off_SFm = 0;  // (medium-block path) S_f at every medium block
 };
 FrLayout fullrate_layout(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64_t nb) {
   const size_t n = 2 * n_sec;
   FrLayout l{};
   l.off_F = 0;
   l.off_SF = align256(sizeof(double) * 2 * n * nb * n_ch);
+  l.off_ST = l.off_SF + align256(sizeof(double) * n * (nb + 1) * n_ch);
+  l.off_TP = l.off_ST + align256(sizeof(double) * n * (nb + 1) * n_ch);
+  l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - nb * lfd::FR_L + padlen) * n_ch);
+  return l;
+}
+// Medium-block path: F2 [ch/16][4 nb][2N][16], SFm [4 nb][N][ch], SF, ST, TP.
+FrLayout fullrate_layout_mb(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64_t nb) {
+  const size_t n = 2 * n_sec, ch16 = (size_t)((n_ch + 15) / 16) * 16, M = 4 * (size_t)nb;
+  FrLayout l{};
+  l.off_F = 0;
+  l.off_SFm = align256(sizeof(double) * 2 * n * M * ch16);
+  l.off_SF = l.off_SFm + align256(sizeof(double) * n * M * n_ch);
   l.off_ST = l.off_SF + align256(sizeof(double) * n * (nb + 1) * n_ch);
   l.off_TP = l.off_ST + align256(sizeof(double) * n * (nb + 1) * n_ch);
   l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - nb * lfd::FR_L + padlen) * n_ch);
@@ -1468,8 +1549,10 @@ struct FrEntry {
   int dev = -1, n_sec = 0;
   double sos[6 * MAX_SEC] = {0};
   lfd::FRConst *d_fc = nullptr;
+  double *d_ktaps = nullptr;  // medium-block functional taps (fullrate_medium_taps)
   ~FrEntry() {
     if (d_fc) (void)hipFree(d_fc);
+    if (d_ktaps) (void)hipFree(d_ktaps);
   }
 };
 std::mutex g_fr_mu;
@@ -1495,8 +1578,12 @@ int fullrate_entry(const double *sos, int n_sec, const Cascade &c, std::shared_p
   auto fc = std::make_unique<lfd::FRConst>();
   fullrate_constants(c, *fc);
   LFD_HIP(hipMalloc(&e->d_fc, sizeof(lfd::FRConst)));
-  const hipError_t he = hipMemcpy(e->d_fc, fc.get(), sizeof(lfd::FRConst), hipMemcpyHostToDevice);
+  hipError_t he = hipMemcpy(e->d_fc, fc.get(), sizeof(lfd::FRConst), hipMemcpyHostToDevice);
   if (he != hipSuccess) return fail(LFD_EHIP, std::string("full-rate constants: ") + hipGetErrorString(he));
+  const std::vector<double> kt = fullrate_medium_taps(c);
+  LFD_HIP(hipMalloc(&e->d_ktaps, sizeof(double) * kt.size()));
+  he = hipMemcpy(e->d_ktaps, kt.data(), sizeof(double) * kt.size(), hipMemcpyHostToDevice);
+  if (he != hipSuccess) return fail(LFD_EHIP, std::string("full-rate taps: ") + hipGetErrorString(he));
   // bounded: drop the oldest from the cache (freed when its last user returns)
   if (g_fr.size() >= 16) g_fr.erase(g_fr.begin());
   g_fr.push_back(e);
@@ -1512,7 +1599,9 @@ size_t lfd_sosfiltfilt_workspace_bytes(int64_t n_ch, int64_t n_t, int padlen, in
   size_t b = align256(sizeof(double) * (size_t)(n_t + 2 * (int64_t)padlen) * (size_t)n_ch);
   if (n_sec >= 1 && n_sec <= MAX_SEC && n_ch >= 1) {
     const int64_t nb = fullrate_blocks(n_t);
-    if (nb > 0) b = std::max(b, fullrate_layout(n_ch, n_t, padlen, n_sec, nb).bytes);
+    if (nb > 0)
+      b = std::max({b, fullrate_layout(n_ch, n_t, padlen, n_sec, nb).bytes,
+                    fullrate_layout_mb(n_ch, n_t, padlen, n_sec, nb).bytes});
   }
   return b;
 }
@@ -1545,7 +1634,12 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
   if (nb > 0 && !lfd::option(LFD_OPT_FULLRATE_SERIAL)) {
     std::shared_ptr<const FrEntry> fe;
     if (int e = fullrate_entry(sos, n_sec, c, &fe)) return e;
-    const FrLayout lo = fullrate_layout(n_ch, n_t, padlen, n_sec, nb);
+    // medium-block path (time-contiguous, 16-B aligned rows): the functionals
+    // on the fp64 matrix cores and the segmented scan
+    const bool mb = s_t == 1 && (s_ch % 4 == 0 || n_ch == 1) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                    !lfd::option(LFD_OPT_FULLRATE_BIGBLOCK);
+    const FrLayout lo = mb ? fullrate_layout_mb(n_ch, n_t, padlen, n_sec, nb)
+                           : fullrate_layout(n_ch, n_t, padlen, n_sec, nb);
     char *ws = static_cast<char *>(workspace);
     double *F = reinterpret_cast<double *>(ws + lo.off_F);
     double *SF = reinterpret_cast<double *>(ws + lo.off_SF);
@@ -1568,11 +1662,23 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
       g_fr_timed = false;
     }
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[0], st));
-    LFD_HIP(lfd::launch_fullrate_blocks(n_sec, false, x, s_ch, s_t, n_ch, nb, fe->d_fc, nullptr, nullptr, F,
-                                        nullptr, 0, 0, st));
-    if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
-    LFD_HIP(lfd::launch_fullrate_scan(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F, SF, ST, TP, y,
-                                      ys_ch, ys_t, st));
+    if (mb) {
+      const int n = 2 * n_sec;
+      const lfd::BlockGeom g{n_ch, 4 * nb, 0, lfd::FR_LB, 2 * n, 0};
+      const lfd::TapGeom tg{lfd::FR_LB, 0, 2 * n, 1, 0};
+      LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, n_t, g, fe->d_ktaps, tg, F, st));
+      if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
+      const lfd::FRSeg sg = fullrate_segments(c, 4 * nb);
+      LFD_HIP(lfd::launch_fullrate_scan_seg(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F,
+                                            reinterpret_cast<double *>(ws + lo.off_SFm), SF, ST, TP, y, ys_ch, ys_t,
+                                            sg, st));
+    } else {
+      LFD_HIP(lfd::launch_fullrate_blocks(n_sec, false, x, s_ch, s_t, n_ch, nb, fe->d_fc, nullptr, nullptr, F,
+                                          nullptr, 0, 0, st));
+      if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
+      LFD_HIP(lfd::launch_fullrate_scan(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F, SF, ST, TP, y,
+                                        ys_ch, ys_t, st));
+    }
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[2], st));
     LFD_HIP(lfd::launch_fullrate_blocks(n_sec, true, x, s_ch, s_t, n_ch, nb, fe->d_fc, SF, ST, nullptr, y,
                                         ys_ch, ys_t, st));

@@ -203,12 +203,19 @@ struct RunGeom {
 // k * FR_L).
 constexpr int FR_LS = 32;
 constexpr int FR_L = 64 * FR_LS;
+// Medium blocks of the matrix-core functionals pass (time-contiguous rows):
+// FR_LB samples, 4 per big block; their functionals (forward exit A and
+// zero-state reverse exit Z, 2N values) are a fp64-MFMA product with a
+// 2N x FR_LB tap table (k_block_functionals_mfma), and the segmented scan
+// (k_fullrate_scan_seg) walks them.
+constexpr int FR_LB = 16 * FR_LS;
 struct FRConst {
   SosCoef cf;
   ZiVec zi;                       // sosfilt_zi (unit step steady state)
   double PhiP[6][MAX_N * MAX_N];  // row-major, stride MAX_N
   double PhiL[MAX_N * MAX_N];     // over FR_L samples
   double M[MAX_N * MAX_N];        // reverse exit state over a big block per forward state entering it
+  double MB[MAX_N * MAX_N];       // the same over a medium block (FR_LB samples; PhiP[4] is its transition)
   double M32[MAX_N * MAX_N];      // the same over one sub-block
   double H[FR_LS][MAX_N];         // zero-input output i steps after unit state e_n
   double Rh[FR_LS][MAX_N];        // zero-state reverse output at i of H's forward output
@@ -231,6 +238,21 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
                                   int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
                                   const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
                                   hipStream_t st);
+// Segmented scan over the medium blocks (FR_LB) of the matrix-core
+// functionals F2 (f_index layout, nF = 2N over 4 nb blocks): a workgroup =
+// 16 channels x G segments of `seglen` medium blocks; per segment a zero-state
+// aggregate, a combine across the segments (powers pseg = PhiB^seglen, plast
+// = PhiB^lastlen), the true states; forward then reverse.  Writes SF / ST at
+// the big-block starts (the output pass's inputs), SFm (all medium blocks),
+// TP and the tail outputs, like k_fullrate_scan.
+struct FRSeg {
+  double pseg[MAX_N * MAX_N], plast[MAX_N * MAX_N];
+  int seglen, lastlen, G, Gu;
+};
+hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
+                                    int64_t nb, int padlen, const FRConst *fc, const double *F2, double *SFm,
+                                    double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
+                                    const FRSeg &sg, hipStream_t st);
 // Per-channel walk over the big blocks + both edges (odd extension, zi) and
 // the outputs of the tail [nb * FR_L, n_t).  TP: (n_t - nb * FR_L + padlen) x n_ch.
 hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch,

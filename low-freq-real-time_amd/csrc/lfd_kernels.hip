@@ -1347,6 +1347,203 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
 }
 
 // ---------------------------------------------------------------------------
+// k_fullrate_scan_seg: the scan over MEDIUM blocks (FR_LB samples, 4 per big
+// block) whose functionals the matrix-core pass wrote (F2, f_index layout:
+// 16 channels contiguous per (block, component); components 0..N-1 = A, the
+// forward exit from zero state, N..2N-1 = Z, the zero-state reverse exit of
+// the zero-state forward output).  One workgroup = 16 channels x G segments
+// of seglen medium blocks (lane = channel, 4 segments per wave):
+//   A  each segment's forward aggregate from zero state
+//   -> entering states E_s = pseg E_{s-1} + agg_{s-1}, E_0 = SciPy's left edge
+//   C  the true S_f at every medium block (SFm; SF at the big-block starts);
+//      the last segment continues over the tail and right pad and returns
+//      from zi * y_f[-1] (T_end, the tail's outputs)
+//   A' each segment's reverse aggregate from zero T: T <- PhiB T + Z + MB S_f
+//   -> entering T from the right, C' the true T (ST at the big-block starts).
+// 16 x G threads per channel group instead of one thread per channel walking
+// every block: the walks are G times shorter (latency-bound chains).
+template <int NS>
+__global__ __launch_bounds__(1024) void k_fullrate_scan_seg(
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t nb, int padlen,
+    const FRConst *__restrict__ fc, const double *__restrict__ F2, double *__restrict__ SFm,
+    double *__restrict__ SF, double *__restrict__ ST, double *__restrict__ TP, double *__restrict__ y,
+    int64_t ys_ch, int64_t ys_t, FRSeg sg) {
+  constexpr int N = 2 * NS;
+  __shared__ double cPB[N * N], cMB[N * N], cPS[N * N], cPT[N * N];
+  __shared__ double slotL[16][N], slotR[16][N];
+  extern __shared__ double agg[];  // [G][16][N]
+  const int tid = threadIdx.x, col = tid & 15, seg = tid >> 4;
+  for (int i = tid; i < N * N; i += blockDim.x) {
+    const int r = i / N, c = i % N;
+    cPB[i] = fc->PhiP[4][r * MAX_N + c];
+    cMB[i] = fc->MB[r * MAX_N + c];
+    cPS[i] = sg.pseg[r * MAX_N + c];
+    cPT[i] = sg.plast[r * MAX_N + c];
+  }
+  __syncthreads();
+  const int64_t ch = (int64_t)blockIdx.x * 16 + col;
+  const bool active = ch < n_ch;
+  const int64_t M = 4 * nb;
+  const int64_t m0 = (int64_t)seg * sg.seglen;
+  const int64_t m1 = m0 + sg.seglen < M ? m0 + sg.seglen : M;
+  const bool live = active && seg < sg.Gu;
+  const int64_t chc = active ? ch : n_ch - 1;
+  const double *Fc = F2 + ((chc >> 4) * M * 2 * N) * 16 + (chc & 15);  // + (m * 2N + c) * 16
+  FwdRec<NS> fr;
+  fr.load(fc->cf);
+  auto mv = [&](const double *P, const double (&v)[N], double (&o)[N], bool tri) {
+    asm volatile("" ::: "memory");  // matrices re-read from LDS, not held in registers
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double acc = o[r];
+#pragma unroll
+      for (int c = 0; c < N; ++c)
+        if (!tri || c / 2 <= r / 2) acc = fma(P[r * N + c], v[c], acc);
+      o[r] = acc;
+    }
+  };
+  double *ag = agg + ((size_t)seg * 16 + col) * N;
+  // ---- A: forward aggregate of the segment from zero state
+  double a[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) a[n] = 0.0;
+  if (live) {
+    for (int64_t m = m0; m < m1; ++m) {
+      double f[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) f[n] = Fc[(m * 2 * N + n) * 16];
+      mv(cPB, a, f, true);
+#pragma unroll
+      for (int n = 0; n < N; ++n) a[n] = f[n];
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) ag[n] = a[n];
+  const float *xc = x + chc * s_ch;
+  const int E = padlen;
+  const float x0 = xc[0], xn = xc[(n_t - 1) * s_t];
+  if (active && seg == 0) {  // SciPy's left edge: zi * ext[0], then the odd extension
+    double z[N];
+    const double e0 = (double)(2.0f * x0 - xc[E * s_t]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * e0;
+    for (int t = 0; t < E; ++t) (void)fr.step(z, (double)(2.0f * x0 - xc[(E - t) * s_t]));
+#pragma unroll
+    for (int n = 0; n < N; ++n) slotL[col][n] = z[n];
+  }
+  __syncthreads();
+  // ---- entering state of the segment
+  double z[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) z[n] = slotL[col][n];
+  for (int sp = 0; sp < seg && sp < sg.Gu; ++sp) {
+    double o[N];
+    const double *as = agg + ((size_t)sp * 16 + col) * N;
+#pragma unroll
+    for (int n = 0; n < N; ++n) o[n] = as[n];
+    mv(cPS, z, o, true);
+#pragma unroll
+    for (int n = 0; n < N; ++n) z[n] = o[n];
+  }
+  // ---- C: true forward states
+  if (live) {
+    for (int64_t m = m0; m < m1; ++m) {
+      double f[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        f[n] = Fc[(m * 2 * N + n) * 16];
+        SFm[(m * N + n) * n_ch + ch] = z[n];
+      }
+      if ((m & 3) == 0) {
+#pragma unroll
+        for (int n = 0; n < N; ++n) SF[((m >> 2) * N + n) * n_ch + ch] = z[n];
+      }
+      mv(cPB, z, f, true);
+#pragma unroll
+      for (int n = 0; n < N; ++n) z[n] = f[n];
+    }
+    if (seg == sg.Gu - 1) {
+      // tail samples [nb FR_L, n_t) and the right pad forward (TP), then the
+      // reverse from zi * y_f[-1] over pad + tail (the tail's outputs)
+      const int64_t t_tail = nb * FR_L, nt = n_t - t_tail;
+      double *tp = TP + ch;
+      const float *xt = xc + t_tail * s_t;
+      double yl = 0.0;
+      for (int64_t i = 0; i < nt; ++i) {
+        yl = fr.step(z, (double)xt[i * s_t]);
+        tp[i * n_ch] = yl;
+      }
+      for (int64_t i = 0; i < E; ++i) {
+        yl = fr.step(z, (double)(2.0f * xn - xc[(n_t - 2 - i) * s_t]));
+        tp[(nt + i) * n_ch] = yl;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * yl;
+      for (int64_t i = nt + E - 1; i >= nt; --i) (void)fr.step(z, tp[i * n_ch]);
+      double *yt = y + ch * ys_ch + t_tail * ys_t;
+      for (int64_t i = nt - 1; i >= 0; --i) yt[i * ys_t] = fr.step(z, tp[i * n_ch]);
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        slotR[col][n] = z[n];
+        ST[(nb * N + n) * n_ch + ch] = z[n];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- A': reverse aggregate of the segment from zero T (true S_f coupling)
+#pragma unroll
+  for (int n = 0; n < N; ++n) a[n] = 0.0;
+  if (live) {
+    for (int64_t m = m1 - 1; m >= m0; --m) {
+      double f[N], sf[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        f[n] = Fc[(m * 2 * N + N + n) * 16];
+        sf[n] = SFm[(m * N + n) * n_ch + ch];
+      }
+      mv(cPB, a, f, true);
+      mv(cMB, sf, f, false);
+#pragma unroll
+      for (int n = 0; n < N; ++n) a[n] = f[n];
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) ag[n] = a[n];
+  __syncthreads();
+  // ---- T entering the segment from its right end
+#pragma unroll
+  for (int n = 0; n < N; ++n) z[n] = slotR[col][n];
+  for (int sp = sg.Gu - 1; sp > seg; --sp) {
+    double o[N];
+    const double *as = agg + ((size_t)sp * 16 + col) * N;
+#pragma unroll
+    for (int n = 0; n < N; ++n) o[n] = as[n];
+    mv(sp == sg.Gu - 1 ? cPT : cPS, z, o, true);
+#pragma unroll
+    for (int n = 0; n < N; ++n) z[n] = o[n];
+  }
+  // ---- C': true reverse states
+  if (live) {
+    for (int64_t m = m1 - 1; m >= m0; --m) {
+      double f[N], sf[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        f[n] = Fc[(m * 2 * N + N + n) * 16];
+        sf[n] = SFm[(m * N + n) * n_ch + ch];
+      }
+      mv(cPB, z, f, true);
+      mv(cMB, sf, f, false);
+#pragma unroll
+      for (int n = 0; n < N; ++n) z[n] = f[n];
+      if ((m & 3) == 0) {
+#pragma unroll
+        for (int n = 0; n < N; ++n) ST[((m >> 2) * N + n) * n_ch + ch] = z[n];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Full-rate sosfiltfilt: one thread per channel; forward outputs staged in a
 // float64 workspace laid out [t][ch] (coalesced across channels).
 // ---------------------------------------------------------------------------
@@ -3867,6 +4064,38 @@ hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t
     default: return hipErrorInvalidValue;
   }
 #undef LFD_FRS
+  return hipGetLastError();
+}
+
+hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
+                                    int64_t nb, int padlen, const FRConst *fc, const double *F2, double *SFm,
+                                    double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
+                                    const FRSeg &sg, hipStream_t st) {
+  if (sg.G < 1 || sg.G > 64 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 || nb < 1) return hipErrorInvalidValue;
+  const unsigned g = nblk(n_ch, 16);
+  const size_t lds = sizeof(double) * (size_t)sg.G * 16 * 2 * n_sec;
+  static bool attr = false;  // (dynamic LDS above 64 KB with the static part)
+  if (!attr) {
+    for (const void *fn : {reinterpret_cast<const void *>(&k_fullrate_scan_seg<1>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<2>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<3>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<4>)}) {
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+      if (e != hipSuccess) return e;
+    }
+    attr = true;
+  }
+#define LFD_FRSS(NS) \
+  k_fullrate_scan_seg<NS><<<g, 16 * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, nb, padlen, fc, F2, SFm, SF, ST, TP, y, \
+                                                    ys_ch, ys_t, sg)
+  switch (n_sec) {
+    case 1: LFD_FRSS(1); break;
+    case 2: LFD_FRSS(2); break;
+    case 3: LFD_FRSS(3); break;
+    case 4: LFD_FRSS(4); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LFD_FRSS
   return hipGetLastError();
 }
 

@@ -193,7 +193,7 @@ EXPORTED = (
 # library reads no environment variable; tests drive the fallback kernels
 # through these)
 OPTIONS = {"no_runs": 1, "k1_recurrence": 2, "tm_no_pairs": 3, "scan_defer": 4, "fullrate_serial": 5,
-           "no_lattice": 6, "no_head_skip": 7, "fir_valu": 8}
+           "no_lattice": 6, "no_head_skip": 7, "fir_valu": 8, "fullrate_bigblock": 9}
 
 
 @contextlib.contextmanager
