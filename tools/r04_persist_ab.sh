@@ -9,3 +9,7 @@ for ch in 1250 2500 5000 10000; do
   timeout -k 10 300 python tools/ab_plan.py --ch $ch --reps 4 --steps 5 "" "LFD_K1_PERSIST=0" > gpurun_out/${tag}_ab_persist_${ch}.txt 2>&1 || { tail -20 gpurun_out/${tag}_ab_persist_${ch}.txt; exit 1; }
   tail -2 gpurun_out/${tag}_ab_persist_${ch}.txt
 done
+for e in "" "LFD_FULLRATE_BIGBLOCK=1"; do
+  echo "== fullrate $e"; env $e timeout -k 10 120 python tools/fr_bench.py > gpurun_out/${tag}_fr_${e:-default}.txt 2>&1 || { tail -20 gpurun_out/${tag}_fr_${e:-default}.txt; exit 1; }
+  tail -6 gpurun_out/${tag}_fr_${e:-default}.txt
+done
