@@ -742,7 +742,7 @@ struct lfd_lowpass_plan {
   int *d_slot_chunk = nullptr;
   size_t off_Y0 = 0, off_AG = 0, off_SR = 0, off_TR = 0, off_CR = 0;
   int64_t sf_blocks = 0, tp_len = 0;
-  size_t off_F = 0, off_SF = 0, off_TP = 0, off_CTR = 0, ws_bytes = 0;
+  size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   // lfd_set_timing(n > 1): a ring of n event triples, so n timed executes
   // need no host synchronisation between them (lfd_lowpass_timings)
@@ -1074,8 +1074,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     end_F = std::max(end_F, align256(p->off_CR + sizeof(double) * (size_t)n_chunks * ch64));
   }
   p->off_TP = end_F;
-  p->off_CTR = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);  // K1 unit counter
-  p->ws_bytes = p->off_CTR + 256;
+  p->ws_bytes = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);
   // Device state.  Without a visible device the plan stays host-only (its
   // geometry and constants can still be inspected); execute then fails.
   int ndev = 0;
@@ -1365,8 +1364,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     double *AG = reinterpret_cast<double *>(ws + p->off_AG);
     double *SR = reinterpret_cast<double *>(ws + p->off_SR);
     if (mfma_runs) {
-      LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st,
-                                          reinterpret_cast<int *>(ws + p->off_CTR)));
+      LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
     } else if (mfma_tm) {
       LFD_HIP(lfd::launch_block_runs_mfma_tm(x, s_t, p->n_t, p->bg, p->d_taps_tm, p->tg_tm, rg, Y0, AG, st));
     } else {

@@ -263,10 +263,9 @@ hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t
 hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n_t,
                                          const BlockGeom &g, const double *taps,
                                          const TapGeom &tg, double *F, hipStream_t st);
-// ctr: a device int the launch zeroes and its persistent waves count units on.
 hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
-                                  double *Y0, double *AG, hipStream_t st, int *ctr);
+                                  double *Y0, double *AG, hipStream_t st);
 // Run-mode MFMA K1 for (time, channel) storage (s_ch == 1, row stride s_t):
 // tap table with row shift 0 (tg.nvar == 1, tg.v0 == 0).
 hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,

@@ -2613,18 +2613,19 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 // of a 64-bit pointer per lane and iteration (fewer VGPRs under MINW)
 // SEPI: streaming run epilogue (run_block_stream; LDS: taps + RUN_CST_S
 // constants, no run buffers, no backward sweep at run ends)
-// PERSIST: a grid of resident workgroups whose waves pull units from the
-// counter *ctr (zeroed before the launch) until none are left: a wave that
-// finishes early takes the next unit at once (with one unit per wave, a
-// workgroup's slot is freed only when its slowest wave is done, and the
-// last partial round of units ran on a fraction of the chip), and the tap
+// PERSIST: a grid of resident workgroups (as many as fit the chip) whose
+// waves walk units w, w + W, w + 2W ... (W = the grid's waves): a wave that
+// finishes a unit starts its next one at once (with one unit per wave, a
+// workgroup's slot is freed only when its slowest wave is done), and the tap
 // table is loaded once per resident workgroup instead of once per 8 units.
+// The assignment is a pure function of the launch (no counter to reset), so
+// the kernel stays hipGraph-capturable.
 template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
           bool PERSIST = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
-    double *__restrict__ AG, int *__restrict__ ctr) {
+    double *__restrict__ AG) {
   extern __shared__ double Ks[];
   const int tab = tg.Lp * tg.nc;
   const int ntab = tab * tg.nvar;
@@ -2650,12 +2651,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   // hoisted out of the unit loop and held in registers across it
   int lane = lane0;
   asm volatile("" : "+v"(lane));
-  // (PERSIST) the next unit's index, requested now and read at the end of
-  // this one (the atomic returns long before the unit's own loads)
-  int got = 0;
-  if constexpr (PERSIST) {
-    if (lane == 0) got = atomicAdd(ctr, 1);
-  }
   // channel-group-major unit order (time-major measured 2 % slower on cfg3);
   // g_k1_band > 0 (A/B knob LFD_K1_BAND) walks bands of that many channel
   // groups, time groups inside a band, so fewer pages are in flight at once
@@ -2908,7 +2903,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   }
   for (int64_t k = kb; k < k1; ++k) guarded_block(k);
   if constexpr (!PERSIST) break;
-  unit = wave_slots + __builtin_amdgcn_readfirstlane(got);
+  unit += wave_slots;
   }  // units
 }
 
@@ -3597,8 +3592,7 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
 template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
           bool PERSIST = false>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
-                  const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st,
-                  int *ctr = nullptr) {
+                  const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
   // (MODE 4 diagnostic and SEPI: no run buffers)
   const size_t lds = SEPI ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
@@ -3622,17 +3616,15 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern), NT, lds);
     if (e != hipSuccess) return e;
     grid = std::min<unsigned>(grid, (unsigned)std::max(1, n_cu * std::max(1, per_cu)));
-    e = hipMemsetAsync(ctr, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
   }
-  kern<<<grid, NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, ctr);
+  kern<<<grid, NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
   return hipGetLastError();
 }
 
 #ifdef LFD_DIAG
 hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
-                                  double *Y0, double *AG, hipStream_t st, int *ctr) {
+                                  double *Y0, double *AG, hipStream_t st) {
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
   // 512-thread workgroups (2 per CU: 16 waves, 2 x 77 KB LDS at cfg3) retire
@@ -3693,7 +3685,7 @@ hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, 
       // persistent units (LFD_K1_PERSIST=0: one unit per wave, the round-3 kernel)
       const char *pv = knob("LFD_K1_PERSIST");
       if (pv && std::atoi(pv) == 0) return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-      return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st, ctr);
+      return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     }
     return hipErrorInvalidValue;
   }
@@ -3722,17 +3714,17 @@ hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, 
 
 hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
-                                  double *Y0, double *AG, hipStream_t st, int *ctr) {
+                                  double *Y0, double *AG, hipStream_t st) {
 #ifdef LFD_DIAG
-  return launch_block_runs_mfma_ab(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, st, ctr);
+  return launch_block_runs_mfma_ab(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, st);
 #else
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
   // 512-thread workgroups (2 per CU: 16 waves), prefetch depth 1, registers
   // capped for 4 waves per SIMD: 12.77 ms vs 13.09-13.12 for depth 2 at the
   // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt);
-  // persistent waves pulling units from *ctr
-  return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st, ctr);
+  // persistent waves (units w, w + W, ...)
+  return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 #endif
 }
 
