@@ -421,7 +421,7 @@ std::vector<double> fullrate_medium_taps(const Cascade &cs) {
 lfd::FRSeg fullrate_segments(const Cascade &cs, int64_t M) {
   lfd::FRSeg sg{};
   const int n = 2 * cs.ns;
-  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(64, M / 4));
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(32, M / 4));
   sg.seglen = (int)((M + G - 1) / G);
   sg.Gu = (int)((M + sg.seglen - 1) / sg.seglen);
   sg.G = (int)G;
@@ -1525,15 +1525,16 @@ FrLayout fullrate_layout(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64
   l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - nb * lfd::FR_L + padlen) * n_ch);
   return l;
 }
-// Medium-block path: F2 [ch/16][4 nb][2N][16], SFm [4 nb][N][ch], SF, ST, TP.
+// Medium-block path: F2 [ch/16][M][2N][16], SF = SFm [M][N][ch], ST = STm
+// [M + 1][N][ch] (M = 4 nb medium blocks), TP.
 FrLayout fullrate_layout_mb(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64_t nb) {
   const size_t n = 2 * n_sec, ch16 = (size_t)((n_ch + 15) / 16) * 16, M = 4 * (size_t)nb;
   FrLayout l{};
   l.off_F = 0;
-  l.off_SFm = align256(sizeof(double) * 2 * n * M * ch16);
-  l.off_SF = l.off_SFm + align256(sizeof(double) * n * M * n_ch);
-  l.off_ST = l.off_SF + align256(sizeof(double) * n * (nb + 1) * n_ch);
-  l.off_TP = l.off_ST + align256(sizeof(double) * n * (nb + 1) * n_ch);
+  l.off_SF = align256(sizeof(double) * 2 * n * M * ch16);
+  l.off_SFm = l.off_SF;
+  l.off_ST = l.off_SF + align256(sizeof(double) * n * M * n_ch);
+  l.off_TP = l.off_ST + align256(sizeof(double) * n * (M + 1) * n_ch);
   l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - nb * lfd::FR_L + padlen) * n_ch);
   return l;
 }
@@ -1667,9 +1668,8 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
       LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, n_t, g, fe->d_ktaps, tg, F, st));
       if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
       const lfd::FRSeg sg = fullrate_segments(c, 4 * nb);
-      LFD_HIP(lfd::launch_fullrate_scan_seg(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F,
-                                            reinterpret_cast<double *>(ws + lo.off_SFm), SF, ST, TP, y, ys_ch, ys_t,
-                                            sg, st));
+      LFD_HIP(lfd::launch_fullrate_scan_seg(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F, SF, ST, TP, y,
+                                            ys_ch, ys_t, sg, st));
     } else {
       LFD_HIP(lfd::launch_fullrate_blocks(n_sec, false, x, s_ch, s_t, n_ch, nb, fe->d_fc, nullptr, nullptr, F,
                                           nullptr, 0, 0, st));
@@ -1679,7 +1679,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     }
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[2], st));
     LFD_HIP(lfd::launch_fullrate_blocks(n_sec, true, x, s_ch, s_t, n_ch, nb, fe->d_fc, SF, ST, nullptr, y,
-                                        ys_ch, ys_t, st));
+                                        ys_ch, ys_t, st, mb));
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[3], st));
     return LFD_OK;
   }

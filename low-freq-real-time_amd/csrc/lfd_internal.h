@@ -234,24 +234,25 @@ struct FRConst {
 // Launchers (lfd_kernels.hip).  All return hipError_t of the launch.
 // Full-rate wave kernels: out == false writes the big blocks' functionals F;
 // out == true reads the scan's SF / ST and writes y[ch, 0 : nb * FR_L].
+// mb (out only): SF / ST are the medium-block states of k_fullrate_scan_seg.
 hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s_ch, int64_t s_t,
                                   int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
                                   const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
-                                  hipStream_t st);
+                                  hipStream_t st, bool mb = false);
 // Segmented scan over the medium blocks (FR_LB) of the matrix-core
 // functionals F2 (f_index layout, nF = 2N over 4 nb blocks): a workgroup =
 // 16 channels x G segments of `seglen` medium blocks; per segment a zero-state
 // aggregate, a combine across the segments (powers pseg = PhiB^seglen, plast
-// = PhiB^lastlen), the true states; forward then reverse.  Writes SF / ST at
-// the big-block starts (the output pass's inputs), SFm (all medium blocks),
-// TP and the tail outputs, like k_fullrate_scan.
+// = PhiB^lastlen), the true states; forward then reverse.  Writes SFm / STm
+// (the states at every medium block: the output pass's inputs), TP and the
+// tail outputs, like k_fullrate_scan.
 struct FRSeg {
   double pseg[MAX_N * MAX_N], plast[MAX_N * MAX_N];
   int seglen, lastlen, G, Gu;
 };
 hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
                                     int64_t nb, int padlen, const FRConst *fc, const double *F2, double *SFm,
-                                    double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
+                                    double *STm, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
                                     const FRSeg &sg, hipStream_t st);
 // Per-channel walk over the big blocks + both edges (odd extension, zi) and
 // the outputs of the tail [nb * FR_L, n_t).  TP: (n_t - nb * FR_L + padlen) x n_ch.

@@ -976,7 +976,90 @@ __constant__ int g_fr_stage_old = 0;
 #define FR_WAVES 4  // waves per SIMD the register budget targets (<= 128 VGPRs)
 #endif
 
-template <int NS, bool OUT>
+// Output stage of the full-rate wave kernel: y_j = r0_j + Q w_j with
+// w_j = (S_j, T_{j+1}) and Q[i] = (Rh[i], H[31 - i]): the 32 x 2N by 2N x 64
+// product on the fp64 matrix cores (v_mfma_f64_16x16x4: A = Q from
+// FRConst::QA, B = w staged through LDS, C = r0 read back in the accumulator
+// layout), two passes of 16 samples through a 64 x 16 LDS stage, rows of
+// 128 B leaving as 16-B stores.  LDS rows of OSTR = 18 doubles (36 dwords =
+// 4 x odd): the MFMA-layout accesses (16 rows x 4 adjacent doubles per
+// instruction) hit distinct banks, and the row writes go out as 16-B
+// ds_write_b128, conflict-free per 8 lanes (lane stride 36 dwords).
+template <int NS>
+__device__ __forceinline__ void fr_out_mfma(int lane, const FRConst *__restrict__ fc, const double (&Sj)[2 * NS],
+                                            const double (&T)[2 * NS], const double (&r0)[FR_LS], double *lds,
+                                            double *__restrict__ yr, int64_t ys_t) {
+  constexpr int N = 2 * NS, LS = FR_LS, OSTR = 18;
+  constexpr int K = 2 * N, KS = K / 4;
+  const int col = lane & 15, q = lane >> 4;
+  double *W = lds;  // [64][K], stride OSTR (the tile's reads are done: one wave, LDS in order)
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    W[lane * OSTR + n] = Sj[n];
+    W[lane * OSTR + N + n] = T[n];
+  }
+  __syncthreads();
+  double bop[KS][4], aop[2][KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bop[ks][nt] = W[(16 * nt + col) * OSTR + 4 * ks + q];
+    aop[0][ks] = fc->QA[0][ks][lane];
+    aop[1][ks] = fc->QA[1][ks][lane];
+  }
+  __syncthreads();
+  double *ob = lds;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 16; i += 2)
+      *reinterpret_cast<double2 *>(ob + lane * OSTR + i) = double2{r0[16 * mt + i], r0[16 * mt + i + 1]};
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      double *o = ob + (16 * nt + col) * OSTR + q;
+      fr_d4v acc = {o[0], o[4], o[8], o[12]};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[mt][ks], bop[ks][nt], acc, 0, 0, 0);
+      o[0] = acc[0];
+      o[4] = acc[1];
+      o[8] = acc[2];
+      o[12] = acc[3];
+    }
+    __syncthreads();
+    if (ys_t == 1 && (reinterpret_cast<uintptr_t>(yr) & 15) == 0) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
+        *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 4 + (lane >> 4), c = lane & 15;
+        yr[(r * LS + 16 * mt + c) * ys_t] = ob[r * OSTR + c];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// One DPP lane move of a double inside 16-lane rows (both 32-bit halves;
+// lanes whose source leaves the row read 0.0): row_shr:d = 0x110 + d,
+// row_shl:d = 0x100 + d.
+template <int CTRL>
+__device__ __forceinline__ double dpp_row_d(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
+  const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+  return __hiloint2double(h2, l2);
+}
+
+// MB (medium-block states, OUT only): SF / ST hold the states at EVERY
+// medium block (FR_LB = 16 sub-blocks: one 16-lane row), so the wave scans
+// run inside the rows on DPP lane moves (row_shr / row_shl: VALU, no LDS
+// round trips) with 4 log-steps instead of 6 ds_bpermute steps over the wave.
+template <int NS, bool OUT, bool MB = false>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t nb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
@@ -1017,7 +1100,46 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   FwdRec<NS> fr;
   fr.load(fc->cf);
   double r0[OUT ? LS : 1], A[N], Z[N];
-  if constexpr (OUT) {
+  float xs_mb[MB ? LS : 1];
+  if constexpr (MB) {
+    // (A_j, Z0_j) = KAZ x_j on the matrix cores (as the functionals pass);
+    // the zero-state responses r0 are formed after the scans, so they are
+    // not held in registers across them
+    fr_d4v acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
+    const float *tb = tile + 36 * col + q;
+#pragma unroll
+    for (int ks = 0; ks < LS / 4; ++ks) {
+      const double av = fc->KAZ[ks][lane];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[36 * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
+    }
+    // the lane's own 32 samples into registers (for r0 after the scans),
+    // then the exchange through the tile's LDS
+    const float *tr = tile + 36 * lane;
+#pragma unroll
+    for (int g = 0; g < LS / 4; ++g) {
+      const float4 v = *reinterpret_cast<const float4 *>(tr + 4 * g);
+      xs_mb[4 * g + 0] = v.x;
+      xs_mb[4 * g + 1] = v.y;
+      xs_mb[4 * g + 2] = v.z;
+      xs_mb[4 * g + 3] = v.w;
+    }
+    __syncthreads();
+    double *az = lds;  // [sub-block][functional], stride OSTR
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) az[(16 * nt + col) * OSTR + q + 4 * r] = acc[nt][r];
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      A[n] = az[lane * OSTR + n];
+      Z[n] = az[lane * OSTR + N + n];
+    }
+  } else if constexpr (OUT) {
     // ---- 1, 2. zero-state forward, then zero-state reverse over its output
     float xs[LS];
     const float *tr = tile + 36 * lane;
@@ -1075,6 +1197,72 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
       v[r] = acc;
     }
   };
+  if constexpr (MB) {
+    // ---- 3, 4 inside the rows: row r = medium block m = 4k + r, lane jr its
+    // 32-sample sub-block; S entering the row SF[m], T entering it ST[m + 1]
+    const int jr = lane & 15;
+    const int64_t m = 4 * k + (lane >> 4);
+    double Sin[N], Tin[N], vf[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      Sin[n] = SF[(m * N + n) * n_ch + ch];
+      vf[n] = A[n];
+    }
+    if (jr == 0) matvec_add(fc->PhiP[0], Sin, vf, true);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double o[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        if (i == 0) o[n] = dpp_row_d<0x111>(vf[n]);
+        if (i == 1) o[n] = dpp_row_d<0x112>(vf[n]);
+        if (i == 2) o[n] = dpp_row_d<0x114>(vf[n]);
+        if (i == 3) o[n] = dpp_row_d<0x118>(vf[n]);
+      }
+      matvec_add(fc->PhiP[i], o, vf, true);  // lanes without a source add PhiP 0
+    }
+    double Sj[N], vb[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const double u = dpp_row_d<0x111>(vf[n]);
+      Sj[n] = jr == 0 ? Sin[n] : u;
+      vb[n] = Z[n];
+    }
+    matvec_add(fc->M32, Sj, vb, false);
+#pragma unroll
+    for (int n = 0; n < N; ++n) Tin[n] = ST[((m + 1) * N + n) * n_ch + ch];
+    if (jr == 15) matvec_add(fc->PhiP[0], Tin, vb, true);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double o[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        if (i == 0) o[n] = dpp_row_d<0x101>(vb[n]);
+        if (i == 1) o[n] = dpp_row_d<0x102>(vb[n]);
+        if (i == 2) o[n] = dpp_row_d<0x104>(vb[n]);
+        if (i == 3) o[n] = dpp_row_d<0x108>(vb[n]);
+      }
+      matvec_add(fc->PhiP[i], o, vb, true);
+    }
+    double T[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const double u = dpp_row_d<0x101>(vb[n]);
+      T[n] = jr == 15 ? Tin[n] : u;
+    }
+    {
+      // ---- zero-state forward, then zero-state reverse over its output
+      double zf[N], zr[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) zf[n] = zr[n] = 0.0;
+#pragma unroll
+      for (int i = 0; i < LS; ++i) r0[i] = fr.step(zf, (double)xs_mb[i]);
+#pragma unroll
+      for (int i = LS - 1; i >= 0; --i) r0[i] = fr.step(zr, r0[i]);
+    }
+    fr_out_mfma<NS>(lane, fc, Sj, T, r0, lds, y + ch * ys_ch + a * ys_t, ys_t);
+    return;
+  }
   // ---- 3. forward wave scan
   double Sin[N], vf[N], Sj[N];
 #pragma unroll
@@ -1134,60 +1322,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     const double u = __shfl_down(vb[n], 1);
     T[n] = lane == 63 ? Tin[n] : u;
   }
-  constexpr int K = 2 * N, KS = K / 4;
-  double *W = lds;  // [64][K], stride OSTR
-#pragma unroll
-  for (int n = 0; n < N; ++n) {
-    W[lane * OSTR + n] = Sj[n];
-    W[lane * OSTR + N + n] = T[n];
-  }
-  __syncthreads();
-  double bop[KS][4], aop[2][KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bop[ks][nt] = W[(16 * nt + col) * OSTR + 4 * ks + q];
-    aop[0][ks] = fc->QA[0][ks][lane];
-    aop[1][ks] = fc->QA[1][ks][lane];
-  }
-  __syncthreads();
-  // two passes of 16 samples (one MFMA row tile each) through a 64 x 16 LDS
-  // stage: rows of 128 B leave as 16-B stores
-  double *ob = lds;
-  double *yr = y + ch * ys_ch + a * ys_t;
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) ob[lane * OSTR + i] = r0[16 * mt + i];
-    __syncthreads();
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      double *o = ob + (16 * nt + col) * OSTR + q;
-      fr_d4v acc = {o[0], o[4], o[8], o[12]};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[mt][ks], bop[ks][nt], acc, 0, 0, 0);
-      o[0] = acc[0];
-      o[4] = acc[1];
-      o[8] = acc[2];
-      o[12] = acc[3];
-    }
-    __syncthreads();
-    if (ys_t == 1 && (reinterpret_cast<uintptr_t>(yr) & 15) == 0) {
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
-        *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) =
-            *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int r = it * 4 + (lane >> 4), c = lane & 15;
-        yr[(r * LS + 16 * mt + c) * ys_t] = ob[r * OSTR + c];
-      }
-    }
-    __syncthreads();
-  }
+  if constexpr (OUT) fr_out_mfma<NS>(lane, fc, Sj, T, r0, lds, y + ch * ys_ch + a * ys_t, ys_t);
 }
 
 // k_fullrate_scan: one thread per channel.  SciPy's left edge (odd extension,
@@ -1352,22 +1487,23 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
 // 16 channels contiguous per (block, component); components 0..N-1 = A, the
 // forward exit from zero state, N..2N-1 = Z, the zero-state reverse exit of
 // the zero-state forward output).  One workgroup = 16 channels x G segments
-// of seglen medium blocks (lane = channel, 4 segments per wave):
+// of seglen medium blocks (G <= 32; lane = channel, 4 segments per wave):
 //   A  each segment's forward aggregate from zero state
 //   -> entering states E_s = pseg E_{s-1} + agg_{s-1}, E_0 = SciPy's left edge
-//   C  the true S_f at every medium block (SFm; SF at the big-block starts);
+//   C  the true S_f at every medium block (SFm);
 //      the last segment continues over the tail and right pad and returns
 //      from zi * y_f[-1] (T_end, the tail's outputs)
 //   A' each segment's reverse aggregate from zero T: T <- PhiB T + Z + MB S_f
-//   -> entering T from the right, C' the true T (ST at the big-block starts).
+//   -> entering T from the right, C' the true T at every medium block (STm).
+// The output pass (k_fullrate_wave<NS, true, true>) reads SFm / STm per row.
 // 16 x G threads per channel group instead of one thread per channel walking
 // every block: the walks are G times shorter (latency-bound chains).
 template <int NS>
-__global__ __launch_bounds__(1024) void k_fullrate_scan_seg(
+__global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t nb, int padlen,
     const FRConst *__restrict__ fc, const double *__restrict__ F2, double *__restrict__ SFm,
-    double *__restrict__ SF, double *__restrict__ ST, double *__restrict__ TP, double *__restrict__ y,
-    int64_t ys_ch, int64_t ys_t, FRSeg sg) {
+    double *__restrict__ STm, double *__restrict__ TP, double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
+    FRSeg sg) {
   constexpr int N = 2 * NS;
   __shared__ double cPB[N * N], cMB[N * N], cPS[N * N], cPT[N * N];
   __shared__ double slotL[16][N], slotR[16][N];
@@ -1403,18 +1539,31 @@ __global__ __launch_bounds__(1024) void k_fullrate_scan_seg(
     }
   };
   double *ag = agg + ((size_t)seg * 16 + col) * N;
+  // Every walk loads QF (forward) / QR (reverse) blocks before applying them,
+  // at clamped indices (unconditional loads: a conditional load made the
+  // compiler wait for everything in flight), so the chain waits one memory
+  // latency per batch instead of per block.
+  constexpr int QF = 4, QR = 2;
+  auto fload = [&](int64_t m, int c0, double (&f)[N]) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) f[n] = Fc[(m * 2 * N + c0 + n) * 16];
+  };
   // ---- A: forward aggregate of the segment from zero state
   double a[N];
 #pragma unroll
   for (int n = 0; n < N; ++n) a[n] = 0.0;
   if (live) {
-    for (int64_t m = m0; m < m1; ++m) {
-      double f[N];
+    for (int64_t mb = m0; mb < m1; mb += QF) {
+      double fq[QF][N];
 #pragma unroll
-      for (int n = 0; n < N; ++n) f[n] = Fc[(m * 2 * N + n) * 16];
-      mv(cPB, a, f, true);
+      for (int u = 0; u < QF; ++u) fload(mb + u < m1 ? mb + u : m1 - 1, 0, fq[u]);
 #pragma unroll
-      for (int n = 0; n < N; ++n) a[n] = f[n];
+      for (int u = 0; u < QF; ++u)
+        if (mb + u < m1) {
+          mv(cPB, a, fq[u], true);
+#pragma unroll
+          for (int n = 0; n < N; ++n) a[n] = fq[u][n];
+        }
     }
   }
 #pragma unroll
@@ -1447,31 +1596,41 @@ __global__ __launch_bounds__(1024) void k_fullrate_scan_seg(
   }
   // ---- C: true forward states
   if (live) {
-    for (int64_t m = m0; m < m1; ++m) {
-      double f[N];
+    for (int64_t mb = m0; mb < m1; mb += QF) {
+      double fq[QF][N];
 #pragma unroll
-      for (int n = 0; n < N; ++n) {
-        f[n] = Fc[(m * 2 * N + n) * 16];
-        SFm[(m * N + n) * n_ch + ch] = z[n];
+      for (int u = 0; u < QF; ++u) fload(mb + u < m1 ? mb + u : m1 - 1, 0, fq[u]);
+#pragma unroll
+      for (int u = 0; u < QF; ++u) {
+        const int64_t m = mb + u;
+        if (m < m1) {
+#pragma unroll
+          for (int n = 0; n < N; ++n) SFm[(m * N + n) * n_ch + ch] = z[n];
+          mv(cPB, z, fq[u], true);
+#pragma unroll
+          for (int n = 0; n < N; ++n) z[n] = fq[u][n];
+        }
       }
-      if ((m & 3) == 0) {
-#pragma unroll
-        for (int n = 0; n < N; ++n) SF[((m >> 2) * N + n) * n_ch + ch] = z[n];
-      }
-      mv(cPB, z, f, true);
-#pragma unroll
-      for (int n = 0; n < N; ++n) z[n] = f[n];
     }
     if (seg == sg.Gu - 1) {
       // tail samples [nb FR_L, n_t) and the right pad forward (TP), then the
-      // reverse from zi * y_f[-1] over pad + tail (the tail's outputs)
+      // reverse from zi * y_f[-1] over pad + tail (the tail's outputs); the
+      // reverse re-reads TP in batches of B (one latency per batch)
+      constexpr int B = 8;
       const int64_t t_tail = nb * FR_L, nt = n_t - t_tail;
       double *tp = TP + ch;
       const float *xt = xc + t_tail * s_t;
       double yl = 0.0;
-      for (int64_t i = 0; i < nt; ++i) {
-        yl = fr.step(z, (double)xt[i * s_t]);
-        tp[i * n_ch] = yl;
+      for (int64_t i0 = 0; i0 < nt; i0 += B) {
+        float xv[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) xv[u] = xt[(i0 + u < nt ? i0 + u : nt - 1) * s_t];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+          if (i0 + u < nt) {
+            yl = fr.step(z, (double)xv[u]);
+            tp[(i0 + u) * n_ch] = yl;
+          }
       }
       for (int64_t i = 0; i < E; ++i) {
         yl = fr.step(z, (double)(2.0f * xn - xc[(n_t - 2 - i) * s_t]));
@@ -1481,30 +1640,43 @@ __global__ __launch_bounds__(1024) void k_fullrate_scan_seg(
       for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * yl;
       for (int64_t i = nt + E - 1; i >= nt; --i) (void)fr.step(z, tp[i * n_ch]);
       double *yt = y + ch * ys_ch + t_tail * ys_t;
-      for (int64_t i = nt - 1; i >= 0; --i) yt[i * ys_t] = fr.step(z, tp[i * n_ch]);
+      for (int64_t i1 = nt - 1; i1 >= 0; i1 -= B) {
+        double tv[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) tv[u] = tp[(i1 - u >= 0 ? i1 - u : 0) * n_ch];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+          if (i1 - u >= 0) yt[(i1 - u) * ys_t] = fr.step(z, tv[u]);
+      }
 #pragma unroll
       for (int n = 0; n < N; ++n) {
         slotR[col][n] = z[n];
-        ST[(nb * N + n) * n_ch + ch] = z[n];
+        STm[(M * N + n) * n_ch + ch] = z[n];
       }
     }
   }
   __syncthreads();
   // ---- A': reverse aggregate of the segment from zero T (true S_f coupling)
+  auto rload = [&](int64_t m, double (&f)[N], double (&sf)[N]) {
+    fload(m, N, f);
+#pragma unroll
+    for (int n = 0; n < N; ++n) sf[n] = SFm[(m * N + n) * n_ch + ch];
+  };
 #pragma unroll
   for (int n = 0; n < N; ++n) a[n] = 0.0;
   if (live) {
-    for (int64_t m = m1 - 1; m >= m0; --m) {
-      double f[N], sf[N];
+    for (int64_t mb = m1 - 1; mb >= m0; mb -= QR) {
+      double fq[QR][N], sq[QR][N];
 #pragma unroll
-      for (int n = 0; n < N; ++n) {
-        f[n] = Fc[(m * 2 * N + N + n) * 16];
-        sf[n] = SFm[(m * N + n) * n_ch + ch];
-      }
-      mv(cPB, a, f, true);
-      mv(cMB, sf, f, false);
+      for (int u = 0; u < QR; ++u) rload(mb - u >= m0 ? mb - u : m0, fq[u], sq[u]);
 #pragma unroll
-      for (int n = 0; n < N; ++n) a[n] = f[n];
+      for (int u = 0; u < QR; ++u)
+        if (mb - u >= m0) {
+          mv(cPB, a, fq[u], true);
+          mv(cMB, sq[u], fq[u], false);
+#pragma unroll
+          for (int n = 0; n < N; ++n) a[n] = fq[u][n];
+        }
     }
   }
 #pragma unroll
@@ -1524,20 +1696,22 @@ __global__ __launch_bounds__(1024) void k_fullrate_scan_seg(
   }
   // ---- C': true reverse states
   if (live) {
-    for (int64_t m = m1 - 1; m >= m0; --m) {
-      double f[N], sf[N];
+    for (int64_t mb = m1 - 1; mb >= m0; mb -= QR) {
+      double fq[QR][N], sq[QR][N];
 #pragma unroll
-      for (int n = 0; n < N; ++n) {
-        f[n] = Fc[(m * 2 * N + N + n) * 16];
-        sf[n] = SFm[(m * N + n) * n_ch + ch];
-      }
-      mv(cPB, z, f, true);
-      mv(cMB, sf, f, false);
+      for (int u = 0; u < QR; ++u) rload(mb - u >= m0 ? mb - u : m0, fq[u], sq[u]);
 #pragma unroll
-      for (int n = 0; n < N; ++n) z[n] = f[n];
-      if ((m & 3) == 0) {
+      for (int u = 0; u < QR; ++u) {
+        const int64_t m = mb - u;
+        if (m >= m0) {
+          mv(cPB, z, fq[u], true);
+          mv(cMB, sq[u], fq[u], false);
 #pragma unroll
-        for (int n = 0; n < N; ++n) ST[((m >> 2) * N + n) * n_ch + ch] = z[n];
+          for (int n = 0; n < N; ++n) {
+            z[n] = fq[u][n];
+            STm[(m * N + n) * n_ch + ch] = z[n];
+          }
+        }
       }
     }
   }
@@ -2650,7 +2824,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   // the lane id laundered per unit, so that nothing derived from it is
   // hoisted out of the unit loop and held in registers across it
   int lane = lane0;
-  asm volatile("" : "+v"(lane));
+  if constexpr (PERSIST) asm volatile("" : "+v"(lane));
   // channel-group-major unit order (time-major measured 2 % slower on cfg3);
   // g_k1_band > 0 (A/B knob LFD_K1_BAND) walks bands of that many channel
   // groups, time groups inside a band, so fewer pages are in flight at once
@@ -3682,10 +3856,14 @@ hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, 
     if (m4 && pf == 1) return run_k1<1, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     if (!m4 && pf == 2) return run_k1<2, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     if (!m4 && pf == 1) {
-      // persistent units (LFD_K1_PERSIST=0: one unit per wave, the round-3 kernel)
+      // LFD_K1_PERSIST=1: persistent waves walking units w, w + W, ... —
+      // measured slower at every width (1,250 ch 1.98 vs 1.65 ms, 10,000 ch
+      // 14.8 vs 13.6 ms; profiles/r04_ab_k1_persist_*.txt): the unit loop
+      // spills 30 VGPRs under the 128-register cap into the sample loop
       const char *pv = knob("LFD_K1_PERSIST");
-      if (pv && std::atoi(pv) == 0) return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-      return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+      if (pv && std::atoi(pv) != 0)
+        return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+      return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     }
     return hipErrorInvalidValue;
   }
@@ -3722,9 +3900,9 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
   // 512-thread workgroups (2 per CU: 16 waves), prefetch depth 1, registers
   // capped for 4 waves per SIMD: 12.77 ms vs 13.09-13.12 for depth 2 at the
-  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt);
-  // persistent waves (units w, w + W, ...)
-  return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt).
+  // One unit per wave: persistent waves measured slower (diag LFD_K1_PERSIST)
+  return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 #endif
 }
 
@@ -4011,7 +4189,7 @@ hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch
 hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s_ch, int64_t s_t,
                                   int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
                                   const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
-                                  hipStream_t st) {
+                                  hipStream_t st, bool mb) {
   const int64_t n_wg = n_ch * nb;
   if (n_wg < 1 || n_wg > INT32_MAX) return hipErrorInvalidValue;
 #ifdef LFD_DIAG
@@ -4021,14 +4199,16 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
     if (stage_old) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stage_old), &stage_old, sizeof(int));
   }
 #endif
-#define LFD_FR(NS, OUT)                                                                                \
-  k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
+#define LFD_FR(NS, OUT, MB)                                                                            \
+  k_fullrate_wave<NS, OUT, MB><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
                                                          ys_t)
 #define LFD_FR2(NS)   \
-  if (out)            \
-    LFD_FR(NS, true); \
+  if (out && mb)      \
+    LFD_FR(NS, true, true); \
+  else if (out)       \
+    LFD_FR(NS, true, false); \
   else                \
-    LFD_FR(NS, false)
+    LFD_FR(NS, false, false)
   switch (n_sec) {
     case 1: LFD_FR2(1); break;
     case 2: LFD_FR2(2); break;
@@ -4061,9 +4241,9 @@ hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t
 
 hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
                                     int64_t nb, int padlen, const FRConst *fc, const double *F2, double *SFm,
-                                    double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
+                                    double *STm, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
                                     const FRSeg &sg, hipStream_t st) {
-  if (sg.G < 1 || sg.G > 64 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 || nb < 1) return hipErrorInvalidValue;
+  if (sg.G < 1 || sg.G > 32 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 || nb < 1) return hipErrorInvalidValue;
   const unsigned g = nblk(n_ch, 16);
   const size_t lds = sizeof(double) * (size_t)sg.G * 16 * 2 * n_sec;
   static bool attr = false;  // (dynamic LDS above 64 KB with the static part)
@@ -4078,7 +4258,7 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
     attr = true;
   }
 #define LFD_FRSS(NS) \
-  k_fullrate_scan_seg<NS><<<g, 16 * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, nb, padlen, fc, F2, SFm, SF, ST, TP, y, \
+  k_fullrate_scan_seg<NS><<<g, 16 * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, nb, padlen, fc, F2, SFm, STm, TP, y, \
                                                     ys_ch, ys_t, sg)
   switch (n_sec) {
     case 1: LFD_FRSS(1); break;
