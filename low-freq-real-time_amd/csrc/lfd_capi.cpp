@@ -1526,16 +1526,18 @@ FrLayout fullrate_layout(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64
   return l;
 }
 // Medium-block path: F2 [ch/16][M][2N][16], SF = SFm [M][N][ch], ST = STm
-// [M + 1][N][ch] (M = 4 nb medium blocks), TP.
-FrLayout fullrate_layout_mb(int64_t n_ch, int64_t n_t, int padlen, int n_sec, int64_t nb) {
-  const size_t n = 2 * n_sec, ch16 = (size_t)((n_ch + 15) / 16) * 16, M = 4 * (size_t)nb;
+// [M + 1][N][ch] (M = (n_t - 1) / FR_LB medium blocks), TP.
+int64_t fullrate_medium_blocks(int64_t n_t) { return (n_t - 1) / lfd::FR_LB; }  // the tail keeps >= 1 sample
+FrLayout fullrate_layout_mb(int64_t n_ch, int64_t n_t, int padlen, int n_sec) {
+  const size_t n = 2 * n_sec, ch16 = (size_t)((n_ch + 15) / 16) * 16;
+  const int64_t M = fullrate_medium_blocks(n_t);
   FrLayout l{};
   l.off_F = 0;
   l.off_SF = align256(sizeof(double) * 2 * n * M * ch16);
   l.off_SFm = l.off_SF;
   l.off_ST = l.off_SF + align256(sizeof(double) * n * M * n_ch);
   l.off_TP = l.off_ST + align256(sizeof(double) * n * (M + 1) * n_ch);
-  l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - nb * lfd::FR_L + padlen) * n_ch);
+  l.bytes = l.off_TP + align256(sizeof(double) * (size_t)(n_t - M * lfd::FR_LB + padlen) * n_ch);
   return l;
 }
 
@@ -1600,7 +1602,7 @@ size_t lfd_sosfiltfilt_workspace_bytes(int64_t n_ch, int64_t n_t, int padlen, in
     const int64_t nb = fullrate_blocks(n_t);
     if (nb > 0)
       b = std::max({b, fullrate_layout(n_ch, n_t, padlen, n_sec, nb).bytes,
-                    fullrate_layout_mb(n_ch, n_t, padlen, n_sec, nb).bytes});
+                    fullrate_layout_mb(n_ch, n_t, padlen, n_sec).bytes});
   }
   return b;
 }
@@ -1637,7 +1639,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     // on the fp64 matrix cores and the segmented scan
     const bool mb = s_t == 1 && (s_ch % 4 == 0 || n_ch == 1) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
                     !lfd::option(LFD_OPT_FULLRATE_BIGBLOCK);
-    const FrLayout lo = mb ? fullrate_layout_mb(n_ch, n_t, padlen, n_sec, nb)
+    const FrLayout lo = mb ? fullrate_layout_mb(n_ch, n_t, padlen, n_sec)
                            : fullrate_layout(n_ch, n_t, padlen, n_sec, nb);
     char *ws = static_cast<char *>(workspace);
     double *F = reinterpret_cast<double *>(ws + lo.off_F);
@@ -1663,12 +1665,13 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[0], st));
     if (mb) {
       const int n = 2 * n_sec;
-      const lfd::BlockGeom g{n_ch, 4 * nb, 0, lfd::FR_LB, 2 * n, 0};
+      const int64_t M = fullrate_medium_blocks(n_t);
+      const lfd::BlockGeom g{n_ch, M, 0, lfd::FR_LB, 2 * n, 0};
       const lfd::TapGeom tg{lfd::FR_LB, 0, 2 * n, 1, 0};
       LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, n_t, g, fe->d_ktaps, tg, F, st));
       if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
-      const lfd::FRSeg sg = fullrate_segments(c, 4 * nb);
-      LFD_HIP(lfd::launch_fullrate_scan_seg(n_sec, x, s_ch, s_t, n_ch, n_t, nb, padlen, fe->d_fc, F, SF, ST, TP, y,
+      const lfd::FRSeg sg = fullrate_segments(c, M);
+      LFD_HIP(lfd::launch_fullrate_scan_seg(n_sec, x, s_ch, s_t, n_ch, n_t, M, padlen, fe->d_fc, F, SF, ST, TP, y,
                                             ys_ch, ys_t, sg, st));
     } else {
       LFD_HIP(lfd::launch_fullrate_blocks(n_sec, false, x, s_ch, s_t, n_ch, nb, fe->d_fc, nullptr, nullptr, F,
@@ -1678,8 +1681,9 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
                                         ys_ch, ys_t, st));
     }
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[2], st));
-    LFD_HIP(lfd::launch_fullrate_blocks(n_sec, true, x, s_ch, s_t, n_ch, nb, fe->d_fc, SF, ST, nullptr, y,
-                                        ys_ch, ys_t, st, mb));
+    const int64_t n_mb = mb ? fullrate_medium_blocks(n_t) : 0;
+    LFD_HIP(lfd::launch_fullrate_blocks(n_sec, true, x, s_ch, s_t, n_ch, mb ? (n_mb + 3) / 4 : nb, fe->d_fc, SF, ST,
+                                        nullptr, y, ys_ch, ys_t, st, mb, n_mb));
     if (timed) LFD_HIP(hipEventRecord(g_fr_ev[3], st));
     return LFD_OK;
   }

@@ -234,11 +234,12 @@ struct FRConst {
 // Launchers (lfd_kernels.hip).  All return hipError_t of the launch.
 // Full-rate wave kernels: out == false writes the big blocks' functionals F;
 // out == true reads the scan's SF / ST and writes y[ch, 0 : nb * FR_L].
-// mb (out only): SF / ST are the medium-block states of k_fullrate_scan_seg.
+// mb (out only): SF / ST are the medium-block states of k_fullrate_scan_seg
+// over n_mb medium blocks; nb = ceil(n_mb / 4) big blocks (the last partial).
 hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s_ch, int64_t s_t,
                                   int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
                                   const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
-                                  hipStream_t st, bool mb = false);
+                                  hipStream_t st, bool mb = false, int64_t n_mb = 0);
 // Segmented scan over the medium blocks (FR_LB) of the matrix-core
 // functionals F2 (f_index layout, nF = 2N over 4 nb blocks): a workgroup =
 // 16 channels x G segments of `seglen` medium blocks; per segment a zero-state
@@ -251,7 +252,7 @@ struct FRSeg {
   int seglen, lastlen, G, Gu;
 };
 hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
-                                    int64_t nb, int padlen, const FRConst *fc, const double *F2, double *SFm,
+                                    int64_t M, int padlen, const FRConst *fc, const double *F2, double *SFm,
                                     double *STm, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
                                     const FRSeg &sg, hipStream_t st);
 // Per-channel walk over the big blocks + both edges (odd extension, zi) and

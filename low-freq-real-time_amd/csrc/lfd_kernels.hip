@@ -985,10 +985,11 @@ __constant__ int g_fr_stage_old = 0;
 // 4 x odd): the MFMA-layout accesses (16 rows x 4 adjacent doubles per
 // instruction) hit distinct banks, and the row writes go out as 16-B
 // ds_write_b128, conflict-free per 8 lanes (lane stride 36 dwords).
+// nsb: sub-blocks (rows of 32 samples) whose outputs are stored (64 = all).
 template <int NS>
 __device__ __forceinline__ void fr_out_mfma(int lane, const FRConst *__restrict__ fc, const double (&Sj)[2 * NS],
                                             const double (&T)[2 * NS], const double (&r0)[FR_LS], double *lds,
-                                            double *__restrict__ yr, int64_t ys_t) {
+                                            double *__restrict__ yr, int64_t ys_t, int nsb = 64) {
   constexpr int N = 2 * NS, LS = FR_LS, OSTR = 18;
   constexpr int K = 2 * N, KS = K / 4;
   const int col = lane & 15, q = lane >> 4;
@@ -1031,13 +1032,14 @@ __device__ __forceinline__ void fr_out_mfma(int lane, const FRConst *__restrict_
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
-        *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
+        if (r < nsb)
+          *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
       }
     } else {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const int r = it * 4 + (lane >> 4), c = lane & 15;
-        yr[(r * LS + 16 * mt + c) * ys_t] = ob[r * OSTR + c];
+        if (r < nsb) yr[(r * LS + 16 * mt + c) * ys_t] = ob[r * OSTR + c];
       }
     }
     __syncthreads();
@@ -1063,7 +1065,7 @@ template <int NS, bool OUT, bool MB = false>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t nb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
-    double *__restrict__ F, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+    double *__restrict__ F, double *__restrict__ y, int64_t ys_ch, int64_t ys_t, int64_t n_mb) {
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L;
   static_assert(LS == 32, "tile reads assume 32-sample sub-blocks");
   constexpr int TLDS = L + 4 * (L / 32);
@@ -1077,12 +1079,18 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   const int col = lane & 15, q = lane >> 4;
   const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
   const int64_t a = k * L;
+  // (MB) the last big block may hold fewer than 4 medium blocks: samples
+  // past them are not loaded (zeros; their rows' outputs are not stored)
+  const int nvs = MB ? (int)(n_mb - 4 * k < 4 ? (n_mb - 4 * k) * FR_LB : L) : L;
   {
     // every load of the big block issued before the first LDS write (8 KB
     // per wave in flight, one memory latency per block); time-contiguous,
     // 16-B aligned rows as float4 (1 KB per instruction)
     const float *row = x + ch * s_ch + a * s_t;
-    if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !LFD_DG(g_fr_stage_old)) {
+    if (MB && nvs < L) {
+#pragma unroll 8
+      for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = u < nvs ? row[u] : 0.0f;
+    } else if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !LFD_DG(g_fr_stage_old)) {
       float4 v[L / 256];
 #pragma unroll
       for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
@@ -1201,7 +1209,8 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     // ---- 3, 4 inside the rows: row r = medium block m = 4k + r, lane jr its
     // 32-sample sub-block; S entering the row SF[m], T entering it ST[m + 1]
     const int jr = lane & 15;
-    const int64_t m = 4 * k + (lane >> 4);
+    const int64_t m_row = 4 * k + (lane >> 4);
+    const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
     double Sin[N], Tin[N], vf[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
@@ -1260,7 +1269,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
 #pragma unroll
       for (int i = LS - 1; i >= 0; --i) r0[i] = fr.step(zr, r0[i]);
     }
-    fr_out_mfma<NS>(lane, fc, Sj, T, r0, lds, y + ch * ys_ch + a * ys_t, ys_t);
+    fr_out_mfma<NS>(lane, fc, Sj, T, r0, lds, y + ch * ys_ch + a * ys_t, ys_t, nvs / LS);
     return;
   }
   // ---- 3. forward wave scan
@@ -1490,7 +1499,9 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
 // of seglen medium blocks (G <= 32; lane = channel, 4 segments per wave):
 //   A  each segment's forward aggregate from zero state
 //   -> entering states E_s = pseg E_{s-1} + agg_{s-1}, E_0 = SciPy's left edge
-//   C  the true S_f at every medium block (SFm);
+//   C  the true S_f at every medium block (SFm); M = (n_t - 1) / FR_LB medium
+//      blocks (the tail keeps < FR_LB + 1 samples: the output pass covers
+//      the medium blocks past the last whole big block as a partial one);
 //      the last segment continues over the tail and right pad and returns
 //      from zi * y_f[-1] (T_end, the tail's outputs)
 //   A' each segment's reverse aggregate from zero T: T <- PhiB T + Z + MB S_f
@@ -1500,7 +1511,7 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
 // every block: the walks are G times shorter (latency-bound chains).
 template <int NS>
 __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
-    const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t nb, int padlen,
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t M, int padlen,
     const FRConst *__restrict__ fc, const double *__restrict__ F2, double *__restrict__ SFm,
     double *__restrict__ STm, double *__restrict__ TP, double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
     FRSeg sg) {
@@ -1519,7 +1530,6 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
   __syncthreads();
   const int64_t ch = (int64_t)blockIdx.x * 16 + col;
   const bool active = ch < n_ch;
-  const int64_t M = 4 * nb;
   const int64_t m0 = (int64_t)seg * sg.seglen;
   const int64_t m1 = m0 + sg.seglen < M ? m0 + sg.seglen : M;
   const bool live = active && seg < sg.Gu;
@@ -1617,7 +1627,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
       // reverse from zi * y_f[-1] over pad + tail (the tail's outputs); the
       // reverse re-reads TP in batches of B (one latency per batch)
       constexpr int B = 8;
-      const int64_t t_tail = nb * FR_L, nt = n_t - t_tail;
+      const int64_t t_tail = M * FR_LB, nt = n_t - t_tail;
       double *tp = TP + ch;
       const float *xt = xc + t_tail * s_t;
       double yl = 0.0;
@@ -4189,7 +4199,7 @@ hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch
 hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s_ch, int64_t s_t,
                                   int64_t n_ch, int64_t nb, const FRConst *fc, const double *SF,
                                   const double *ST, double *F, double *y, int64_t ys_ch, int64_t ys_t,
-                                  hipStream_t st, bool mb) {
+                                  hipStream_t st, bool mb, int64_t n_mb) {
   const int64_t n_wg = n_ch * nb;
   if (n_wg < 1 || n_wg > INT32_MAX) return hipErrorInvalidValue;
 #ifdef LFD_DIAG
@@ -4201,7 +4211,7 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
 #endif
 #define LFD_FR(NS, OUT, MB)                                                                            \
   k_fullrate_wave<NS, OUT, MB><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
-                                                         ys_t)
+                                                             ys_t, n_mb)
 #define LFD_FR2(NS)   \
   if (out && mb)      \
     LFD_FR(NS, true, true); \
@@ -4240,10 +4250,10 @@ hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t
 }
 
 hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
-                                    int64_t nb, int padlen, const FRConst *fc, const double *F2, double *SFm,
+                                    int64_t M, int padlen, const FRConst *fc, const double *F2, double *SFm,
                                     double *STm, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
                                     const FRSeg &sg, hipStream_t st) {
-  if (sg.G < 1 || sg.G > 32 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 || nb < 1) return hipErrorInvalidValue;
+  if (sg.G < 1 || sg.G > 32 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 || M < 1) return hipErrorInvalidValue;
   const unsigned g = nblk(n_ch, 16);
   const size_t lds = sizeof(double) * (size_t)sg.G * 16 * 2 * n_sec;
   static bool attr = false;  // (dynamic LDS above 64 KB with the static part)
@@ -4258,7 +4268,7 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
     attr = true;
   }
 #define LFD_FRSS(NS) \
-  k_fullrate_scan_seg<NS><<<g, 16 * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, nb, padlen, fc, F2, SFm, STm, TP, y, \
+  k_fullrate_scan_seg<NS><<<g, 16 * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, M, padlen, fc, F2, SFm, STm, TP, y, \
                                                     ys_ch, ys_t, sg)
   switch (n_sec) {
     case 1: LFD_FRSS(1); break;

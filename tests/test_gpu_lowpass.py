@@ -107,7 +107,9 @@ def test_lfproc_parity_lattice_grid(layout, off_ns, null):
         f = np.isfinite(r)
         num += float(np.sum((y[:, oa:ob][f] - r[f]) ** 2))
         den += float(np.sum(r[f] ** 2))
-    assert (num / den) ** 0.5 < 1e-4
+    # 1e-4 is the gate; 1e-6 pins the lattice plan's extra float32 rounding
+    # of the phase outputs before the blend (measured ~4e-8)
+    assert (num / den) ** 0.5 < 1e-6
     assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
@@ -333,26 +335,36 @@ def test_full_rate_filtfilt_parity():
     (1000.0, 1.0, 10.0, 2 * 2048, None),
     (1000.0, 1.0, 10.0, 3 * 2048 + 5, 0),
     (250.0, 2.0, None, 6000, 700),
+    # medium-block path (512): one medium block past the last big block with a
+    # 1-sample tail, three past it, a 512-sample tail
+    (1000.0, 1.0, 10.0, 9 * 512 + 1, None),
+    (1000.0, 1.0, 10.0, 11 * 512 + 77, None),
+    (1000.0, 1.0, 10.0, 9 * 512, None),
 ])
-def test_full_rate_blocked_parity(case):
-    """lfd_sosfiltfilt_f32's blocked path (k_fullrate_wave functionals ->
-    k_fullrate_scan -> k_fullrate_wave outputs) against SciPy's sosfiltfilt
-    restatement: relRMS < 1e-10 per channel."""
+@pytest.mark.parametrize("bigblock", [0, 1])
+def test_full_rate_blocked_parity(case, bigblock):
+    """lfd_sosfiltfilt_f32's blocked paths against SciPy's sosfiltfilt
+    restatement, relRMS < 1e-10 per channel: the medium-block path (matrix-core
+    functionals -> k_fullrate_scan_seg -> row-scan output pass, the default
+    for time-contiguous rows) and the big-block path (k_fullrate_wave
+    functionals -> k_fullrate_scan -> k_fullrate_wave outputs)."""
     import torch
+    from lfdas._lib import kernel_options
     from lfdas.plan import sosfiltfilt_device
     fs, lo, hi, n_t, padlen = case
     sos = oracle.dascore_pass_filter_sos(fs, lo, hi)
     rng = np.random.default_rng(n_t)
     x = (rng.standard_normal((5, n_t)) + 3).astype(np.float32)
     pl = -1 if padlen is None else padlen
-    y = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos, pl).cpu().numpy()
-    ref = oracle.sosfiltfilt(sos, x, padlen=padlen)
-    for c in range(x.shape[0]):
-        assert _relrms(y[c], ref[c]) < 1e-10, c
-    for order in (2, 6):  # other cascade lengths (n_sec = 1, 3)
-        sos2 = oracle.butter_sos(order, 0.05)
-        y2 = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos2, pl).cpu().numpy()
-        assert _relrms(y2, oracle.sosfiltfilt(sos2, x, padlen=padlen)) < 1e-10
+    with kernel_options(fullrate_bigblock=bigblock):
+        y = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos, pl).cpu().numpy()
+        ref = oracle.sosfiltfilt(sos, x, padlen=padlen)
+        for c in range(x.shape[0]):
+            assert _relrms(y[c], ref[c]) < 1e-10, c
+        for order in (2, 6):  # other cascade lengths (n_sec = 1, 3)
+            sos2 = oracle.butter_sos(order, 0.05)
+            y2 = sosfiltfilt_device(torch.from_numpy(x).cuda(), sos2, pl).cpu().numpy()
+            assert _relrms(y2, oracle.sosfiltfilt(sos2, x, padlen=padlen)) < 1e-10
 
 
 def test_full_rate_blocked_strides_and_nan():
