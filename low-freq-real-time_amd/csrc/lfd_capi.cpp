@@ -372,6 +372,18 @@ void fullrate_constants(const Cascade &cs, lfd::FRConst &fc) {
     for (int ks = 0; ks < lfd::FR_LS / 4; ++ks)
       for (int l = 0; l < 64; ++l) fc.KAZ[ks][l] = (double)kaz[l & 15][4 * ks + (l >> 4)];
   }
+  {
+    R kr[lfd::FR_LS][lfd::FR_LS] = {{0}};  // kr[i][p]
+    for (int p = 0; p < lfd::FR_LS; ++p) {
+      R z[MAX_N] = {0}, yo[lfd::FR_LS];
+      for (int i = 0; i < lfd::FR_LS; ++i) yo[i] = tdf2_step(cs, z, i == p ? 1.0L : 0.0L);
+      R t[MAX_N] = {0};
+      for (int i = lfd::FR_LS - 1; i >= 0; --i) kr[i][p] = tdf2_step(cs, t, yo[i]);
+    }
+    for (int mt = 0; mt < 2; ++mt)
+      for (int ks = 0; ks < lfd::FR_LS / 4; ++ks)
+        for (int l = 0; l < 64; ++l) fc.KRA[mt][ks][l] = (double)kr[16 * mt + (l & 15)][4 * ks + (l >> 4)];
+  }
   for (int mt = 0; mt < 2; ++mt)
     for (int ks = 0; ks < 4; ++ks)
       for (int l = 0; l < 64; ++l) {

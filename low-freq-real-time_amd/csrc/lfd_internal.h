@@ -227,6 +227,10 @@ struct FRConst {
   // zero-state reverse exit Z0 of a sub-block per unit sample p (rows >= 2N
   // zero), as the A operand per k-step: KAZ[ks][l] = Kaz[l & 15][4 ks + (l >> 4)]
   double KAZ[FR_LS / 4][64];
+  // zero-state response of a sub-block (forward, then reverse over its
+  // output): r0[i] = sum_p Kr[i][p] x[p], as the A operand per row tile mt
+  // and k-step ks: KRA[mt][ks][l] = Kr[16 mt + (l & 15)][4 ks + (l >> 4)]
+  double KRA[2][FR_LS / 4][64];
 };
 // Layouts (channel fastest, so the scan's per-channel threads coalesce):
 //   F [k][2N][ch] (e_f then e_r), SF / ST [k][N][ch] for k in [0, nb].

@@ -1334,6 +1334,245 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   if constexpr (OUT) fr_out_mfma<NS>(lane, fc, Sj, T, r0, lds, y + ch * ys_ch + a * ys_t, ys_t);
 }
 
+// 4 x 4 transpose across the 16-lane rows of a wave: register c of row R
+// becomes register R of row c (v[c] at row R = E[R][c]  ->  v[c] at row R =
+// E[c][R]); two v_permlane32_swap then two v_permlane16_swap per 32-bit half
+// (VALU lane exchanges, no LDS).  permlane32_swap(a, b) swaps a's rows 2, 3
+// with b's rows 0, 1; permlane16_swap(a, b) swaps a's odd rows with b's even
+// rows (tools/check_permlane.hip).
+__device__ __forceinline__ void swap32_d(double &a, double &b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)__double2loint(a), (uint32_t)__double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)__double2hiint(a), (uint32_t)__double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16_d(double &a, double &b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)__double2loint(a), (uint32_t)__double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)__double2hiint(a), (uint32_t)__double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &v2, double &v3) {
+  swap32_d(v0, v2);
+  swap32_d(v1, v3);
+  swap16_d(v0, v1);
+  swap16_d(v2, v3);
+}
+
+// ---------------------------------------------------------------------------
+// k_fullrate_out_mb — output pass of the medium-block full-rate path, with no
+// fp64 recurrence at all: one wave = one big block (FR_L samples, the last
+// one partial), lane = 32-sample sub-block, 16-lane row = medium block with
+// its entering states SF[m] / ST[m + 1] from k_fullrate_scan_seg.
+//   1. (A_j, Z0_j) = KAZ x_j (fp64 MFMA, B from the LDS tile), to the lanes
+//      by a permlane transpose;
+//   2. row scans on DPP: S_j (forward), T_{j+1} (reverse, with Z + M32 S_j);
+//   3. y = Kr x + Q (S_j, T_{j+1}): the zero-state response of the sub-block
+//      AND the state responses as fp64 MFMA products into one accumulator
+//      (A = KRA / QA tables, B = the tile / the states transposed by permlane),
+//      staged through the tile's LDS into rows and stored as 16-B pieces.
+// The round-3 output pass ran the zero-state responses as TDF-II recurrences
+// (40 fp64 FMAs per sample on the VALU: the pass was fp64-issue bound).
+template <int NS>
+__global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
+    const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
+    const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
+    double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+  constexpr int N = 2 * NS, LS = FR_LS, L = FR_L, K = 2 * N, KS = K / 4, OSTR = 18;
+  static_assert(N % 2 == 0 && K % 4 == 0, "state components in groups of 4");
+  constexpr int TLDS = L + 4 * (L / 32);
+  constexpr int NLDS = 64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2;
+  __shared__ __attribute__((aligned(16))) double lds[NLDS];
+  float *tile = reinterpret_cast<float *>(lds);
+  const int lane = threadIdx.x;
+  const int col = lane & 15, q = lane >> 4, jr = lane & 15;
+  const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
+  const int64_t a = k * L;
+  const int nvs = (int)(n_mb - 4 * k < 4 ? (n_mb - 4 * k) * FR_LB : L);
+  {
+    const float *row = x + ch * s_ch + a;
+    if (nvs < L) {
+#pragma unroll 8
+      for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = u < nvs ? row[u] : 0.0f;
+    } else {
+      float4 v[L / 256];
+#pragma unroll
+      for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
+#pragma unroll
+      for (int i = 0; i < L / 256; ++i) {
+        const int u = 4 * lane + 256 * i;
+        *reinterpret_cast<float4 *>(tile + u + 4 * (u >> 5)) = v[i];
+      }
+    }
+  }
+  __syncthreads();
+  const float *tb = tile + 36 * col + q;  // B[k = q][j = col] of tile nt, k-step ks: tb[36*16*nt + 4*ks]
+  // ---- 1. sub-block exits on the matrix cores
+  double A[N], Z[N];
+  {
+    fr_d4v acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < LS / 4; ++ks) {
+      const double av = fc->KAZ[ks][lane];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[36 * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
+    }
+    // acc[nt][r] at row q = functional q + 4r of sub-block 16 nt + col: per r,
+    // transpose (row q <-> register nt) -> at row R, register q' = functional
+    // q' + 4r of this lane's sub-block 16 R + col
+    double f[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double v0 = acc[0][r], v1 = acc[1][r], v2 = acc[2][r], v3 = acc[3][r];
+      rows_transpose4(v0, v1, v2, v3);
+      f[r][0] = v0;
+      f[r][1] = v1;
+      f[r][2] = v2;
+      f[r][3] = v3;
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      A[n] = f[n / 4][n % 4];
+      Z[n] = f[(N + n) / 4][(N + n) % 4];
+    }
+  }
+  auto matvec_add = [&](const double *P, const double (&o)[N], double (&v)[N], bool tri) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double acc = v[r];
+#pragma unroll
+      for (int c = 0; c < N; ++c)
+        if (!tri || c / 2 <= r / 2) acc = fma(P[r * MAX_N + c], o[c], acc);
+      v[r] = acc;
+    }
+  };
+  // ---- 2. row scans (row = medium block m, lane jr = its sub-block)
+  const int64_t m_row = 4 * k + (lane >> 4);
+  const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
+  double W[K];  // (S_j, T_{j+1})
+  {
+    double Sin[N], vf[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      Sin[n] = SF[(m * N + n) * n_ch + ch];
+      vf[n] = A[n];
+    }
+    if (jr == 0) matvec_add(fc->PhiP[0], Sin, vf, true);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double o[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        if (i == 0) o[n] = dpp_row_d<0x111>(vf[n]);
+        if (i == 1) o[n] = dpp_row_d<0x112>(vf[n]);
+        if (i == 2) o[n] = dpp_row_d<0x114>(vf[n]);
+        if (i == 3) o[n] = dpp_row_d<0x118>(vf[n]);
+      }
+      matvec_add(fc->PhiP[i], o, vf, true);  // lanes without a source add PhiP 0
+    }
+    double vb[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const double u = dpp_row_d<0x111>(vf[n]);
+      W[n] = jr == 0 ? Sin[n] : u;
+      vb[n] = Z[n];
+    }
+    double Sj[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) Sj[n] = W[n];
+    matvec_add(fc->M32, Sj, vb, false);
+    double Tin[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) Tin[n] = ST[((m + 1) * N + n) * n_ch + ch];
+    if (jr == 15) matvec_add(fc->PhiP[0], Tin, vb, true);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double o[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        if (i == 0) o[n] = dpp_row_d<0x101>(vb[n]);
+        if (i == 1) o[n] = dpp_row_d<0x102>(vb[n]);
+        if (i == 2) o[n] = dpp_row_d<0x104>(vb[n]);
+        if (i == 3) o[n] = dpp_row_d<0x108>(vb[n]);
+      }
+      matvec_add(fc->PhiP[i], o, vb, true);
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const double u = dpp_row_d<0x101>(vb[n]);
+      W[N + n] = jr == 15 ? Tin[n] : u;
+    }
+  }
+  // ---- 3. y = Kr x + Q w on the matrix cores
+  // state product first (W dies as it is consumed), then Kr x from the tile.
+  // B operand of the state product: k-step ks, tile nt at row q =
+  // W_{sub-block 16 nt + col}[4 ks + q]: per ks a row transpose of W[4ks..]
+  fr_d4v yacc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) yacc[mt][nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    double bop[4] = {W[4 * ks], W[4 * ks + 1], W[4 * ks + 2], W[4 * ks + 3]};
+    rows_transpose4(bop[0], bop[1], bop[2], bop[3]);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const double av = fc->QA[mt][ks][lane];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        yacc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[nt], yacc[mt][nt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < LS / 4; ++ks) {
+    double bx[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bx[nt] = (double)tb[36 * 16 * nt + 4 * ks];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const double av = fc->KRA[mt][ks][lane];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) yacc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bx[nt], yacc[mt][nt], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // the tile's reads are done: its LDS becomes the output stage
+  double *ob = lds;
+  double *yr = y + ch * ys_ch + a * ys_t;
+  const int nsb = nvs / LS;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    // yacc[mt][nt][r] = y[sample 16 mt + q + 4 r] of sub-block 16 nt + col
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      double *o = ob + (16 * nt + col) * OSTR + q;
+      o[0] = yacc[mt][nt][0];
+      o[4] = yacc[mt][nt][1];
+      o[8] = yacc[mt][nt][2];
+      o[12] = yacc[mt][nt][3];
+    }
+    __syncthreads();
+    if (ys_t == 1 && (reinterpret_cast<uintptr_t>(yr) & 15) == 0) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
+        if (r < nsb)
+          *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int r = it * 4 + (lane >> 4), c = lane & 15;
+        if (r < nsb) yr[(r * LS + 16 * mt + c) * ys_t] = ob[r * OSTR + c];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // k_fullrate_scan: one thread per channel.  SciPy's left edge (odd extension,
 // zi * ext[0]) -> S_f at every big block start -> the tail + right pad
 // forward (TP) -> reverse from zi * y_f[-1] over pad + tail, writing the
@@ -4214,7 +4453,7 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
                                                              ys_t, n_mb)
 #define LFD_FR2(NS)   \
   if (out && mb)      \
-    LFD_FR(NS, true, true); \
+    k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out)       \
     LFD_FR(NS, true, false); \
   else                \
