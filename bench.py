@@ -221,6 +221,9 @@ def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_majo
                         "frac": gbs / HBM_PEAK_GBS, "kernel": K1_KERNELS.get(plan.last_kernel()),
                         "kernel_ms": k1, "scan_kernel_ms": float(np.mean(scan_ms)),
                         "alg_bytes_per_sample": 4.0 + 4.0 / R}}
+    n_off, onepass, _ = plan.lattice()
+    if n_off or "lattice" in label:
+        out["lattice"] = {"offsets": n_off, "onepass": onepass}
     plan.close()
     del x, y, wsb
     torch.cuda.empty_cache()
@@ -899,12 +902,12 @@ def main():
     if ws == 1 and not args.no_extra:
         # a grid no single uniform block plan takes: 3 kHz samples on integer-ns
         # times (333,333 ns) drift against the 1 s output grid (lattice plan:
-        # one block sub-plan per phase + the interp1d blend)
+        # one K1 pass forms every phase's outputs, then the interp1d blend)
         secondary["lowpass_3khz_lattice"] = bench_lowpass_line(
             dev, 2000, 3000.0, 1800.0, 1.0, 600, 7,
             label="2,000 ch x 30 min @ 3 kHz (333,333 ns samples: varying interpolation fraction, spacing "
-                  "3,000 / 3,001), dt = 1 s, P = 600, B = 7: lattice plan (kernel_ms = all phase sub-plans, "
-                  "scan_kernel_ms = the blend)")
+                  "3,000 / 3,001), dt = 1 s, P = 600, B = 7: lattice plan, one pass (kernel_ms = the K1 pass "
+                  "with every phase's outputs, scan_kernel_ms = state scan + per-phase outputs + blend)")
     if ws == 1 and not args.no_extra:
         # strong-scaling proxy on one GPU: the channel shard one rank of an
         # N-GPU run owns, timed alone (the driver's SCALE run is the record)

@@ -70,6 +70,7 @@ int lfd_device_count(int *count);
 #define LFD_OPT_NO_HEAD_SKIP 7    /* off-sample grids: walk chunk heads                   */
 #define LFD_OPT_FIR_VALU 8        /* lfd_fir_decimate_f32: VALU kernel, not matrix cores  */
 #define LFD_OPT_FULLRATE_BIGBLOCK 9 /* lfd_sosfiltfilt_f32: big-block functionals + serial scan */
+#define LFD_OPT_LATTICE_PHASES 10   /* lattice plans: one block plan per phase, not one pass */
 int lfd_set_option(int option, int64_t value);
 int lfd_get_option(int option, int64_t *value);
 
@@ -153,6 +154,13 @@ int lfd_debug_block_taps(const lfd_lowpass_plan *plan, double *taps, size_t n_ta
  * are skipped.  LFD_EUNSUPPORTED when the plan has no run mode. */
 int lfd_debug_runs(const lfd_lowpass_plan *plan, int64_t *run_ks, int *run_len,
                    int64_t max_runs, int64_t *n_runs, void *run_const, size_t rc_bytes);
+/* Testing hook: a lattice (composite) plan's one-pass form.  *n_offsets =
+ * its output offsets (0: the plan has no one-pass form and runs one block
+ * plan per phase), *last_onepass = whether the last execute ran it, and
+ * *one_pass = the inner block plan (for lfd_debug_block_taps / _runs /
+ * _plan_constants; owned by the plan).  NULL outputs are skipped. */
+int lfd_debug_lattice(const lfd_lowpass_plan *plan, int64_t *n_offsets, int *last_onepass,
+                      const lfd_lowpass_plan **one_pass);
 /* Testing hook (not a stable interface): copies the plan's kernel constants
  * (lfd::BlockConst, lfd::ScanConst, lfd::ChunkGeom[n_chunks] of
  * csrc/lfd_internal.h) so CPU tests can check the host math without a GPU.

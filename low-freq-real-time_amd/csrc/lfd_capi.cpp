@@ -42,14 +42,14 @@ std::atomic<int> g_timing{0};
 bool lfd::timing_enabled() { return g_timing.load() != 0; }
 
 namespace {
-constexpr int N_OPT = 10;  // LFD_OPT_* ids are 1 .. N_OPT - 1
+constexpr int N_OPT = 11;  // LFD_OPT_* ids are 1 .. N_OPT - 1
 std::atomic<int64_t> g_opt[N_OPT];
 #ifdef LFD_DIAG
 // the A/B environment names the tools/ recipes of rounds 1-3 use
 const char *const k_opt_env[N_OPT] = {nullptr,          "LFD_NO_RUNS",    "LFD_K1_REC",
                                       "LFD_TM_NO_X2",   "LFD_SCAN_DEFER", "LFD_FULLRATE_SERIAL",
                                       "LFD_NO_LATTICE", "LFD_NO_HSKIP",   "LFD_FIR_VALU",
-                                      "LFD_FULLRATE_BIGBLOCK"};
+                                      "LFD_FULLRATE_BIGBLOCK", "LFD_LATTICE_PHASES"};
 #endif
 }  // namespace
 
@@ -244,9 +244,9 @@ struct BlockSim {
 
 // One block of L samples with given initial forward state, reverse state
 // entering from the right and an optional unit impulse in w at offset imp.
-// p0 is the output functional: (1 - ow) y[0] + ow y[1] (ow > 0 needs
-// L >= J + 2).
-BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp, R ow) {
+// p0 is the output functional: (1 - ow) y[off] + ow y[off + 1] (ow > 0 needs
+// L >= off + J + 2; off > 0: the lattice plans' output offsets).
+BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp, R ow, int off = 0) {
   const int n = 2 * m.ns;
   R S[MAX_N], T[MAX_N];
   for (int i = 0; i < n; ++i) {
@@ -263,8 +263,8 @@ BlockSim sim_block(const RModel &m, int L, const R *Sf0, const R *Tr0, int imp, 
   }
   R acc0 = 0, acc1 = 0;
   for (int j = 0; j <= m.J; ++j) {
-    acc0 += m.c[j] * ql[j];
-    if (ow != 0) acc1 += m.c[j] * ql[j + 1];
+    acc0 += m.c[j] * ql[off + j];
+    if (ow != 0) acc1 += m.c[j] * ql[off + j + 1];
   }
   o.p0 = m.G * ((1.0L - ow) * acc0 + ow * acc1);
   return o;
@@ -568,11 +568,13 @@ int block_constants(const Cascade &cs, int L, R ow, lfd::BlockConst &kc, lfd::Sc
 // sample, so the blended output functional (weight ow) runs it over
 // (1 - ow) z[k] + ow z[k-1].
 // Same definitions as sim_block (impulse at w[k], zero states).
-int block_taps(const Cascade &cs, int L, R ow, std::vector<long double> &Kx, int &nc, int &row) {
+// n_off > 0 (lattice plans, ow = 0): rows 2n + d, d < n_off, are the outputs
+// at offset d, the same backward run over z shifted by d samples.
+int block_taps(const Cascade &cs, int L, R ow, std::vector<long double> &Kx, int &nc, int &row, int n_off = 0) {
   RModel m;
   if (int e = make_rmodel(cs, m)) return e;
   const int n = 2 * m.ns, J = m.J;
-  nc = 2 * n + 1;
+  nc = 2 * n + (n_off > 0 ? n_off : 1);
   row = L + J;
   std::vector<R> hS((size_t)L * n), hv(L), Kw((size_t)nc * L, 0.0L);
   {
@@ -598,8 +600,15 @@ int block_taps(const Cascade &cs, int L, R ow, std::vector<long double> &Kx, int
     for (int j = 0; j <= J && j <= k; ++j) acc += m.c[j] * hv[k - j];
     z[k] = acc;
   }
-  for (int k = 0; k < L; ++k) s[k] = (1.0L - ow) * z[k] + (k >= 1 ? ow * z[k - 1] : 0.0L);
-  backward(s, m.G * m.G, &Kw[(size_t)(2 * n) * L]);
+  if (n_off > 0) {
+    for (int d = 0; d < n_off; ++d) {
+      for (int k = 0; k < L; ++k) s[k] = k >= d ? z[k - d] : 0.0L;
+      backward(s, m.G * m.G, &Kw[(size_t)(2 * n + d) * L]);
+    }
+  } else {
+    for (int k = 0; k < L; ++k) s[k] = (1.0L - ow) * z[k] + (k >= 1 ? ow * z[k - 1] : 0.0L);
+    backward(s, m.G * m.G, &Kw[(size_t)(2 * n) * L]);
+  }
   Kx.assign((size_t)nc * row, 0.0L);
   for (int c = 0; c < nc; ++c)
     for (int p = 0; p < row; ++p) {
@@ -752,6 +761,16 @@ struct lfd_lowpass_plan {
   lfd::RunConst *d_rc = nullptr;
   std::vector<int> slot_chunk;    // run slot (chunk-ordered runs) -> its chunk
   int *d_slot_chunk = nullptr;
+  // lattice one-pass plan (n_off > 0; built by plan_create_composite): the
+  // grid is the lattice at its lowest phase, K1 forms the outputs at offsets
+  // 0 .. n_off - 1 of every output block (MFMA rows 8 + d), runs start at
+  // output blocks; per offset its run constants (G0/H0 of that offset) and
+  // chunk output ranges (the points that need that phase)
+  int n_off = 0;
+  std::vector<lfd::RunConst> rc_off;
+  std::vector<lfd::ChunkGeom> chunks_off;  // [n_off][n_chunks]
+  lfd::RunConst *d_rc_off = nullptr;
+  lfd::ChunkGeom *d_chunks_off = nullptr;
   size_t off_Y0 = 0, off_AG = 0, off_SR = 0, off_TR = 0, off_CR = 0;
   int64_t sf_blocks = 0, tp_len = 0;
   size_t off_F = 0, off_SF = 0, off_TP = 0, ws_bytes = 0;
@@ -775,6 +794,12 @@ struct lfd_lowpass_plan {
   size_t off_tmp = 0;
   int64_t *d_bj = nullptr, *d_bi = nullptr;  // grid index; scratch index of y[lo], y[lo + 1] (-1: w == 0)
   double *d_bw = nullptr;
+  // one-pass alternative (channel-major, 16-B aligned rows): one lattice plan
+  // for every phase (n_off offsets), scratch [n_ch][n_off * n_grid]
+  lfd_lowpass_plan *lat = nullptr;
+  int64_t *d_bi_lat = nullptr;
+  size_t off_tmp_lat = 0;
+  mutable bool last_onepass = false;
 };
 
 extern "C" {
@@ -812,7 +837,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
                                int padlen, int64_t n_ch, int64_t n_t,
                                const int64_t *grid_lo, const double *grid_w,
                                int64_t n_grid, const lfd_chunk *chunks,
-                               int64_t n_chunks);
+                               int64_t n_chunks, int n_off = 0);
 static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int n_sec,
                                  int padlen, int64_t n_ch, int64_t n_t,
                                  const int64_t *grid_lo, const double *grid_w,
@@ -838,7 +863,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
                                int padlen, int64_t n_ch, int64_t n_t,
                                const int64_t *grid_lo, const double *grid_w,
                                int64_t n_grid, const lfd_chunk *chunks,
-                               int64_t n_chunks) {
+                               int64_t n_chunks, int n_off) {
   if (!out) return fail(LFD_EINVAL, "plan out-pointer is NULL");
   *out = nullptr;
   Cascade c;
@@ -861,12 +886,15 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
   }
   if (Rg < 2 || Rg > (int64_t)1 << 30)
     return fail(LFD_EUNSUPPORTED, "grid spacing must be in [2, 2^30] samples");
+  if (n_off > 0 && (n_off > lfd::LAT_MAX_OFF || n_sec != 2 || w0 != 0.0))
+    return fail(LFD_EUNSUPPORTED, "lattice one-pass: 2 sections, sample-aligned lattice, <= 8 offsets");
   // Block length L = Rg / kstep: long grid spacings (Rg > 504: dt = 10 s at
   // 200 Hz - 2 kHz, dt = 1 s at 2 kHz) are cut into sub-blocks of <= 504
   // samples so that the MFMA tap table (L * 72 B) + run buffers fit two
   // 512-thread workgroups per CU; outputs sit at every kstep-th block start.
   const int64_t kstep = sub_block_step(Rg, 2 * n_sec, w0 != 0.0);
   const int L = (int)(Rg / kstep);
+  if (n_off > 0 && L < n_off + 2 * n_sec + 1) return fail(LFD_EUNSUPPORTED, "lattice one-pass: block too short");
   const int64_t base0 = ((grid_lo[0] % L) + L) % L;
 
   auto *p = new lfd_lowpass_plan();
@@ -913,6 +941,8 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     bool any_block = false;
     for (int64_t j = ch.g0; j < ch.g1; ++j) {
       const int64_t pos = grid_lo[j];
+      if (n_off > 0 && (pos < ch.s0 || pos + n_off - 1 > ch.s1))
+        return bad(LFD_EUNSUPPORTED, "lattice one-pass: output offsets outside the chunk");
       if (pos < ch.s0 || pos > ch.s1 || (w0 != 0.0 && pos + 1 > ch.s1))
         return bad(LFD_EINVAL, "output grid point outside the chunk");
       const int64_t kj = (pos - base0) / L;
@@ -927,10 +957,15 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
         // unreachable: grid points are block starts and blocks start >= s0
         return bad(LFD_EINVAL, "internal: output grid point inside a chunk head");
       } else {
+        if (n_off > 0) return bad(LFD_EUNSUPPORTED, "lattice one-pass: an output in a chunk tail");
         G.tail_out_pos = pos;
         G.tail_out_j = j;
       }
     }
+    // (one-pass lattice) the output at block kb would need the FIR-history
+    // correction of every offset (CR holds offset 0's)
+    if (n_off > 0 && any_block && G.kout0 == G.kb)
+      return bad(LFD_EUNSUPPORTED, "lattice one-pass: an output in a chunk's first block");
     kmin = std::min(kmin, G.hskip ? G.kb - 1 : G.kb);
     kmax = std::max(kmax, G.ke);
     const int64_t nhead = G.head_end - G.s0, ntail = G.s1 + 1 - G.tail_begin;
@@ -961,8 +996,8 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
   }
   std::vector<long double> Kx;
   int nc = 0, row = 0;
-  if (2 * n + 1 <= 16) {
-    if (int e = block_taps(c, L, (R)w0, Kx, nc, row)) {
+  if (2 * n + (n_off > 0 ? n_off : 1) <= 16) {
+    if (int e = block_taps(c, L, (R)w0, Kx, nc, row, n_off)) {
       delete p;
       return e;
     }
@@ -976,6 +1011,12 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
       p->tg = lfd::TapGeom{Lp, J, nc, nvar, v0};
     }
   }
+  if (n_off > 0 && (p->taps.empty() ||
+                    sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 224) > (size_t)lfd::TAP_LDS_MAX)) {
+    delete p;
+    return fail(LFD_EUNSUPPORTED, "lattice one-pass: tap table does not fit LDS");
+  }
+  p->n_off = n_off;
   p->bg.n_sf = p->sf_blocks;
   // run mode: 4th-order cascades.  The MFMA K1 folds runs in registers when
   // its LDS holds the taps + 16 run buffers; otherwise (and for the recurrence
@@ -987,7 +1028,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     // (time, channel) rows: k_block_runs_mfma_tm reads each block row from
     // its first sample (no 16-B shift): one table, shift 0; its 512-thread
     // workgroup holds 8 waves x 2 channel tiles of run buffers
-    if (!p->taps.empty()) {
+    if (!p->taps.empty() && n_off == 0) {
       const int row = (int)(p->taps.size() / p->tg.nc);
       const int Lp_tm = (row + 63) / 64 * 64;
       if (sizeof(double) * ((size_t)Lp_tm * p->tg.nc + 64 + 8 * 2 * lfd::RUN_R * 5 * 16) <= (size_t)lfd::TAP_LDS_MAX)
@@ -999,6 +1040,10 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
       cuts.push_back(G.kb);
       if (G.kb + 1 < G.ke) cuts.push_back(G.kb + 1);
       cuts.push_back(G.ke);
+      // (one-pass lattice) every output block starts a run: K1 forms y0 of a
+      // run's first block only
+      if (n_off > 0)
+        for (int64_t k = G.kout0; k < G.kout1; k += kstep) cuts.push_back(k);
     }
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
@@ -1069,6 +1114,29 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     for (int i = 0; i < 4; ++i)
       for (int q = 0; q < lfd::HSKIP_MAX; ++q)
         p->rc.KfH[i][q] = (nc > i && q < row) ? (double)Kx[(size_t)i * row + q] : 0.0;
+    if (n_off > 0) {
+      // per offset d: the output's responses to the states (G0_d, H0_d) and
+      // the run constants built on them; H0_d also into the K1 constants
+      RModel m;
+      if (int e = make_rmodel(c, m)) {
+        delete p;
+        return e;
+      }
+      p->rc_off.resize(n_off);
+      for (int d = 0; d < n_off; ++d) {
+        lfd::ScanConst sd = p->sc;
+        for (int i = 0; i < n; ++i) {
+          R e[MAX_N] = {0};
+          e[i] = 1;
+          sd.G0[i] = (double)sim_block(m, L, e, nullptr, -1, 0, d).p0;
+          sd.H0[i] = (double)sim_block(m, L, nullptr, e, -1, 0, d).p0;
+          p->rc.H0L[d][i] = sd.H0[i];
+        }
+        run_constants(sd, p->rc_off[d]);
+        std::memcpy(p->rc_off[d].KfH, p->rc.KfH, sizeof(p->rc.KfH));
+      }
+      for (int d = 0; d < n_off; ++d) std::memcpy(p->rc_off[d].H0L, p->rc.H0L, sizeof(p->rc.H0L));
+    }
     p->run_ok = true;
   }
   // channel-group-major layouts (lfd_internal.h f_index / sf_index): channels
@@ -1079,7 +1147,7 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
   size_t end_F = align256(p->off_SF + sizeof(double) * (size_t)p->sf_blocks * n * ch64);
   if (p->run_ok) {  // run-mode buffers alias SF (unused in run mode); F stays for the fold
     p->off_Y0 = p->off_SF;
-    p->off_AG = align256(p->off_Y0 + sizeof(double) * (size_t)p->bg.nb * ch16);
+    p->off_AG = align256(p->off_Y0 + sizeof(double) * (size_t)p->bg.nb * ch16 * std::max(1, n_off));
     p->off_SR = align256(p->off_AG + sizeof(double) * (size_t)p->run_ks.size() * 8 * ch16);
     p->off_TR = align256(p->off_SR + sizeof(double) * (size_t)p->n_sr * 4 * ch64);
     p->off_CR = align256(p->off_TR + sizeof(double) * (size_t)p->n_sr * 4 * ch64);
@@ -1141,6 +1209,11 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     if (e == hipSuccess && !p->slot_chunk.empty())
       e = hipMemcpy(p->d_slot_chunk, p->slot_chunk.data(), sizeof(int) * p->slot_chunk.size(),
                     hipMemcpyHostToDevice);
+    if (e == hipSuccess && n_off > 0) {
+      e = hipMalloc(&p->d_rc_off, sizeof(lfd::RunConst) * n_off);
+      if (e == hipSuccess)
+        e = hipMemcpy(p->d_rc_off, p->rc_off.data(), sizeof(lfd::RunConst) * n_off, hipMemcpyHostToDevice);
+    }
   }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
   if (e != hipSuccess) {
@@ -1265,8 +1338,56 @@ static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int 
       bw.push_back(w[j]);
     }
   p->n_blend = (int64_t)bj.size();
+  // one-pass alternative: every phase from one K1 pass (MFMA rows 8 + d are
+  // the outputs at offset d from the lowest phase's lattice point, d < 8);
+  // when it does not apply (more than 8 phases, points at chunk edges,
+  // another cascade order) the per-phase sub-plans above run
+  std::vector<int64_t> bi_lat;
+  const int64_t dmin = ph.front().first, n_off = ph.back().first - dmin + 1;
+  if (n_off <= lfd::LAT_MAX_OFF && n_sec == 2 && !lfd::option(LFD_OPT_LATTICE_PHASES)) {
+    std::vector<int64_t> pos((size_t)n);
+    for (int64_t j = 0; j < n; ++j) pos[j] = lo[0] + j * R + dmin;
+    std::vector<double> zw((size_t)n, 0.0);
+    lfd_lowpass_plan *lat = nullptr;
+    const std::string err_keep = g_err;
+    if (plan_create_uniform(&lat, sos, n_sec, padlen, n_ch, n_t, pos.data(), zw.data(), n, chunks, n_chunks,
+                            (int)n_off) == LFD_OK) {
+      lat->chunks_off.resize((size_t)(n_off * n_chunks));
+      for (int64_t o = 0; o < n_off; ++o)
+        for (int64_t c = 0; c < n_chunks; ++c) {
+          const lfd::ChunkGeom &B = lat->chunks[c];
+          lfd::ChunkGeom G = B;
+          G.tail_out_j = -1;
+          G.tail_out_pos = -1;
+          int64_t a = INT64_MAX, b = INT64_MIN;
+          for (int64_t j = chunks[c].g0; j < chunks[c].g1; ++j)
+            if (phase(j) == dmin + o || (w[j] != 0.0 && phase(j) + 1 == dmin + o)) {
+              a = std::min(a, j);
+              b = std::max(b, j);
+            }
+          if (a <= b) {
+            G.kout0 = B.kout0 + (a - B.jout0) * B.kstep;
+            G.kout1 = B.kout0 + (b - B.jout0) * B.kstep + 1;
+            G.jout0 = a;
+          } else {
+            G.kout0 = G.kout1 = G.kb;
+            G.jout0 = 0;
+          }
+          lat->chunks_off[o * n_chunks + c] = G;
+        }
+      for (int64_t c = 0; c < n_chunks; ++c)
+        for (int64_t j = chunks[c].g0; j < chunks[c].g1; ++j) {
+          bi_lat.push_back((phase(j) - dmin) * n + j);
+          bi_lat.push_back(w[j] != 0.0 ? (phase(j) + 1 - dmin) * n + j : -1);
+        }
+      p->lat = lat;
+      ws_max = std::max(ws_max, lat->ws_bytes);
+    }
+    g_err = err_keep;
+  }
   p->off_tmp = align256(ws_max);
-  p->ws_bytes = align256(p->off_tmp + sizeof(float) * (size_t)n_ch * (size_t)p->comp_T);
+  p->ws_bytes = align256(p->off_tmp + sizeof(float) * (size_t)n_ch *
+                                          (size_t)std::max(p->comp_T, p->lat ? n_off * n : (int64_t)0));
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     (void)hipGetLastError();
@@ -1281,6 +1402,16 @@ static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int 
   if (e == hipSuccess && !bj.empty()) e = hipMemcpy(p->d_bj, bj.data(), sizeof(int64_t) * bj.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !bi.empty()) e = hipMemcpy(p->d_bi, bi.data(), sizeof(int64_t) * bi.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !bw.empty()) e = hipMemcpy(p->d_bw, bw.data(), sizeof(double) * bw.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && p->lat) {
+    lfd_lowpass_plan *lat = p->lat;
+    e = hipMalloc(&p->d_bi_lat, sizeof(int64_t) * std::max<size_t>(1, bi_lat.size()));
+    if (e == hipSuccess && !bi_lat.empty())
+      e = hipMemcpy(p->d_bi_lat, bi_lat.data(), sizeof(int64_t) * bi_lat.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&lat->d_chunks_off, sizeof(lfd::ChunkGeom) * lat->chunks_off.size());
+    if (e == hipSuccess)
+      e = hipMemcpy(lat->d_chunks_off, lat->chunks_off.data(), sizeof(lfd::ChunkGeom) * lat->chunks_off.size(),
+                    hipMemcpyHostToDevice);
+  }
   for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreate(&p->ev[i]);
   // (the sub-plans hold the chunk tables; d_chunks marks the plan executable)
   if (e == hipSuccess) e = hipMalloc(&p->d_chunks, sizeof(lfd::ChunkGeom));
@@ -1341,9 +1472,34 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     LFD_HIP(hipEventRecord(ev[0], st));
   }
   if (!p->subs.empty()) {
-    // lattice plan: the phase sub-plans into the scratch (ev[0] .. ev[1]),
-    // then the blend (ev[1] .. ev[2])
     float *tmp = reinterpret_cast<float *>(ws + p->off_tmp);
+    const lfd_lowpass_plan *L = p->lat;
+    p->last_onepass = L && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                      !lfd::option(LFD_OPT_LATTICE_PHASES);
+    if (p->last_onepass) {
+      // one pass: K1 with every phase's outputs (ev[0] .. ev[1]), then the
+      // state scan, the outputs per offset and the blend (ev[1] .. ev[2])
+      const lfd::RunGeom rg{(int64_t)L->run_ks.size(), (int64_t)L->group_r0.size() - 1, L->n_sr,
+                            L->d_run_ks, L->d_run_len, L->d_group_r0, L->d_rc};
+      double *Y0 = reinterpret_cast<double *>(ws + L->off_Y0);
+      double *AG = reinterpret_cast<double *>(ws + L->off_AG);
+      LFD_HIP(lfd::launch_block_runs_mfma_lat(x, s_ch, L->n_t, L->bg, L->d_taps, L->tg, rg, Y0, AG, st));
+      if (timed) LFD_HIP(hipEventRecord(ev[1], st));
+      const int64_t n_g = p->n_grid;
+      LFD_HIP(lfd::launch_lattice_scan(x, s_ch, s_t, L->bg, L->padlen, L->sc, rg, L->d_chunks, L->n_chunks, Y0, AG,
+                                       reinterpret_cast<double *>(ws + L->off_SR),
+                                       reinterpret_cast<double *>(ws + L->off_TP), L->tp_len,
+                                       reinterpret_cast<double *>(ws + L->off_TR),
+                                       reinterpret_cast<double *>(ws + L->off_CR), L->d_slot_chunk, L->n_off,
+                                       L->d_rc_off, L->d_chunks_off, tmp, L->n_off * n_g, n_g, st));
+      LFD_HIP(lfd::launch_blend_grid(tmp, L->n_off * n_g, p->n_ch, p->d_bj, p->d_bi_lat, p->d_bw, p->n_blend, y,
+                                     ys_ch, ys_t, st, gen));
+      if (timed) LFD_HIP(hipEventRecord(ev[2], st));
+      p->last_k1 = LFD_K1_MFMA_RUNS;
+      return LFD_OK;
+    }
+    // per-phase sub-plans into the scratch (ev[0] .. ev[1]), then the blend
+    // (ev[1] .. ev[2])
     for (size_t i = 0; i < p->subs.size(); ++i) {
       const int rc = lfd_lowpass_execute(p->subs[i], x, s_ch, s_t, tmp + p->sub_toff[i], p->comp_T, 1, workspace,
                                          stream);
@@ -1467,6 +1623,15 @@ int lfd_debug_block_taps(const lfd_lowpass_plan *p, double *taps, size_t n_taps,
   return LFD_OK;
 }
 
+int lfd_debug_lattice(const lfd_lowpass_plan *p, int64_t *n_offsets, int *last_onepass,
+                      const lfd_lowpass_plan **one_pass) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  if (n_offsets) *n_offsets = p->lat ? p->lat->n_off : 0;
+  if (last_onepass) *last_onepass = p->last_onepass ? 1 : 0;
+  if (one_pass) *one_pass = p->lat;
+  return LFD_OK;
+}
+
 int lfd_debug_runs(const lfd_lowpass_plan *p, int64_t *run_ks, int *run_len, int64_t max_runs,
                    int64_t *n_runs, void *run_const, size_t rc_bytes) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
@@ -1494,7 +1659,9 @@ int lfd_lowpass_last_kernel(const lfd_lowpass_plan *p) {
 void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   if (!p) return;
   for (auto *sp : p->subs) lfd_lowpass_plan_destroy(sp);
-  for (void *d : {(void *)p->d_bj, (void *)p->d_bi, (void *)p->d_bw})
+  if (p->lat) lfd_lowpass_plan_destroy(p->lat);
+  for (void *d : {(void *)p->d_bj, (void *)p->d_bi, (void *)p->d_bw, (void *)p->d_bi_lat, (void *)p->d_rc_off,
+                  (void *)p->d_chunks_off})
     if (d) (void)hipFree(d);
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);

@@ -180,7 +180,11 @@ struct RunConst {
   // scan head skip: e_f taps of a block row's first HSKIP_MAX samples
   // (Kx[c][p], c < 4: lfd_capi.cpp block_taps)
   double KfH[4][32];
+  // lattice one-pass plans (lfd_capi.cpp plan_create_uniform n_off > 0): H0
+  // of the outputs at offsets d = 0 .. LAT_MAX_OFF - 1 of a block
+  double H0L[8][4];
 };
+constexpr int LAT_MAX_OFF = 8;  // output offsets of a lattice one-pass K1 (MFMA rows 8 .. 15)
 constexpr int HSKIP_MAX = 32;
 struct RunGeom {
   int64_t n_runs, n_groups, n_sr;
@@ -279,6 +283,20 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
                                      double *AG, hipStream_t st);
 // Run epilogue applied to per-block functionals F (K1 kernels without run
 // mode): F -> Y0, AG (n_sec == 2).
+// Lattice one-pass K1 (tg.nc = 8 + n_off output offsets, every run's first
+// block an output block): per run, y0 of its first block at every offset
+// into Y0 + d * (ceil(n_ch / 16) * nb * 16), and the run aggregates.
+hipError_t launch_block_runs_mfma_lat(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+                                      const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
+                                      double *AG, hipStream_t st);
+// Lattice one-pass scan: the state scan once (deferred outputs: SR, TR, CR),
+// then k_run_outputs per offset d with RunConst rc_off[d], chunk outputs
+// cg_off[d * n_chunks ..] and Y0 slice d, into y + d * y_off.
+hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
+                               const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
+                               const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
+                               double *TR, double *CR, const int *slot_chunk, int n_off, const RunConst *rc_off,
+                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st);
 hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,
                             double *AG, hipStream_t st);
 // Run-mode scan.  With TR / CR / slot_chunk (per run slot: its chunk) the

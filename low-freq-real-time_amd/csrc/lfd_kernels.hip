@@ -3043,8 +3043,17 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 // table is loaded once per resident workgroup instead of once per 8 units.
 // The assignment is a pure function of the launch (no counter to reset), so
 // the kernel stays hipGraph-capturable.
+// LAT (lattice one-pass plans): tg.nc = 8 + n_off, MFMA rows 8 + d the
+// outputs at offset d of the block; every run's first block is an output
+// block (the plan cuts runs there), so only its y0 is formed, streamed like
+// SEPI: with v_p as above and S0 = 0 at the run start,
+//   y0_d(first) = p0_d + H0_d T1,  E_r = v_0 + PhiR T1,  T1 = sum_{p>=1} PhiR^(p-1) v_p.
+// Lane (q, col) holds offsets q (row 8 + q, acc[2]) and 4 + q (acc[3]).
+struct LatAcc {
+  double S0 = 0.0, T1 = 0.0, v0 = 0.0, ya = 0.0, yb = 0.0;
+};
 template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
-          bool PERSIST = false>
+          bool PERSIST = false, bool LAT = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -3056,12 +3065,17 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
   double *cst = Ks + ntab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4] (SEPI: + PhiR^p[8][16] + B[8][4])
   for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
-  if (SEPI) {
+  if (SEPI || LAT) {
     for (int i = threadIdx.x; i < RUN_R * 16; i += blockDim.x) cst[56 + i] = (&rg.rc->PhiRp[0][0])[i];
-    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x) cst[184 + i] = (&rg.rc->B[0][0])[i];
+    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x)
+      cst[184 + i] = LAT ? (&rg.rc->H0L[0][0])[i] : (&rg.rc->B[0][0])[i];
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int n_off = tg.nc - 2 * RUN_N;  // (LAT)
+  const int64_t y0_slice = ((g.n_ch + 15) / 16) * g.nb * 16;
+  (void)n_off;
+  (void)y0_slice;
   double *wb = Ks + ntab + RUN_CST + wave * RUN_WB;
   (void)wb;
   const int64_t n_cg = (g.n_ch + 15) / 16;
@@ -3127,9 +3141,60 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   int rlen = run_len_of(r);
   double S0 = 0.0;  // run prefix state, component q of channel col
   RunAccS ra;       // (SEPI)
+  LatAcc la;        // (LAT)
   auto block_done = [&](const d4v &a, int64_t k) {
     // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
     const int p = (int)(k - rks);
+    if constexpr (LAT) {
+      double sv[4];
+      row_gather4(la.S0, sv);
+      double v = a[1], sn = a[0];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v = fma(Mm[q * 4 + j], sv[j], v);
+        sn = fma(PhiF[q * 4 + j], sv[j], sn);
+      }
+      la.S0 = sn;
+      if (p == 0) {
+        la.ya = a[2];
+        la.yb = a[3];
+        la.v0 = v;
+        la.T1 = 0.0;
+      } else {
+        double vv[4];
+        row_gather4(v, vv);
+        const double *pr = cst + 56 + (p - 1) * 16 + q * 4;
+        double t1 = la.T1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t1 = fma(pr[j], vv[j], t1);
+        la.T1 = t1;
+      }
+      if (p + 1 == rlen) {
+        double tv[4];
+        row_gather4(la.T1, tv);
+        const double *ha = cst + 184 + q * 4, *hb = cst + 184 + (4 + q) * 4;
+        double ya = la.ya, yb = la.yb, er = la.v0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ya = fma(ha[j], tv[j], ya);
+          yb = fma(hb[j], tv[j], yb);
+          er = fma(PhiR[q * 4 + j], tv[j], er);
+        }
+        double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
+        if (q < n_off) y0o[q * y0_slice] = ya;
+        if (q + 4 < n_off) y0o[(q + 4) * y0_slice] = yb;
+        double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + col;
+        ag[q * 16] = la.S0;
+        ag[(4 + q) * 16] = er;
+        la = LatAcc{};
+        ++r;
+        if (r < r_end) {
+          rks = run_ks_of(r);
+          rlen = run_len_of(r);
+        }
+      }
+      return;
+    }
     if constexpr (SEPI) {
       const double a3[3] = {a[0], a[1], a[2]};
       run_block_stream(cst, q, p, a3, ra);
@@ -4013,15 +4078,15 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
 }
 
 template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
-          bool PERSIST = false>
+          bool PERSIST = false, bool LAT = false>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
-  // (MODE 4 diagnostic and SEPI: no run buffers)
-  const size_t lds = SEPI ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
+  // (MODE 4 diagnostic, SEPI and LAT: no run buffers)
+  const size_t lds = (SEPI || LAT) ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
                           : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  auto kern = &k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI, PERSIST>;
+  auto kern = &k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI, PERSIST, LAT>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -4153,6 +4218,15 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   // One unit per wave: persistent waves measured slower (diag LFD_K1_PERSIST)
   return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 #endif
+}
+
+hipError_t launch_block_runs_mfma_lat(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
+                                      const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
+                                      double *AG, hipStream_t st) {
+  if (tg.nc <= 2 * RUN_N || tg.nc > 2 * RUN_N + LAT_MAX_OFF || tg.Lp % 64 != 0 || rg.n_groups < 1)
+    return hipErrorInvalidValue;
+  const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
+  return run_k1<1, 0, 512, false, 4, false, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -4412,6 +4486,35 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   k_chunk_scan<2, true><<<nb, threads, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                             tp_len, y, ys_ch, ys_t, rg, Y0);
   return hipGetLastError();
+}
+
+hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
+                               const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
+                               const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
+                               double *TR, double *CR, const int *slot_chunk, int n_off, const RunConst *rc_off,
+                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st) {
+  if (n_off < 1 || n_off > LAT_MAX_OFF || !TR || !CR || !slot_chunk) return hipErrorInvalidValue;
+  const int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
+  const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
+  if (rg.n_sr >= 128 * n_chunks)
+    k_chunk_scan<2, true, true, 16, 8><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
+                                                            tp_len, y, ys_ch, 1, rg, Y0, TR, CR);
+  else
+    k_chunk_scan<2, true, true><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP, tp_len,
+                                                     y, ys_ch, 1, rg, Y0, TR, CR);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t waves = ((g.n_ch + 63) / 64) * rg.n_sr;
+  const int64_t slice = ((g.n_ch + 15) / 16) * g.nb * 16;
+  for (int d = 0; d < n_off; ++d) {
+    RunGeom rd = rg;
+    rd.rc = rc_off + d;
+    k_run_outputs<<<nblk(waves, 4), 256, 0, st>>>(g, cg_off + (int64_t)d * n_chunks, rd, slot_chunk, Y0 + d * slice,
+                                                  SR, TR, CR, y + d * y_off, ys_ch, 1);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch, int64_t s_t,

@@ -45,7 +45,7 @@ RUN_CONST_DTYPE = np.dtype([("PhiFp", "f8", (RUN_R + 1, 16)), ("PhiRp", "f8", (R
                             ("C", "f8", (RUN_R + 1, 16)), ("A", "f8", (RUN_R + 1, RUN_R, 4)),
                             ("B", "f8", (RUN_R, 4)), ("PhiF", "f8", 16), ("M", "f8", 16),
                             ("PhiR", "f8", 16), ("G0", "f8", 4), ("H0", "f8", 4),
-                            ("KfH", "f8", (4, 32))])
+                            ("KfH", "f8", (4, 32)), ("H0L", "f8", (8, 4))])
 
 
 class LFDLibraryError(RuntimeError):
@@ -160,6 +160,7 @@ def load():
         "lfd_stream_info": ([vp, P(i64), P(i64), P(i64)], i32),
         "lfd_stream_close": ([vp], None),
         "lfd_debug_stream_plans": ([vp, P(i64), P(i64)], i32),
+        "lfd_debug_lattice": ([vp, P(i64), P(i32), P(vp)], i32),
         "lfd_host_alloc": ([P(vp), sz], i32),
         "lfd_host_free": ([vp], None),
         "lfd_host_register": ([vp, sz], i32),
@@ -184,7 +185,7 @@ EXPORTED = (
     "lfd_lfproc_schedule", "lfd_stream_open", "lfd_stream_reserve", "lfd_stream_push", "lfd_stream_flush",
     "lfd_stream_last_output", "lfd_stream_last_chunks", "lfd_stream_fetch",
     "lfd_stream_synchronize", "lfd_stream_wait_copy", "lfd_stream_last_timing", "lfd_stream_info", "lfd_stream_close",
-    "lfd_debug_stream_plans",
+    "lfd_debug_stream_plans", "lfd_debug_lattice",
     "lfd_host_alloc", "lfd_host_free", "lfd_host_register", "lfd_host_unregister", "lfd_demean_scale_f64", "lfd_median_filter_f64",
 )
 
@@ -193,7 +194,7 @@ EXPORTED = (
 # library reads no environment variable; tests drive the fallback kernels
 # through these)
 OPTIONS = {"no_runs": 1, "k1_recurrence": 2, "tm_no_pairs": 3, "scan_defer": 4, "fullrate_serial": 5,
-           "no_lattice": 6, "no_head_skip": 7, "fir_valu": 8, "fullrate_bigblock": 9}
+           "no_lattice": 6, "no_head_skip": 7, "fir_valu": 8, "fullrate_bigblock": 9, "lattice_phases": 10}
 
 
 @contextlib.contextmanager

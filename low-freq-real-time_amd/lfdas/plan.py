@@ -87,7 +87,8 @@ class LowpassPlan:
 
     def close(self):
         if getattr(self, "_h", None):
-            self._lib.lfd_lowpass_plan_destroy(self._h)
+            if getattr(self, "_owned", True):
+                self._lib.lfd_lowpass_plan_destroy(self._h)
             self._h = None
 
     def __del__(self):  # pragma: no cover
@@ -167,6 +168,23 @@ class LowpassPlan:
         out = np.zeros((nc.value, row.value), np.float64)
         check(self._lib.lfd_debug_block_taps(self._h, out.ctypes.data, out.size, None, None))
         return out
+
+    def lattice(self):
+        """(n_offsets, whether the last execute ran the one-pass form, a view
+        of the one-pass inner plan or None) of a lattice plan — testing hook."""
+        n = ctypes.c_int64()
+        last = ctypes.c_int32()
+        inner = ctypes.c_void_p()
+        check(self._lib.lfd_debug_lattice(self._h, ctypes.byref(n), ctypes.byref(last), ctypes.byref(inner)))
+        view = None
+        if inner.value:
+            view = LowpassPlan.__new__(LowpassPlan)
+            view._lib = self._lib
+            view._h = inner
+            view._owned = False  # owned by this plan
+            view.chunks = self.chunks
+            view.n_ch, view.n_t = self.n_ch, self.n_t
+        return int(n.value), bool(last.value), view
 
     def constants(self):
         """(BlockConst, ScanConst, ChunkGeom[]) numpy records — testing hook."""

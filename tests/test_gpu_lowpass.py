@@ -43,6 +43,7 @@ def _run(x, fs, dt_out, P, B, layout="tc", off_ns=0):
     plan.execute(xd, yd, plan.alloc_workspace())
     torch.cuda.synchronize()
     _run.last_kernel = plan.last_kernel()
+    _run.lattice = plan.lattice()[:2]
     y = yd.cpu().numpy()
     ref = oracle.lfproc_process(x, t0, dt_ns, tg[0], tg[-1] + 1, dt_out, P, B)
     _run.w = w
@@ -81,15 +82,18 @@ def test_lfproc_parity(cfg, dc, layout, off_ns):
     assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
+@pytest.mark.parametrize("phases", [False, True])
 @pytest.mark.parametrize("layout,off_ns,null", [("tc", 0, False), ("tc", 123_457, False), ("cc", 123_457, False),
                                                 ("tc", 0, True)])
-def test_lfproc_parity_lattice_grid(layout, off_ns, null):
+def test_lfproc_parity_lattice_grid(layout, off_ns, null, phases):
     """3 kHz data on integer-ns sample times (333,333 ns): the 1 s output grid
     drifts against the samples, so the fraction w varies from point to point
     and the spacing is 3,000 or 3,001 samples.  The plan decomposes the grid
-    into lattice phases (one uniform block sub-plan per phase, then the
-    interp1d blend) and still runs the block-plan kernels; outputs match the
-    oracle (relRMS 1e-4) with identical shapes."""
+    into lattice phases and still runs the block-plan kernels: for
+    (channel, time) rows one K1 pass forms every phase's outputs (MFMA rows
+    8 + d, the one-pass form), otherwise (time-major rows, or option
+    lattice_phases) one uniform block sub-plan per phase; then the interp1d
+    blend.  Outputs match the oracle (relRMS 1e-4) with identical shapes."""
     fs, dt_out, P, B, n_ch, dur = 3000.0, 1.0, 120, 7, 20, 1300.0
     n = int(dur * fs)
     rng = np.random.default_rng(5)
@@ -97,7 +101,10 @@ def test_lfproc_parity_lattice_grid(layout, off_ns, null):
     x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.02 * t) + 50.0).astype(np.float32)
     if null:  # a NaN in one channel: NaN in every output of the chunks holding it
         x[3, n // 2] = np.nan
-    y, ref, sched = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
+    with kernel_options(lattice_phases=1 if phases else 0):
+        y, ref, sched = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
+    assert _run.lattice == ((0 if phases else _run.lattice[0]), layout == "tc" and not phases)
+    assert phases or 2 <= _run.lattice[0] <= 8
     w = _run.w
     assert len(np.unique(w)) > 100  # a varying fraction
     num = den = 0.0

@@ -176,6 +176,68 @@ def test_lattice_plan_3khz_grid_host_only():
     plan.close()
 
 
+def _r_model(sos):
+    """Realization R of the cascade (lfd_internal.h RCoef): FIR c (c[0] = 1),
+    gain G, all-pole sections (a1, a2)."""
+    num = np.array([1.0])
+    for s in sos:
+        num = np.convolve(num, s[:3])
+    return num / num[0], num[0], [(s[4], s[5]) for s in sos]
+
+
+def _allpole(secs, w):
+    v = np.array(w, dtype=np.float64)
+    for a1, a2 in secs:
+        out = np.zeros_like(v)
+        p1 = p2 = 0.0
+        for i, u in enumerate(v):
+            o = u - a1 * p1 - a2 * p2
+            p2, p1 = p1, o
+            out[i] = o
+        v = out
+    return v
+
+
+def test_lattice_onepass_plan_host_math():
+    """The lattice plan's one-pass form (3 kHz on integer-ns times): the
+    output rows 8 + d of its block taps are the zero-boundary zero-phase
+    output at offset d of a block (forward all-pole from zero state with the
+    block's true FIR history, reverse from zero state at the block end),
+    every output block starts a run, and each offset's chunk outputs cover
+    the points that need that phase."""
+    plan, sched, tg = _plan_for(3000.0, 1.0, 120, 7, 8, 3000 * 1300)
+    n_off, last, view = plan.lattice()
+    assert 2 <= n_off <= 8 and not last and view is not None
+    Kx = view.block_taps()
+    L, J = view.block_len if hasattr(view, "block_len") else 500, 4
+    assert Kx.shape == (8 + n_off, L + J)
+    c, G, secs = _r_model(plan.sos)
+    rng = np.random.default_rng(11)
+    xe = rng.standard_normal(L + J)
+    w = np.array([np.dot(c, xe[J + t - np.arange(J + 1)]) for t in range(L)])
+    yf = G * _allpole(secs, w)
+    ql = _allpole(secs, yf[::-1])[::-1]
+    for d in range(n_off):
+        ref = G * np.dot(c, ql[d:d + J + 1])
+        got = Kx[8 + d] @ xe
+        assert abs(got - ref) <= 1e-10 * max(1.0, abs(ref)), (d, got, ref)
+    ks, ln, rc = view.runs()
+    _, _, cg = view.constants()
+    starts = set(ks.tolist())
+    for G_ in cg:
+        for k in range(G_["kout0"], G_["kout1"], G_["kstep"]):
+            assert k in starts
+        assert G_["tail_out_j"] < 0 and (G_["kout1"] == G_["kout0"] or G_["kout0"] > G_["kb"])
+    # H0 of offset 0 is the plan's own H0; later offsets differ
+    np.testing.assert_allclose(rc["H0L"][0], rc["H0"], rtol=1e-13)
+    assert not np.allclose(rc["H0L"][1], rc["H0"])
+    plan.close()
+    with _lib.kernel_options(lattice_phases=1):
+        plan2, _, _ = _plan_for(3000.0, 1.0, 120, 7, 8, 3000 * 1300)
+        assert plan2.lattice()[0] == 0
+        plan2.close()
+
+
 @pytest.mark.parametrize("name", ["lfproc_cfg1.npz", "lfproc_cfg5_slice.npz"])
 def test_plan_constants_reproduce_golden(name):
     """Host-only plan → NumPy model of the kernels → SciPy golden vectors."""
