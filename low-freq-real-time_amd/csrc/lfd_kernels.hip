@@ -1057,15 +1057,13 @@ __device__ __forceinline__ double dpp_row_d(double v) {
   return __hiloint2double(h2, l2);
 }
 
-// MB (medium-block states, OUT only): SF / ST hold the states at EVERY
-// medium block (FR_LB = 16 sub-blocks: one 16-lane row), so the wave scans
-// run inside the rows on DPP lane moves (row_shr / row_shl: VALU, no LDS
-// round trips) with 4 log-steps instead of 6 ds_bpermute steps over the wave.
-template <int NS, bool OUT, bool MB = false>
+// (big-block path, option fullrate_bigblock; the medium-block output pass
+// is k_fullrate_out_mb)
+template <int NS, bool OUT>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t nb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
-    double *__restrict__ F, double *__restrict__ y, int64_t ys_ch, int64_t ys_t, int64_t n_mb) {
+    double *__restrict__ F, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L;
   static_assert(LS == 32, "tile reads assume 32-sample sub-blocks");
   constexpr int TLDS = L + 4 * (L / 32);
@@ -1079,18 +1077,12 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   const int col = lane & 15, q = lane >> 4;
   const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
   const int64_t a = k * L;
-  // (MB) the last big block may hold fewer than 4 medium blocks: samples
-  // past them are not loaded (zeros; their rows' outputs are not stored)
-  const int nvs = MB ? (int)(n_mb - 4 * k < 4 ? (n_mb - 4 * k) * FR_LB : L) : L;
   {
     // every load of the big block issued before the first LDS write (8 KB
     // per wave in flight, one memory latency per block); time-contiguous,
     // 16-B aligned rows as float4 (1 KB per instruction)
     const float *row = x + ch * s_ch + a * s_t;
-    if (MB && nvs < L) {
-#pragma unroll 8
-      for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = u < nvs ? row[u] : 0.0f;
-    } else if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !LFD_DG(g_fr_stage_old)) {
+    if (s_t == 1 && (reinterpret_cast<uintptr_t>(row) & 15) == 0 && !LFD_DG(g_fr_stage_old)) {
       float4 v[L / 256];
 #pragma unroll
       for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
@@ -1108,46 +1100,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
   FwdRec<NS> fr;
   fr.load(fc->cf);
   double r0[OUT ? LS : 1], A[N], Z[N];
-  float xs_mb[MB ? LS : 1];
-  if constexpr (MB) {
-    // (A_j, Z0_j) = KAZ x_j on the matrix cores (as the functionals pass);
-    // the zero-state responses r0 are formed after the scans, so they are
-    // not held in registers across them
-    fr_d4v acc[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
-    const float *tb = tile + 36 * col + q;
-#pragma unroll
-    for (int ks = 0; ks < LS / 4; ++ks) {
-      const double av = fc->KAZ[ks][lane];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[36 * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
-    }
-    // the lane's own 32 samples into registers (for r0 after the scans),
-    // then the exchange through the tile's LDS
-    const float *tr = tile + 36 * lane;
-#pragma unroll
-    for (int g = 0; g < LS / 4; ++g) {
-      const float4 v = *reinterpret_cast<const float4 *>(tr + 4 * g);
-      xs_mb[4 * g + 0] = v.x;
-      xs_mb[4 * g + 1] = v.y;
-      xs_mb[4 * g + 2] = v.z;
-      xs_mb[4 * g + 3] = v.w;
-    }
-    __syncthreads();
-    double *az = lds;  // [sub-block][functional], stride OSTR
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) az[(16 * nt + col) * OSTR + q + 4 * r] = acc[nt][r];
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-      A[n] = az[lane * OSTR + n];
-      Z[n] = az[lane * OSTR + N + n];
-    }
-  } else if constexpr (OUT) {
+  if constexpr (OUT) {
     // ---- 1, 2. zero-state forward, then zero-state reverse over its output
     float xs[LS];
     const float *tr = tile + 36 * lane;
@@ -1205,73 +1158,6 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_wave(
       v[r] = acc;
     }
   };
-  if constexpr (MB) {
-    // ---- 3, 4 inside the rows: row r = medium block m = 4k + r, lane jr its
-    // 32-sample sub-block; S entering the row SF[m], T entering it ST[m + 1]
-    const int jr = lane & 15;
-    const int64_t m_row = 4 * k + (lane >> 4);
-    const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
-    double Sin[N], Tin[N], vf[N];
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-      Sin[n] = SF[(m * N + n) * n_ch + ch];
-      vf[n] = A[n];
-    }
-    if (jr == 0) matvec_add(fc->PhiP[0], Sin, vf, true);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double o[N];
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        if (i == 0) o[n] = dpp_row_d<0x111>(vf[n]);
-        if (i == 1) o[n] = dpp_row_d<0x112>(vf[n]);
-        if (i == 2) o[n] = dpp_row_d<0x114>(vf[n]);
-        if (i == 3) o[n] = dpp_row_d<0x118>(vf[n]);
-      }
-      matvec_add(fc->PhiP[i], o, vf, true);  // lanes without a source add PhiP 0
-    }
-    double Sj[N], vb[N];
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-      const double u = dpp_row_d<0x111>(vf[n]);
-      Sj[n] = jr == 0 ? Sin[n] : u;
-      vb[n] = Z[n];
-    }
-    matvec_add(fc->M32, Sj, vb, false);
-#pragma unroll
-    for (int n = 0; n < N; ++n) Tin[n] = ST[((m + 1) * N + n) * n_ch + ch];
-    if (jr == 15) matvec_add(fc->PhiP[0], Tin, vb, true);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double o[N];
-#pragma unroll
-      for (int n = 0; n < N; ++n) {
-        if (i == 0) o[n] = dpp_row_d<0x101>(vb[n]);
-        if (i == 1) o[n] = dpp_row_d<0x102>(vb[n]);
-        if (i == 2) o[n] = dpp_row_d<0x104>(vb[n]);
-        if (i == 3) o[n] = dpp_row_d<0x108>(vb[n]);
-      }
-      matvec_add(fc->PhiP[i], o, vb, true);
-    }
-    double T[N];
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-      const double u = dpp_row_d<0x101>(vb[n]);
-      T[n] = jr == 15 ? Tin[n] : u;
-    }
-    {
-      // ---- zero-state forward, then zero-state reverse over its output
-      double zf[N], zr[N];
-#pragma unroll
-      for (int n = 0; n < N; ++n) zf[n] = zr[n] = 0.0;
-#pragma unroll
-      for (int i = 0; i < LS; ++i) r0[i] = fr.step(zf, (double)xs_mb[i]);
-#pragma unroll
-      for (int i = LS - 1; i >= 0; --i) r0[i] = fr.step(zr, r0[i]);
-    }
-    fr_out_mfma<NS>(lane, fc, Sj, T, r0, lds, y + ch * ys_ch + a * ys_t, ys_t, nvs / LS);
-    return;
-  }
   // ---- 3. forward wave scan
   double Sin[N], vf[N], Sj[N];
 #pragma unroll
@@ -4551,16 +4437,15 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
     if (stage_old) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stage_old), &stage_old, sizeof(int));
   }
 #endif
-#define LFD_FR(NS, OUT, MB)                                                                            \
-  k_fullrate_wave<NS, OUT, MB><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, \
-                                                             ys_t, n_mb)
+#define LFD_FR(NS, OUT) \
+  k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, ys_t)
 #define LFD_FR2(NS)   \
   if (out && mb)      \
     k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out)       \
-    LFD_FR(NS, true, false); \
+    LFD_FR(NS, true); \
   else                \
-    LFD_FR(NS, false, false)
+    LFD_FR(NS, false)
   switch (n_sec) {
     case 1: LFD_FR2(1); break;
     case 2: LFD_FR2(2); break;

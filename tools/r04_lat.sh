@@ -10,3 +10,7 @@ for e in "" "LFD_FULLRATE_BIGBLOCK=1"; do
 done
 echo "== lattice"; timeout -k 10 200 python tools/lattice_bench.py > gpurun_out/${tag}_lattice.txt 2>&1 || { tail -20 gpurun_out/${tag}_lattice.txt; exit 1; }
 cat gpurun_out/${tag}_lattice.txt
+for c in 1250 2500; do
+  echo "== narrow shard $c"; timeout -k 10 240 python tools/ab_plan.py --ch $c --replan --reps 3 "" "LFD_RUN_UNIT=8" "LFD_RUN_TAIL=0" "LFD_RUN_UNIT=8 LFD_RUN_TAIL=4" > gpurun_out/${tag}_ab_narrow_$c.txt 2>&1 || { tail -20 gpurun_out/${tag}_ab_narrow_$c.txt; exit 1; }
+  tail -6 gpurun_out/${tag}_ab_narrow_$c.txt
+done
