@@ -1259,7 +1259,9 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
 //      staged through the tile's LDS into rows and stored as 16-B pieces.
 // The round-3 output pass ran the zero-state responses as TDF-II recurrences
 // (40 fp64 FMAs per sample on the VALU: the pass was fp64-issue bound).
-template <int NS>
+// DIRECT (diag A/B): y stored straight from the MFMA layout (32-B pieces per
+// lane quad, 4 instructions per 128-B line) instead of through the LDS stage
+template <int NS, bool DIRECT = false>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
@@ -1425,10 +1427,24 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       for (int nt = 0; nt < 4; ++nt) yacc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bx[nt], yacc[mt][nt], 0, 0, 0);
     }
   }
-  __syncthreads();  // the tile's reads are done: its LDS becomes the output stage
-  double *ob = lds;
   double *yr = y + ch * ys_ch + a * ys_t;
   const int nsb = nvs / LS;
+  if constexpr (DIRECT) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int sb = 16 * nt + col;
+        if (sb < nsb) {
+          double *o = yr + (int64_t)(sb * LS + 16 * mt + q) * ys_t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[4 * r * ys_t] = yacc[mt][nt][r];
+        }
+      }
+    return;
+  }
+  __syncthreads();  // the tile's reads are done: its LDS becomes the output stage
+  double *ob = lds;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     // yacc[mt][nt][r] = y[sample 16 mt + q + 4 r] of sub-block 16 nt + col
@@ -4439,8 +4455,15 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
 #endif
 #define LFD_FR(NS, OUT) \
   k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, ys_t)
+#ifdef LFD_DIAG
+  static const bool fr_direct = knob_flag("LFD_FR_OUT_DIRECT");
+#else
+  constexpr bool fr_direct = false;
+#endif
 #define LFD_FR2(NS)   \
-  if (out && mb)      \
+  if (out && mb && fr_direct)      \
+    k_fullrate_out_mb<NS, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
+  else if (out && mb)      \
     k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out)       \
     LFD_FR(NS, true); \
