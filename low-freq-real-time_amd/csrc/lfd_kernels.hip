@@ -1261,14 +1261,30 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
 // (40 fp64 FMAs per sample on the VALU: the pass was fp64-issue bound).
 // DIRECT (diag A/B): y stored straight from the MFMA layout (32-B pieces per
 // lane quad, 4 instructions per 128-B line) instead of through the LDS stage
-template <int NS, bool DIRECT = false>
+// LAY: 1 (production) = tile rows 36 floats apart written as 16-B pieces,
+// row reads pairing rows r and r + 1; 0 (diag A/B) = the bank-conflict-free
+// layout below (tile rows 34 floats apart, 8-B staging writes, r / r + 8 row
+// reads): 2.5x fewer SQ_LDS_BANK_CONFLICT cycles (1.9e8 -> 7.5e7 per call)
+// but 1 % slower on the same box (4.19 vs 4.14 ms; the pass is matrix-core
+// bound, profiles/r04h_fr_ab_lds_layout.txt); 2 (diag) = the 36-float tile
+// with the r / r + 8 row reads (4.17 ms)
+template <int NS, bool DIRECT = false, int LAY = 1>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
     double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L, K = 2 * N, KS = K / 4, OSTR = 18;
   static_assert(N % 2 == 0 && K % 4 == 0, "state components in groups of 4");
-  constexpr int TLDS = L + 4 * (L / 32);
+  // LDS banks (gfx950: 32 banks for 4-B accesses, 64 for 8 / 16 B): the
+  // tile's sub-block rows are TS = 34 floats apart, so the MFMA B reads (lane
+  // (q, col) reads row col + q: 2 col + q mod 32) are conflict-free, and
+  // each 8-B staging write pairs rows i and i + 16 (34 x 16 = 32 mod 64);
+  // the output stage's rows are OSTR = 18 doubles apart (MFMA-layout 8-B
+  // writes: 36 col + 2 q distinct mod 64 per half wave) and each 16-B row
+  // read pairs rows r and r + 8 (36 x 8 = 32 mod 64)
+  constexpr bool T36 = LAY != 0;
+  constexpr int TS = T36 ? 36 : 34;
+  constexpr int TLDS = 64 * TS;
   constexpr int NLDS = 64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2;
   __shared__ __attribute__((aligned(16))) double lds[NLDS];
   float *tile = reinterpret_cast<float *>(lds);
@@ -1281,8 +1297,8 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *row = x + ch * s_ch + a;
     if (nvs < L) {
 #pragma unroll 8
-      for (int u = lane; u < L; u += 64) tile[u + 4 * (u >> 5)] = u < nvs ? row[u] : 0.0f;
-    } else {
+      for (int u = lane; u < L; u += 64) tile[(u >> 5) * TS + (u & 31)] = u < nvs ? row[u] : 0.0f;
+    } else if constexpr (T36) {
       float4 v[L / 256];
 #pragma unroll
       for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
@@ -1291,10 +1307,19 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
         const int u = 4 * lane + 256 * i;
         *reinterpret_cast<float4 *>(tile + u + 4 * (u >> 5)) = v[i];
       }
+    } else {
+      // instruction i: lane quarter g = lane >> 4 reads sub-block 16 g + i
+      // (4 x 128-B pieces), 2 samples per lane
+      const int g = lane >> 4, e2 = 2 * (lane & 15);
+      float2 v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const float2 *>(row + (16 * g + i) * LS + e2);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) *reinterpret_cast<float2 *>(tile + (16 * g + i) * TS + e2) = v[i];
     }
   }
   __syncthreads();
-  const float *tb = tile + 36 * col + q;  // B[k = q][j = col] of tile nt, k-step ks: tb[36*16*nt + 4*ks]
+  const float *tb = tile + TS * col + q;  // B[k = q][j = col] of tile nt, k-step ks: tb[TS*16*nt + 4*ks]
   // ---- 1. sub-block exits on the matrix cores
   double A[N], Z[N];
   {
@@ -1306,7 +1331,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       const double av = fc->KAZ[ks][lane];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[36 * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[TS * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
     }
     // acc[nt][r] at row q = functional q + 4r of sub-block 16 nt + col: per r,
     // transpose (row q <-> register nt) -> at row R, register q' = functional
@@ -1419,7 +1444,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
   for (int ks = 0; ks < LS / 4; ++ks) {
     double bx[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bx[nt] = (double)tb[36 * 16 * nt + 4 * ks];
+    for (int nt = 0; nt < 4; ++nt) bx[nt] = (double)tb[TS * 16 * nt + 4 * ks];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const double av = fc->KRA[mt][ks][lane];
@@ -1460,7 +1485,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     if (ys_t == 1 && (reinterpret_cast<uintptr_t>(yr) & 15) == 0) {
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
-        const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
+        const int r = LAY == 1 ? it * 8 + (lane >> 3) : it + 8 * (lane >> 3), c2 = 2 * (lane & 7);
         if (r < nsb)
           *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
       }
@@ -4457,12 +4482,18 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
   k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, ys_t)
 #ifdef LFD_DIAG
   static const bool fr_direct = knob_flag("LFD_FR_OUT_DIRECT");
+  static const int fr_lay = knob("LFD_FR_LAYOUT") ? std::atoi(knob("LFD_FR_LAYOUT")) : 1;
 #else
   constexpr bool fr_direct = false;
+  constexpr int fr_lay = 1;
 #endif
 #define LFD_FR2(NS)   \
   if (out && mb && fr_direct)      \
     k_fullrate_out_mb<NS, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
+  else if (out && mb && fr_lay == 0)      \
+    k_fullrate_out_mb<NS, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
+  else if (out && mb && fr_lay == 2)      \
+    k_fullrate_out_mb<NS, false, 2><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out && mb)      \
     k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out)       \
