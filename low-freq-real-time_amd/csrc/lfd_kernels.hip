@@ -519,9 +519,17 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // instead of 64 scattered 4-B stores (0.2 ms of the cfg3 scan)
   __shared__ float outs[RUNS ? 4 : 1][64][RUN_R + 1];
   if constexpr (RUNS) {
+    // the fields this scan reads: PhiFp, PhiRp, C (+ A, B for in-chain
+    // outputs) and KfH — not the whole 12 KB RunConst (a 64-thread group of
+    // a narrow shard loaded 24 doubles per thread before its first step)
     const double *src = &rg.rc->PhiFp[0][0];
     double *dst = &rcs[0].PhiFp[0][0];
-    for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
+    constexpr int n_head = (int)((offsetof(RunConst, A) - offsetof(RunConst, PhiFp)) / sizeof(double));
+    constexpr int n_ab = (int)((offsetof(RunConst, PhiF) - offsetof(RunConst, A)) / sizeof(double));
+    constexpr int o_kfh = (int)((offsetof(RunConst, KfH) - offsetof(RunConst, PhiFp)) / sizeof(double));
+    constexpr int n_copy = n_head + (DEFER ? 0 : n_ab);
+    for (int i = threadIdx.x; i < n_copy; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 4 * HSKIP_MAX; i += blockDim.x) dst[o_kfh + i] = src[o_kfh + i];
     __syncthreads();
   }
   // whole wave active and inside one chunk: outputs leave through LDS (above)
@@ -4169,12 +4177,14 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
                                                      const double *__restrict__ TR, const double *__restrict__ CR,
                                                      float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = RUN_N;
-  __shared__ RunConst rcs[1];
+  // only the output constants A[len][p], B[d] (2.5 KB; the whole RunConst
+  // is 12 KB, and a 1,250-channel shard launches ~2,200 of these groups)
+  __shared__ double sA[RUN_R + 1][RUN_R][4], sB[RUN_R][4];
   __shared__ float outs[4][64][RUN_R + 1];
   {
-    const double *src = &rg.rc->PhiFp[0][0];
-    double *dst = &rcs[0].PhiFp[0][0];
-    for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x) dst[i] = src[i];
+    const double *srcA = &rg.rc->A[0][0][0], *srcB = &rg.rc->B[0][0];
+    for (int i = threadIdx.x; i < (RUN_R + 1) * RUN_R * 4; i += blockDim.x) (&sA[0][0][0])[i] = srcA[i];
+    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x) (&sB[0][0])[i] = srcB[i];
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
@@ -4205,7 +4215,6 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
   }
   const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
   const double cr = CR[c * (n_c64 * 64) + chc];
-  const RunConst &rc = rcs[0];
   float ov[RUN_R];
 #pragma unroll
   for (int pp = 0; pp < RUN_R; ++pp) {
@@ -4213,8 +4222,8 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
     ov[pp] = 0.f;
     if (pp >= len || !is_out(k)) continue;
     double acc = y0b[k * 16] + (k == G.kb ? cr : 0.0);
-    const double *A = rc.A[len][pp];
-    const double *B = rc.B[len - 1 - pp];
+    const double *A = sA[len][pp];
+    const double *B = sB[len - 1 - pp];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       acc = fma(A[i], sin[i], acc);
@@ -4368,6 +4377,20 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   // option LFD_OPT_SCAN_DEFER = 1 / 2 forces in-chain / deferred outputs
   bool defer = n_chunks * g.n_ch < 40000 || rg.n_sr >= 128 * n_chunks;
   if (const int64_t o = option(LFD_OPT_SCAN_DEFER)) defer = o == 2;
+#ifdef LFD_DIAG
+  static int diag = -1, threads_ab = 256;
+  if (diag < 0) {
+    const char *v = knob("LFD_SCAN_DIAG");
+    diag = v ? std::atoi(v) : 0;
+    if (diag) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_scan_diag), &diag, sizeof(int));
+    // workgroup size A/B knob (64, 128 or 256 threads; the kernel's LDS
+    // staging is per wave and its launch bound is 256)
+    if (const char *t = knob("LFD_SCAN_THREADS")) {
+      const int w = std::atoi(t);
+      if (w == 64 || w == 128 || w == 256) threads_ab = w;
+    }
+  }
+#endif
   if (TR && CR && slot_chunk && defer) {
     // narrow shards: 64-thread workgroups (one wave per CU instead of four
     // sharing one): 1,250 channels 0.150 -> 0.126 ms, bit-identical
@@ -4375,11 +4398,12 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
     if (const char *tv = knob("LFD_SCAN_DEFER_THREADS")) dthr = std::atoi(tv) == 64 ? 64 : (std::atoi(tv) == 128 ? 128 : 256);
     const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
-    // long run chains (>= 128 runs per chunk) keep 16 / 8 runs in flight
-    // instead of 4 / 2: dt = 10 s at 1 kHz 0.401 -> 0.352 ms, bit-identical;
-    // narrow shards measure the same either way (profiles/r03_ab_scan_deep.txt;
-    // A/B knob LFD_SCAN_DEEP=0/1)
-    bool deep = rg.n_sr >= 128 * n_chunks;
+    // 16 / 8 runs in flight instead of 4 / 2: dt = 10 s at 1 kHz 0.401 ->
+    // 0.352 ms (profiles/r03_ab_scan_deep.txt); the 1,250- / 2,500-channel
+    // shards' scan kernel 90.6 -> 74.4 / 99.6 -> 78.3 us by rocprofv3 kernel
+    // trace (profiles/r04l_scan_deep.txt); bit-identical (A/B knob
+    // LFD_SCAN_DEEP=0/1)
+    bool deep = true;
     if (const char *dv = knob("LFD_SCAN_DEEP")) deep = std::atoi(dv) != 0;
     if (deep)
       k_chunk_scan<2, true, true, 16, 8><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
@@ -4395,18 +4419,6 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   }
   int threads = 256;
 #ifdef LFD_DIAG
-  static int diag = -1, threads_ab = 256;
-  if (diag < 0) {
-    const char *v = knob("LFD_SCAN_DIAG");
-    diag = v ? std::atoi(v) : 0;
-    if (diag) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_scan_diag), &diag, sizeof(int));
-    // workgroup size A/B knob (64, 128 or 256 threads; the kernel's LDS
-    // staging is per wave and its launch bound is 256)
-    if (const char *t = knob("LFD_SCAN_THREADS")) {
-      const int w = std::atoi(t);
-      if (w == 64 || w == 128 || w == 256) threads_ab = w;
-    }
-  }
   threads = threads_ab;
 #endif
   const unsigned nb = nblk(n_chunks * g.n_ch, threads);
