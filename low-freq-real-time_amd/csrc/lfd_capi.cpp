@@ -795,7 +795,7 @@ struct lfd_lowpass_plan {
   int64_t *d_bj = nullptr, *d_bi = nullptr;  // grid index; scratch index of y[lo], y[lo + 1] (-1: w == 0)
   double *d_bw = nullptr;
   // one-pass alternative (channel-major, 16-B aligned rows): one lattice plan
-  // for every phase (n_off offsets), scratch [n_ch][n_off * n_grid]
+  // for every phase (n_off offsets), slot-major scratch [n_off * n_grid][n_ch]
   lfd_lowpass_plan *lat = nullptr;
   int64_t *d_bi_lat = nullptr;
   size_t off_tmp_lat = 0;
@@ -1492,8 +1492,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
                                        reinterpret_cast<double *>(ws + L->off_TR),
                                        reinterpret_cast<double *>(ws + L->off_CR), L->d_slot_chunk, L->n_off,
                                        L->d_rc_off, L->d_chunks_off, tmp, L->n_off * n_g, n_g, st));
-      LFD_HIP(lfd::launch_blend_grid(tmp, L->n_off * n_g, p->n_ch, p->d_bj, p->d_bi_lat, p->d_bw, p->n_blend, y,
-                                     ys_ch, ys_t, st, gen));
+      LFD_HIP(lfd::launch_blend_grid_sm(tmp, p->n_ch, p->d_bj, p->d_bi_lat, p->d_bw, p->n_blend, y, ys_ch, ys_t, st,
+                                        gen));
       if (timed) LFD_HIP(hipEventRecord(ev[2], st));
       p->last_k1 = LFD_K1_MFMA_RUNS;
       return LFD_OK;

@@ -290,8 +290,9 @@ hipError_t launch_block_runs_mfma_lat(const float *x, int64_t s_ch, int64_t n_t,
                                       const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
                                       double *AG, hipStream_t st);
 // Lattice one-pass scan: the state scan once (deferred outputs: SR, TR, CR),
-// then k_run_outputs per offset d with RunConst rc_off[d], chunk outputs
-// cg_off[d * n_chunks ..] and Y0 slice d, into y + d * y_off.
+// then k_lat_outputs: every offset d (RunConst rc_off[d], chunk outputs
+// cg_off[d * n_chunks ..], Y0 slice d) into the slot-major scratch
+// y[(d * y_off + j) * n_ch + ch] (y_off = grid points per offset; ys_ch unused).
 hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
                                const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
@@ -345,6 +346,11 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
 struct GridGen {
   int64_t rel0 = 0, step = 0, dts = 0;
 };
+// the same blend from a slot-major scratch tmp[slot * n_ch + ch] (one-pass
+// lattice plans), LDS-tiled so that reads and writes are both coalesced
+hipError_t launch_blend_grid_sm(const float *tmp, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                                const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+                                const GridGen &gen);
 hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
                              const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
                              const GridGen &gen = GridGen{});

@@ -4427,6 +4427,117 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// k_lat_outputs — the one-pass lattice plan's outputs, every offset in one
+// launch: one wave = 64 channels x one run slot; the run's entering states
+// (S_in, T_in) are loaded once and its first block (every output block starts
+// a run) gives y = y0_d + A_d[len][0] S_in + B_d[len-1] T_in for each offset
+// d whose points include that block, into a slot-major scratch
+// tmp[(d n_g + j) n_ch + ch] (64 consecutive channels per store).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_lat_outputs(BlockGeom g, const ChunkGeom *__restrict__ cg_off, int64_t n_chunks,
+                                                     int n_off, RunGeom rg, const int *__restrict__ slot_chunk,
+                                                     const RunConst *__restrict__ rc_off, const double *__restrict__ Y0,
+                                                     const double *__restrict__ SR, const double *__restrict__ TR,
+                                                     float *__restrict__ tmp, int64_t n_g) {
+  constexpr int N = RUN_N;
+  __shared__ double sA[LAT_MAX_OFF][RUN_R + 1][4], sB[LAT_MAX_OFF][RUN_R + 1][4];
+  for (int i = threadIdx.x; i < n_off * (RUN_R + 1) * 4; i += blockDim.x) {
+    const int d = i / ((RUN_R + 1) * 4), rem = i - d * (RUN_R + 1) * 4, len = rem >> 2, e = rem & 3;
+    sA[d][len][e] = rc_off[d].A[len][0][e];
+    sB[d][len][e] = len >= 1 ? rc_off[d].B[len - 1][e] : 0.0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t n_c64 = (g.n_ch + 63) / 64;
+  const int64_t w = uniform64((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (w >= n_c64 * rg.n_sr) return;
+  const int64_t c64 = w % n_c64, j = w / n_c64;
+  const int64_t ch = c64 * 64 + lane;
+  const bool valid = ch < g.n_ch;
+  const int64_t chc = valid ? ch : g.n_ch - 1;
+  const int c = __builtin_amdgcn_readfirstlane(slot_chunk[j]);
+  const ChunkGeom &G0 = cg_off[c];
+  const int64_t r = G0.r0 + (j - G0.sr_off);
+  const int64_t ks = rg.run_ks[r];
+  const int len = rg.run_len[r];
+  double sin[N], tin[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    sin[i] = SR[sf_index(j, i, chc, rg.n_sr, N)];
+    tin[i] = TR[sf_index(j, i, chc, rg.n_sr, N)];
+  }
+  const int64_t slice = ((g.n_ch + 15) / 16) * g.nb * 16;
+  const double *y0b = Y0 + ((chc >> 4) * g.nb + ks) * 16 + (chc & 15);
+  for (int d = 0; d < n_off; ++d) {
+    const ChunkGeom &G = cg_off[(int64_t)d * n_chunks + c];
+    const int64_t kst = G.kstep;
+    if (ks < G.kout0 || ks >= G.kout1 || (ks - G.kout0) % kst != 0) continue;
+    const int64_t jo = G.jout0 + (ks - G.kout0) / kst;
+    double acc = y0b[d * slice];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      acc = fma(sA[d][len][i], sin[i], acc);
+      acc = fma(sB[d][len][i], tin[i], acc);
+    }
+    if (valid) tmp[((int64_t)d * n_g + jo) * g.n_ch + ch] = (float)acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_blend_grid_sm — the interp1d blend from the slot-major scratch: a
+// workgroup = 64 blend points x 64 channels; reads of tmp rows (64 channels)
+// and writes of y rows (64 points) both coalesced through an LDS tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_blend_grid_sm(const float *__restrict__ tmp, int64_t n_ch,
+                                                       const int64_t *__restrict__ bj, const int64_t *__restrict__ bi,
+                                                       const double *__restrict__ bw, int64_t nb, float *__restrict__ y,
+                                                       int64_t ys_ch, int64_t ys_t, GridGen gen) {
+  __shared__ float tile[64][65];
+  const int64_t i0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int ii = ty; ii < 64; ii += 4) {
+    const int64_t i = i0 + ii, ch = c0 + tx;
+    float v = 0.f;
+    if (i < nb && ch < n_ch) {
+      const int64_t ia = bi[2 * i], ib = bi[2 * i + 1];
+      double a = (double)tmp[ia * n_ch + ch];
+      if (ib >= 0) {
+        double wv;
+        if (gen.dts > 0) {
+          const int64_t rel = gen.rel0 + bj[i] * gen.step;
+          int64_t lo = rel / gen.dts;
+          if (rel % gen.dts != 0 && rel < 0) --lo;
+          wv = (double)(rel - lo * gen.dts) / (double)gen.dts;
+        } else {
+          wv = bw[i];
+        }
+        a = fma(wv, (double)tmp[ib * n_ch + ch] - a, a);
+      }
+      v = (float)a;
+    }
+    tile[ii][tx] = v;
+  }
+  __syncthreads();
+  const int64_t i = i0 + tx;
+  if (i >= nb) return;
+  const int64_t jj = bj[i];
+  for (int cc = ty; cc < 64; cc += 4) {
+    const int64_t ch = c0 + cc;
+    if (ch < n_ch) y[ch * ys_ch + jj * ys_t] = tile[tx][cc];
+  }
+}
+
+hipError_t launch_blend_grid_sm(const float *tmp, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                                const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+                                const GridGen &gen) {
+  if (nb <= 0 || n_ch <= 0) return hipSuccess;
+  if ((n_ch + 63) / 64 > 65535) return hipErrorInvalidValue;
+  dim3 grid((unsigned)((nb + 63) / 64), (unsigned)((n_ch + 63) / 64));
+  k_blend_grid_sm<<<grid, 256, 0, st>>>(tmp, n_ch, bj, bi, bw, nb, y, ys_ch, ys_t, gen);
+  return hipGetLastError();
+}
+
 hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
                                const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
@@ -4444,16 +4555,10 @@ hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int64_t waves = ((g.n_ch + 63) / 64) * rg.n_sr;
-  const int64_t slice = ((g.n_ch + 15) / 16) * g.nb * 16;
-  for (int d = 0; d < n_off; ++d) {
-    RunGeom rd = rg;
-    rd.rc = rc_off + d;
-    k_run_outputs<<<nblk(waves, 4), 256, 0, st>>>(g, cg_off + (int64_t)d * n_chunks, rd, slot_chunk, Y0 + d * slice,
-                                                  SR, TR, CR, y + d * y_off, ys_ch, 1);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  (void)ys_ch;
+  k_lat_outputs<<<nblk(waves, 4), 256, 0, st>>>(g, cg_off, n_chunks, n_off, rg, slot_chunk, rc_off, Y0, SR, TR, y,
+                                                y_off);
+  return hipGetLastError();
 }
 
 hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch, int64_t s_t,
