@@ -3510,9 +3510,11 @@ __device__ __forceinline__ void tm_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t 
 // a wave issued no loads.  Registers allow 2 waves per SIMD (8 per CU: the
 // occupancy at which this access shape streams fastest,
 // profiles/r03_ubench_tm.txt).
+// TMW (diag A/B): minimum waves per SIMD for the register allocation (0: 4
+// for one tile, 2 with SEPI, else 1)
 template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false, bool BUF = false,
-          int MODE = 0, bool SEPI = false>
-__global__ __launch_bounds__(NT, NTILE == 1 ? 4 : (SEPI ? 2 : 1)) void k_block_runs_mfma_tm(
+          int MODE = 0, bool SEPI = false, int TMW = 0>
+__global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1))) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
   extern __shared__ double Ks[];
@@ -3869,6 +3871,16 @@ hipError_t launch_block_runs_mfma_tm_ab(const float *x, int64_t s_t, int64_t n_t
       lds = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
       // (LFD_TM_M4=1: v_mfma_f64_4x4x4 steps, a third less matrix-core issue time)
       if (m4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true, true, 0, true>, 512);
+      // production: 256-thread groups, registers for 2 waves per SIMD;
+      // LFD_TM_W=512: the 512-thread groups of round 3; =3: 256 threads,
+      // registers for 3 waves per SIMD (spills); =21: 128-thread groups
+      // (profiles/r04q_ab_tm_w.txt)
+      if (const char *wv = knob("LFD_TM_W")) {
+        if (std::atoi(wv) == 3) return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 3>, 256);
+        if (std::atoi(wv) == 21) return go(&k_block_runs_mfma_tm<1, 128, false, 2, true, false, true, 0, true, 2>, 128);
+        if (std::atoi(wv) == 512) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
+      }
+      if (pfb == 1) return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 2>, 256);
       if (pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 0, true>, 512);
       return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
     }
@@ -3908,13 +3920,14 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || tg.nvar != 1 || tg.v0 != 0 || rg.n_groups < 1)
     return hipErrorInvalidValue;
   const size_t tab = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST);
-  auto go = [&](auto kern, size_t lds) -> hipError_t {
+  auto go = [&](auto kern, size_t lds, int nt) -> hipError_t {
     if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
     if (e != hipSuccess) return e;
     const int64_t units = ((g.n_ch + 31) / 32) * rg.n_groups;  // two 16-channel tiles per wave
-    kern<<<(unsigned)((units + 7) / 8), 512, lds, st>>>(x, s_t, n_t, g, taps, tg, rg, Y0, AG);
+    const int w = nt / 64;
+    kern<<<(unsigned)((units + w - 1) / w), nt, lds, st>>>(x, s_t, n_t, g, taps, tg, rg, Y0, AG);
     return hipGetLastError();
   };
   // channel-pair loads need 8-B aligned pairs (even n_ch and row stride)
@@ -3923,12 +3936,15 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   if (x2 && s_t < (int64_t)1 << 22)
     // buffer loads at prefetch depth 1 (14.01 vs 14.18 ms) with the streaming
     // run epilogue, taps + constants only in LDS (13.85 vs 14.35 ms) on cfg3
-    // stored time-major (profiles/r03_ab_tm_sepi.txt)
-    return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>,
-              sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S));
+    // stored time-major (profiles/r03_ab_tm_sepi.txt); 256-thread groups (4
+    // per CU, registers for 2 waves per SIMD as before): 13.06 vs 13.50 ms
+    // median against 512-thread groups, bit-identical; 128-thread groups 15.03
+    // (profiles/r04q_ab_tm_w.txt)
+    return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 2>,
+              sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S), 256);
   const size_t lds = tab + sizeof(double) * 8 * 2 * RUN_WB;  // + 8 waves x 2 tiles of run buffers
-  if (x2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, lds);
-  return go(&k_block_runs_mfma_tm<2, 512, false>, lds);
+  if (x2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, lds, 512);
+  return go(&k_block_runs_mfma_tm<2, 512, false>, lds, 512);
 #endif
 }
 
@@ -4112,6 +4128,15 @@ hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, 
       const char *pv = knob("LFD_K1_PERSIST");
       if (pv && std::atoi(pv) != 0)
         return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+      // LFD_K1_WG=256: 256-thread groups with the streaming epilogue (taps +
+      // constants only in LDS: 4 groups / 16 waves per CU); =2561: the same
+      // with the LDS run buffers (57 KB: 2 groups / 8 waves per CU)
+      if (const char *wv = knob("LFD_K1_WG")) {
+        if (std::atoi(wv) == 256)
+          return run_k1<1, 0, 256, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+        if (std::atoi(wv) == 2561)
+          return run_k1<1, 0, 256, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+      }
       return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
     }
     return hipErrorInvalidValue;
