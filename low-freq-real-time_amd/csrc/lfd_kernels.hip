@@ -3996,11 +3996,38 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   int pf = 2, mode = 0;
   if (const char *v = knob("LFD_MF_PF")) pf = std::atoi(v);
   if (const char *v = knob("LFD_MF_MODE")) mode = std::atoi(v);  // diagnostics (results invalid)
-  // blocks per wave: MF_RUN when the array is wide; narrow arrays (the
-  // real-time edge runs: 2,000 channels, 44 blocks of 2,000 samples) get
-  // fewer so that >= ~4,096 waves (16 per CU) cover the chip
+  // blocks per wave: narrow arrays (the real-time edge runs: 2,000
+  // channels, 44 blocks of 2,000 samples) get fewer so that >= ~4,096 waves
+  // (16 per CU) cover the chip; within that, the largest count whose units
+  // fill their last round of wave slots to >= 95 % (every wave streams at
+  // about the same rate, so a last round of 13 % of the slots costs nearly a
+  // full round: the full-rate functionals of 2,000 x 600,000 ran 4,625 units
+  // of 32 blocks = 1.13 rounds; 12 blocks make 2.99 rounds)
   const int64_t n_cg = (g.n_ch + 15) / 16;
-  int bpw = (int)std::max<int64_t>(1, std::min<int64_t>(MF_RUN, n_cg * g.nb / 4096));
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
+      n_cu = 256;
+    slots = 16 * n_cu;
+  }
+  const int bmax = (int)std::max<int64_t>(1, std::min<int64_t>(MF_RUN, n_cg * g.nb / slots));
+  int bpw = bmax;
+  {
+    double best = -1.0;
+    for (int b = bmax; b >= 1; --b) {
+      const double rounds = (double)(n_cg * ((g.nb + b - 1) / b)) / slots;
+      const double eff = rounds / std::ceil(rounds);
+      if (eff >= 0.95) {
+        bpw = b;
+        break;
+      }
+      if (eff > best + 1e-9) {
+        best = eff;
+        bpw = b;
+      }
+    }
+  }
   if (const char *v = knob("LFD_MF_BPW")) bpw = std::max(1, std::min(MF_RUN, std::atoi(v)));
   const int64_t n_runs = (g.nb + bpw - 1) / bpw;
   const int64_t units = n_cg * n_runs;
