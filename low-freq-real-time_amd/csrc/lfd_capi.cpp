@@ -430,10 +430,23 @@ std::vector<double> fullrate_medium_taps(const Cascade &cs) {
 // Segment plan of k_fullrate_scan_seg for M medium blocks: G segments of
 // seglen blocks (Gu non-empty), PhiB^seglen and PhiB^lastlen in extended
 // precision.
-lfd::FRSeg fullrate_segments(const Cascade &cs, int64_t M) {
+// Segments of the full-rate scan: 16 channels x <= 32 segments per
+// workgroup, or, when the 16-channel groups would leave CUs idle (2,000
+// channels = 125 groups on 256 CUs), 8 channels x <= 64 segments (twice the
+// workgroups, half the chain per thread); >= 4 medium blocks per segment.
+lfd::FRSeg fullrate_segments(const Cascade &cs, int64_t M, int64_t n_ch) {
   lfd::FRSeg sg{};
   const int n = 2 * cs.ns;
-  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(32, M / 4));
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n_cu < 1)
+      n_cu = 256;
+  }
+  sg.cw = (n_ch + 15) / 16 < n_cu ? 8 : 16;
+  if (const char *v = lfd::knob("LFD_FR_SEG_CW")) sg.cw = std::atoi(v) == 8 ? 8 : 16;  // (diag A/B)
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(512 / sg.cw, M / 4));
   sg.seglen = (int)((M + G - 1) / G);
   sg.Gu = (int)((M + sg.seglen - 1) / sg.seglen);
   sg.G = (int)G;
@@ -1849,7 +1862,7 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
       const lfd::TapGeom tg{lfd::FR_LB, 0, 2 * n, 1, 0};
       LFD_HIP(lfd::launch_block_functionals_mfma(x, s_ch, n_t, g, fe->d_ktaps, tg, F, st));
       if (timed) LFD_HIP(hipEventRecord(g_fr_ev[1], st));
-      const lfd::FRSeg sg = fullrate_segments(c, M);
+      const lfd::FRSeg sg = fullrate_segments(c, M, n_ch);
       LFD_HIP(lfd::launch_fullrate_scan_seg(n_sec, x, s_ch, s_t, n_ch, n_t, M, padlen, fe->d_fc, F, SF, ST, TP, y,
                                             ys_ch, ys_t, sg, st));
     } else {

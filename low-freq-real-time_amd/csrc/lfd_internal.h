@@ -250,14 +250,15 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
                                   hipStream_t st, bool mb = false, int64_t n_mb = 0);
 // Segmented scan over the medium blocks (FR_LB) of the matrix-core
 // functionals F2 (f_index layout, nF = 2N over 4 nb blocks): a workgroup =
-// 16 channels x G segments of `seglen` medium blocks; per segment a zero-state
+// cw channels (16, or 8 when fewer 16-channel groups than CUs) x G <= 512 / cw
+// segments of `seglen` medium blocks; per segment a zero-state
 // aggregate, a combine across the segments (powers pseg = PhiB^seglen, plast
 // = PhiB^lastlen), the true states; forward then reverse.  Writes SFm / STm
 // (the states at every medium block: the output pass's inputs), TP and the
 // tail outputs, like k_fullrate_scan.
 struct FRSeg {
   double pseg[MAX_N * MAX_N], plast[MAX_N * MAX_N];
-  int seglen, lastlen, G, Gu;
+  int seglen, lastlen, G, Gu, cw;
 };
 hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
                                     int64_t M, int padlen, const FRConst *fc, const double *F2, double *SFm,

@@ -1683,7 +1683,7 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
 // The output pass (k_fullrate_wave<NS, true, true>) reads SFm / STm per row.
 // 16 x G threads per channel group instead of one thread per channel walking
 // every block: the walks are G times shorter (latency-bound chains).
-template <int NS>
+template <int NS, int CW = 16>
 __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t M, int padlen,
     const FRConst *__restrict__ fc, const double *__restrict__ F2, double *__restrict__ SFm,
@@ -1691,9 +1691,10 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     FRSeg sg) {
   constexpr int N = 2 * NS;
   __shared__ double cPB[N * N], cMB[N * N], cPS[N * N], cPT[N * N];
-  __shared__ double slotL[16][N], slotR[16][N];
-  extern __shared__ double agg[];  // [G][16][N]
-  const int tid = threadIdx.x, col = tid & 15, seg = tid >> 4;
+  static_assert(CW == 16 || CW == 8, "16 or 8 channels per workgroup");
+  __shared__ double slotL[CW][N], slotR[CW][N];
+  extern __shared__ double agg[];  // [G][CW][N]
+  const int tid = threadIdx.x, col = tid % CW, seg = tid / CW;
   for (int i = tid; i < N * N; i += blockDim.x) {
     const int r = i / N, c = i % N;
     cPB[i] = fc->PhiP[4][r * MAX_N + c];
@@ -1702,7 +1703,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     cPT[i] = sg.plast[r * MAX_N + c];
   }
   __syncthreads();
-  const int64_t ch = (int64_t)blockIdx.x * 16 + col;
+  const int64_t ch = (int64_t)blockIdx.x * CW + col;
   const bool active = ch < n_ch;
   const int64_t m0 = (int64_t)seg * sg.seglen;
   const int64_t m1 = m0 + sg.seglen < M ? m0 + sg.seglen : M;
@@ -1722,7 +1723,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
       o[r] = acc;
     }
   };
-  double *ag = agg + ((size_t)seg * 16 + col) * N;
+  double *ag = agg + ((size_t)seg * CW + col) * N;
   // Every walk loads QF (forward) / QR (reverse) blocks before applying them,
   // at clamped indices (unconditional loads: a conditional load made the
   // compiler wait for everything in flight), so the chain waits one memory
@@ -1771,7 +1772,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
   for (int n = 0; n < N; ++n) z[n] = slotL[col][n];
   for (int sp = 0; sp < seg && sp < sg.Gu; ++sp) {
     double o[N];
-    const double *as = agg + ((size_t)sp * 16 + col) * N;
+    const double *as = agg + ((size_t)sp * CW + col) * N;
 #pragma unroll
     for (int n = 0; n < N; ++n) o[n] = as[n];
     mv(cPS, z, o, true);
@@ -1871,7 +1872,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
   for (int n = 0; n < N; ++n) z[n] = slotR[col][n];
   for (int sp = sg.Gu - 1; sp > seg; --sp) {
     double o[N];
-    const double *as = agg + ((size_t)sp * 16 + col) * N;
+    const double *as = agg + ((size_t)sp * CW + col) * N;
 #pragma unroll
     for (int n = 0; n < N; ++n) o[n] = as[n];
     mv(sp == sg.Gu - 1 ? cPT : cPS, z, o, true);
@@ -4703,23 +4704,33 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
                                     int64_t M, int padlen, const FRConst *fc, const double *F2, double *SFm,
                                     double *STm, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
                                     const FRSeg &sg, hipStream_t st) {
-  if (sg.G < 1 || sg.G > 32 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 || M < 1) return hipErrorInvalidValue;
-  const unsigned g = nblk(n_ch, 16);
-  const size_t lds = sizeof(double) * (size_t)sg.G * 16 * 2 * n_sec;
+  if ((sg.cw != 16 && sg.cw != 8) || sg.G < 1 || sg.G * sg.cw > 512 || sg.Gu < 1 || sg.Gu > sg.G || sg.seglen < 1 ||
+      M < 1)
+    return hipErrorInvalidValue;
+  const unsigned g = nblk(n_ch, sg.cw);
+  const size_t lds = sizeof(double) * (size_t)sg.G * sg.cw * 2 * n_sec;
   static bool attr = false;  // (dynamic LDS above 64 KB with the static part)
   if (!attr) {
     for (const void *fn : {reinterpret_cast<const void *>(&k_fullrate_scan_seg<1>),
                            reinterpret_cast<const void *>(&k_fullrate_scan_seg<2>),
                            reinterpret_cast<const void *>(&k_fullrate_scan_seg<3>),
-                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<4>)}) {
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<4>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<1, 8>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<2, 8>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<3, 8>),
+                           reinterpret_cast<const void *>(&k_fullrate_scan_seg<4, 8>)}) {
       const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
       if (e != hipSuccess) return e;
     }
     attr = true;
   }
-#define LFD_FRSS(NS) \
-  k_fullrate_scan_seg<NS><<<g, 16 * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, M, padlen, fc, F2, SFm, STm, TP, y, \
-                                                    ys_ch, ys_t, sg)
+#define LFD_FRSS(NS)                                                                                               \
+  if (sg.cw == 8)                                                                                                  \
+    k_fullrate_scan_seg<NS, 8><<<g, sg.cw * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, M, padlen, fc, F2, SFm, STm, \
+                                                            TP, y, ys_ch, ys_t, sg);                               \
+  else                                                                                                             \
+    k_fullrate_scan_seg<NS><<<g, sg.cw * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, M, padlen, fc, F2, SFm, STm, TP,  \
+                                                         y, ys_ch, ys_t, sg)
   switch (n_sec) {
     case 1: LFD_FRSS(1); break;
     case 2: LFD_FRSS(2); break;
