@@ -431,20 +431,14 @@ std::vector<double> fullrate_medium_taps(const Cascade &cs) {
 // seglen blocks (Gu non-empty), PhiB^seglen and PhiB^lastlen in extended
 // precision.
 // Segments of the full-rate scan: 16 channels x <= 32 segments per
-// workgroup, or, when the 16-channel groups would leave CUs idle (2,000
-// channels = 125 groups on 256 CUs), 8 channels x <= 64 segments (twice the
-// workgroups, half the chain per thread); >= 4 medium blocks per segment.
+// workgroup, >= 4 medium blocks per segment.  (8 channels x <= 64 segments,
+// twice the workgroups for 2,000 channels = 125 groups on 256 CUs, measured
+// 0.49 vs 0.48 ms: the diag A/B LFD_FR_SEG_CW=8, profiles/r04s_fr_seg_cw.txt.)
 lfd::FRSeg fullrate_segments(const Cascade &cs, int64_t M, int64_t n_ch) {
   lfd::FRSeg sg{};
   const int n = 2 * cs.ns;
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || n_cu < 1)
-      n_cu = 256;
-  }
-  sg.cw = (n_ch + 15) / 16 < n_cu ? 8 : 16;
+  (void)n_ch;
+  sg.cw = 16;
   if (const char *v = lfd::knob("LFD_FR_SEG_CW")) sg.cw = std::atoi(v) == 8 ? 8 : 16;  // (diag A/B)
   const int64_t G = std::max<int64_t>(1, std::min<int64_t>(512 / sg.cw, M / 4));
   sg.seglen = (int)((M + G - 1) / G);
