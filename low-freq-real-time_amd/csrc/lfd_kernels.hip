@@ -1253,6 +1253,45 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
   swap16_d(v2, v3);
 }
 
+// One 16x16x4 fp64 MFMA step as four v_mfma_f64_4x4x4_4b (M4): the same
+// 1,024 MACs at 4 x 18.5 instead of ~109 cycles per SIMD with dense A
+// operands (tools/ubench_mfma64b.hip, profiles/r02_ubench_mfma64b.txt).  The
+// 4x4x4_4b lane layout (A[i][k] at lane 16k + 4b + i, B[k][j] at 16k + 4b + j,
+// D[i][j] at 16i + 4b + j; tools/check_mfma4x4.hip) makes B the 16x16x4 B
+// register unchanged and D[r] the 16x16x4 accumulator's row q + 4r when A is
+// the 16x16x4 A register with quad r of every 16-lane row broadcast to its
+// four quads: ds_swizzle bit-mask mode (and 0x13, or 4r: lane bits 0, 1, 4
+// kept, bits 2, 3 = r), a lane crossbar with no memory access.
+template <int FG>
+__device__ __forceinline__ double quad_bcast(double v) {
+  constexpr int pat = 0x13 | ((FG << 2) << 5);
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+  return __hiloint2double(hi, lo);
+}
+// one k-step of A (this lane's 16x16x4 A value) against four column tiles
+// (one broadcast variant live at a time)
+template <bool M4>
+__device__ __forceinline__ void mfma_k4(double av, const double (&b)[4], fr_d4v (&acc)[4]) {
+  if constexpr (M4) {
+    const double a0 = quad_bcast<0>(av);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, b[nt], acc[nt][0], 0, 0, 0);
+    const double a1 = quad_bcast<1>(av);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, b[nt], acc[nt][1], 0, 0, 0);
+    const double a2 = quad_bcast<2>(av);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, b[nt], acc[nt][2], 0, 0, 0);
+    const double a3 = quad_bcast<3>(av);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt][3] = __builtin_amdgcn_mfma_f64_4x4x4f64(a3, b[nt], acc[nt][3], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[nt], acc[nt], 0, 0, 0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_fullrate_out_mb — output pass of the medium-block full-rate path, with no
 // fp64 recurrence at all: one wave = one big block (FR_L samples, the last
@@ -1276,7 +1315,8 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
 // but 1 % slower on the same box (4.19 vs 4.14 ms; the pass is matrix-core
 // bound, profiles/r04h_fr_ab_lds_layout.txt); 2 (diag) = the 36-float tile
 // with the r / r + 8 row reads (4.17 ms)
-template <int NS, bool DIRECT = false, int LAY = 1>
+// M4: every product as 4x4x4_4b steps (mfma16x4)
+template <int NS, bool DIRECT = false, int LAY = 1, bool M4 = false>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
@@ -1337,9 +1377,10 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
 #pragma unroll
     for (int ks = 0; ks < LS / 4; ++ks) {
       const double av = fc->KAZ[ks][lane];
+      double bk[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, (double)tb[TS * 16 * nt + 4 * ks], acc[nt], 0, 0, 0);
+      for (int nt = 0; nt < 4; ++nt) bk[nt] = (double)tb[TS * 16 * nt + 4 * ks];
+      mfma_k4<M4>(av, bk, acc);
     }
     // acc[nt][r] at row q = functional q + 4r of sub-block 16 nt + col: per r,
     // transpose (row q <-> register nt) -> at row R, register q' = functional
@@ -1442,10 +1483,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     rows_transpose4(bop[0], bop[1], bop[2], bop[3]);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      const double av = fc->QA[mt][ks][lane];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        yacc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bop[nt], yacc[mt][nt], 0, 0, 0);
+      mfma_k4<M4>(fc->QA[mt][ks][lane], bop, yacc[mt]);
     }
   }
 #pragma unroll
@@ -1455,9 +1493,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     for (int nt = 0; nt < 4; ++nt) bx[nt] = (double)tb[TS * 16 * nt + 4 * ks];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      const double av = fc->KRA[mt][ks][lane];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) yacc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bx[nt], yacc[mt][nt], 0, 0, 0);
+      mfma_k4<M4>(fc->KRA[mt][ks][lane], bx, yacc[mt]);
     }
   }
   double *yr = y + ch * ys_ch + a * ys_t;
@@ -4653,12 +4689,16 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
 #ifdef LFD_DIAG
   static const bool fr_direct = knob_flag("LFD_FR_OUT_DIRECT");
   static const int fr_lay = knob("LFD_FR_LAYOUT") ? std::atoi(knob("LFD_FR_LAYOUT")) : 1;
+  static const bool fr_m4 = knob_flag("LFD_FR_M4");
 #else
   constexpr bool fr_direct = false;
   constexpr int fr_lay = 1;
+  constexpr bool fr_m4 = false;
 #endif
 #define LFD_FR2(NS)   \
-  if (out && mb && fr_direct)      \
+  if (out && mb && fr_m4)      \
+    k_fullrate_out_mb<NS, false, 1, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
+  else if (out && mb && fr_direct)      \
     k_fullrate_out_mb<NS, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out && mb && fr_lay == 0)      \
     k_fullrate_out_mb<NS, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
