@@ -67,17 +67,71 @@ case "$1" in
       echo "== $e"; env $e timeout -k 10 120 python tools/fr_bench.py || exit 1
     done &&
     bash tools/pmc_kernel.sh fr fullrate tools/fr_one.py 2 ;;
-  lattice)  # lattice plan vs the per-chunk general path at 3 kHz
+  lattice)  # lattice plan: one pass vs the per-phase sub-plans at 3 kHz
+            # (profiles/r04d_lattice_onepass_vs_phases.txt, r04n_lattice_fused_outputs.txt)
     timeout -k 10 300 python tools/lattice_bench.py ;;
   multi)    # N > 1 launcher on a 1-GPU box: refusal, then the one-device rehearsal
     timeout -k 10 120 python bench.py --gpus 2 --steps 1; echo "bench --gpus 2 exit $? (want 2)"
     timeout -k 10 300 python bench.py --gpus 2 --one-device --steps 2 --warmup 1 --no-cpu --no-rolling \
         --no-extra --no-stream ;;
   # ---- round 4
-  persist)  # persistent run-mode K1 (units pulled from a counter) vs one unit per wave, by shard width
+  persist)  # persistent run-mode K1 (static unit assignment) vs one unit per wave, by shard width
+            # (profiles/r04_ab_k1_persist_*.txt)
     for ch in 1250 2500 5000 10000; do
-      timeout -k 10 300 python tools/ab_plan.py --ch $ch --reps 4 --steps 5 "" "LFD_K1_PERSIST=0" || exit 1
+      timeout -k 10 300 python tools/ab_plan.py --ch $ch --reps 4 --steps 5 "" "LFD_K1_PERSIST=1" || exit 1
     done ;;
+  narrow_units) # K1 unit size / tail rounds at 1,250 and 2,500 channels (profiles/r04d_ab_narrow_units.txt)
+    for c in 1250 2500; do
+      timeout -k 10 240 python tools/ab_plan.py --ch $c --replan --reps 3 "" "LFD_RUN_UNIT=8" "LFD_RUN_TAIL=0" \
+          "LFD_RUN_UNIT=8 LFD_RUN_TAIL=4" || exit 1
+    done ;;
+  scan_trace) # narrow-shard scan phases (diag) and kernel times, deep vs 4 / 2 ring
+              # (profiles/r04l_scan_deep.txt)
+    timeout -k 10 350 python tools/probe_scan.py narrow || exit 1
+    cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+    for e in "" "LFD_SCAN_DEEP=0"; do
+      for c in 1250 2500; do
+        d=gpurun_out/scan_trace_${c}_${e:-default}
+        env $e timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $d -o tr -- python3 tools/scan_one.py $c \
+            > $d.log 2>&1 || exit 1
+        echo "== $c ${e:-default}"; grep -h "chunk_scan\|run_outputs\|runs_mfma" $d/*/tr_kernel_stats.csv $d/tr_kernel_stats.csv 2>/dev/null
+      done
+    done ;;
+  fr_mb)    # full-rate: medium-block path vs the big-block path (profiles/r04d_fr_ab_mfma_output_vs_bigblock.txt)
+    for e in "" "LFD_FULLRATE_BIGBLOCK=1"; do
+      echo "== $e"; env $e timeout -k 10 120 python tools/fr_bench.py || exit 1
+    done ;;
+  fr_out)   # full-rate output pass variants: direct stores, LDS layouts, 4x4x4 steps
+            # (profiles/r04e_fr_ab_direct_stores.txt, r04h_fr_ab_lds_layout.txt, r04t_fr_ab_mfma4x4.txt)
+    for e in "" "LFD_FR_OUT_DIRECT=1" "LFD_FR_LAYOUT=0" "LFD_FR_LAYOUT=2" "LFD_FR_M4=1" \
+             "LFD_MF_BPW=32" "LFD_FR_SEG_CW=8"; do
+      echo "== $e"; env $e timeout -k 10 120 python tools/fr_bench.py || exit 1
+    done ;;
+  fr_pmc)   # PMC of the medium-block full-rate kernels (profiles/r04_pmc_fullrate.txt)
+    bash tools/pmc_fullrate.sh r04fr ;;
+  lattice_pmc) # PMC of the lattice one-pass line (profiles/r04_pmc_lattice.txt)
+    bash tools/pmc_kernel.sh r04lat "k_block_runs_mfma|k_chunk_scan|k_lat_outputs|k_blend_grid" tools/lattice_one.py 2 ;;
+  tm_wg)    # time-major K1 workgroup size / waves per SIMD (profiles/r04q_ab_tm_w.txt)
+    timeout -k 10 400 python tools/ab_plan.py --tm --reps 5 "" "LFD_TM_W=512" "LFD_TM_W=21" "LFD_TM_W=3" ;;
+  cm_wg)    # channel-major K1 with 256-thread groups (profiles/r04q_ab_cm_wg.txt)
+    timeout -k 10 400 python tools/ab_plan.py --reps 5 "" "LFD_K1_WG=256" "LFD_K1_WG=2561" &&
+    timeout -k 10 300 python tools/ab_plan.py --ch 1250 --reps 5 "" "LFD_K1_WG=256" ;;
+  fir_strip) # FIR tiles per workgroup (profiles: DESIGN §9)
+    for e in "" "LFD_FIR_STRIP=4" "LFD_FIR_STRIP=6" "LFD_FIR_STRIP=12"; do
+      echo "${e:-default}"; env $e timeout -k 10 120 python tools/fir_bench.py | grep "q= 10" || exit 1
+    done ;;
+  final)    # the driver's round-end steps: GPU suite, smoke, default bench line (product library)
+    unset LFDAS_LIB
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+        > gpurun_out/final_pytest_gpu.log 2>&1 || { tail -40 gpurun_out/final_pytest_gpu.log; exit 1; }
+    tail -1 gpurun_out/final_pytest_gpu.log
+    timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+    timeout -k 10 700 python bench.py > gpurun_out/final_bench.json 2> gpurun_out/final_bench.err || exit 1
+    tail -1 gpurun_out/final_bench.json ;;
+  rehearsal) # N = 2 on one device: strong-scaling headline + sharded cfg5 stream
+    unset LFDAS_LIB
+    timeout -k 10 400 python bench.py --gpus 2 --one-device --steps 3 --warmup 1 --no-cpu --no-rolling --no-extra ;;
   *) echo "recipes: k1 units scan offgrid tm_r02 rolling_r02 mfma tm tm_ubench narrow longscan rolling fir fir_pmc"
-     echo "         fullrate lattice multi persist"; exit 2 ;;
+     echo "         fullrate lattice multi persist narrow_units scan_trace fr_mb fr_out fr_pmc lattice_pmc tm_wg"
+     echo "         cm_wg fir_strip final rehearsal"; exit 2 ;;
 esac
