@@ -59,8 +59,8 @@ int64_t lfd::option(int id) {
 #ifdef LFD_DIAG
   if (v == 0 && k_opt_env[id]) {
     if (const char *e = std::getenv(k_opt_env[id])) {
-      // LFD_SCAN_DEFER=0/1 meant in-chain / deferred
-      if (id == LFD_OPT_SCAN_DEFER) return std::atoi(e) != 0 ? 2 : 1;
+      // LFD_SCAN_DEFER=0/1 meant in-chain / deferred (3: segmented chains)
+      if (id == LFD_OPT_SCAN_DEFER) return std::atoi(e) == 3 ? 3 : (std::atoi(e) != 0 ? 2 : 1);
       return std::atoll(e);
     }
   }
@@ -768,6 +768,11 @@ struct lfd_lowpass_plan {
   lfd::RunConst *d_rc = nullptr;
   std::vector<int> slot_chunk;    // run slot (chunk-ordered runs) -> its chunk
   int *d_slot_chunk = nullptr;
+  // segmented run chains (lfd_internal.h SegGeom): [n_chunks][seg_max]
+  std::vector<lfd::SegGeom> segs;
+  lfd::SegGeom *d_segs = nullptr;
+  int seg_max = 0;
+  size_t off_SC = 0;
   // lattice one-pass plan (n_off > 0; built by plan_create_composite): the
   // grid is the lattice at its lowest phase, K1 forms the outputs at offsets
   // 0 .. n_off - 1 of every output block (MFMA rows 8 + d), runs start at
@@ -822,7 +827,7 @@ int lfd_device_count(int *count) {
 
 int lfd_set_option(int option, int64_t value) {
   if (option <= 0 || option >= N_OPT) return fail(LFD_EINVAL, "unknown option " + std::to_string(option));
-  if (value < 0 || (option == LFD_OPT_SCAN_DEFER ? value > 2 : value > 1))
+  if (value < 0 || (option == LFD_OPT_SCAN_DEFER ? value > 3 : value > 1))
     return fail(LFD_EINVAL, "option " + std::to_string(option) + ": value out of range");
   g_opt[option].store(value);
   return LFD_OK;
@@ -1121,6 +1126,44 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     for (int i = 0; i < 4; ++i)
       for (int q = 0; q < lfd::HSKIP_MAX; ++q)
         p->rc.KfH[i][q] = (nc > i && q < row) ? (double)Kx[(size_t)i * row + q] : 0.0;
+    // segmented chains: each chunk's runs in <= SEG_MAX segments of >=
+    // SEG_MIN_RUNS runs; P / Q = PhiF / PhiR to the segment's block count
+    {
+      int64_t gmax = 1;
+      for (const auto &G : p->chunks)
+        gmax = std::max<int64_t>(gmax, std::min<int64_t>(lfd::SEG_MAX, (G.r1 - G.r0) / lfd::SEG_MIN_RUNS));
+      p->seg_max = (int)gmax;
+      p->segs.assign((size_t)(n_chunks * gmax), lfd::SegGeom{});
+      Mat PF(4), PR(4);
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+          PF.a[i][j] = p->sc.PhiF[i * MAX_N + j];
+          PR.a[i][j] = p->sc.PhiR[i * MAX_N + j];
+        }
+      for (int64_t ci = 0; ci < n_chunks; ++ci) {
+        const auto &G = p->chunks[ci];
+        const int64_t nr = G.r1 - G.r0;
+        const int64_t gc = std::max<int64_t>(1, std::min<int64_t>(gmax, nr / lfd::SEG_MIN_RUNS));
+        const int64_t per = (nr + gc - 1) / gc;
+        for (int64_t k = 0; k < gmax; ++k) {
+          lfd::SegGeom &sgm = p->segs[(size_t)(ci * gmax + k)];
+          sgm.ra = std::min(G.r1, G.r0 + k * per);
+          sgm.rb = std::min(G.r1, sgm.ra + per);
+          if (k >= gc || sgm.ra >= sgm.rb) {
+            sgm.ra = sgm.rb = G.r1;
+            continue;
+          }
+          sgm.last = (k == gc - 1 || G.r0 + (k + 1) * per >= G.r1) ? 1 : 0;
+          const int64_t blocks = p->run_ks[sgm.rb - 1] + p->run_len[sgm.rb - 1] - p->run_ks[sgm.ra];
+          const Mat Pk = mpow(PF, (int)blocks), Qk = mpow(PR, (int)blocks);
+          for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+              sgm.P[i * 4 + j] = (double)Pk.a[i][j];
+              sgm.Q[i * 4 + j] = (double)Qk.a[i][j];
+            }
+        }
+      }
+    }
     if (n_off > 0) {
       // per offset d: the output's responses to the states (G0_d, H0_d) and
       // the run constants built on them; H0_d also into the K1 constants
@@ -1158,7 +1201,8 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     p->off_SR = align256(p->off_AG + sizeof(double) * (size_t)p->run_ks.size() * 8 * ch16);
     p->off_TR = align256(p->off_SR + sizeof(double) * (size_t)p->n_sr * 4 * ch64);
     p->off_CR = align256(p->off_TR + sizeof(double) * (size_t)p->n_sr * 4 * ch64);
-    end_F = std::max(end_F, align256(p->off_CR + sizeof(double) * (size_t)n_chunks * ch64));
+    p->off_SC = align256(p->off_CR + sizeof(double) * (size_t)n_chunks * ch64);
+    end_F = std::max(end_F, align256(p->off_SC + sizeof(double) * (size_t)n_chunks * lfd::SC_N_HOST * ch64));
   }
   p->off_TP = end_F;
   p->ws_bytes = align256(p->off_TP + sizeof(double) * (size_t)p->tp_len * n_chunks * n_ch);
@@ -1216,6 +1260,11 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     if (e == hipSuccess && !p->slot_chunk.empty())
       e = hipMemcpy(p->d_slot_chunk, p->slot_chunk.data(), sizeof(int) * p->slot_chunk.size(),
                     hipMemcpyHostToDevice);
+    if (e == hipSuccess && !p->segs.empty()) {
+      e = hipMalloc(&p->d_segs, sizeof(lfd::SegGeom) * p->segs.size());
+      if (e == hipSuccess)
+        e = hipMemcpy(p->d_segs, p->segs.data(), sizeof(lfd::SegGeom) * p->segs.size(), hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess && n_off > 0) {
       e = hipMalloc(&p->d_rc_off, sizeof(lfd::RunConst) * n_off);
       if (e == hipSuccess)
@@ -1498,7 +1547,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
                                        reinterpret_cast<double *>(ws + L->off_TP), L->tp_len,
                                        reinterpret_cast<double *>(ws + L->off_TR),
                                        reinterpret_cast<double *>(ws + L->off_CR), L->d_slot_chunk, L->n_off,
-                                       L->d_rc_off, L->d_chunks_off, tmp, L->n_off * n_g, n_g, st));
+                                       L->d_rc_off, L->d_chunks_off, tmp, L->n_off * n_g, n_g, st, L->d_segs,
+                                       L->seg_max, reinterpret_cast<double *>(ws + L->off_SC)));
       LFD_HIP(lfd::launch_blend_grid_sm(tmp, p->n_ch, p->d_bj, p->d_bi_lat, p->d_bw, p->n_blend, y, ys_ch, ys_t, st,
                                         gen));
       if (timed) LFD_HIP(hipEventRecord(ev[2], st));
@@ -1553,7 +1603,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks, p->n_chunks, Y0,
                                         AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st,
                                         reinterpret_cast<double *>(ws + p->off_TR),
-                                        reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk));
+                                        reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk, p->d_segs,
+                                        p->seg_max, reinterpret_cast<double *>(ws + p->off_SC)));
     if (timed) LFD_HIP(hipEventRecord(ev[2], st));
     return LFD_OK;
   }
@@ -1668,7 +1719,7 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   for (auto *sp : p->subs) lfd_lowpass_plan_destroy(sp);
   if (p->lat) lfd_lowpass_plan_destroy(p->lat);
   for (void *d : {(void *)p->d_bj, (void *)p->d_bi, (void *)p->d_bw, (void *)p->d_bi_lat, (void *)p->d_rc_off,
-                  (void *)p->d_chunks_off})
+                  (void *)p->d_chunks_off, (void *)p->d_segs})
     if (d) (void)hipFree(d);
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);

@@ -185,6 +185,17 @@ struct RunConst {
   double H0L[8][4];
 };
 constexpr int LAT_MAX_OFF = 8;  // output offsets of a lattice one-pass K1 (MFMA rows 8 .. 15)
+// Segmented run chains (long chains: lattice plans, dt = 10 s): a chunk's runs
+// [r0, r1) cut into <= SEG_MAX segments [ra, rb) of >= SEG_MIN_RUNS runs; P /
+// Q = PhiF / PhiR to the segment's block count (the forward / reverse
+// transition across it: powers of one matrix, so the run order does not
+// matter); last = the chunk's last segment.  Inactive slots: ra == rb.
+constexpr int SEG_MAX = 16, SEG_MIN_RUNS = 8;
+constexpr int SC_N_HOST = 24;  // doubles per (chunk, channel) of the segmented scan's scratch (k_chunk_scan SC_N)
+struct SegGeom {
+  int64_t ra, rb, last;
+  double P[16], Q[16];
+};
 constexpr int HSKIP_MAX = 32;
 struct RunGeom {
   int64_t n_runs, n_groups, n_sr;
@@ -298,7 +309,8 @@ hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const 
                                const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
                                double *TR, double *CR, const int *slot_chunk, int n_off, const RunConst *rc_off,
-                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st);
+                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st,
+                               const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr);
 hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,
                             double *AG, hipStream_t st);
 // Run-mode scan.  With TR / CR / slot_chunk (per run slot: its chunk) the
@@ -309,7 +321,8 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   const ChunkGeom *cg_dev, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
                                   float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR = nullptr,
-                                  double *CR = nullptr, const int *slot_chunk = nullptr);
+                                  double *CR = nullptr, const int *slot_chunk = nullptr,
+                                  const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr);
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g,
                                     const BlockConst &kc, double *F,

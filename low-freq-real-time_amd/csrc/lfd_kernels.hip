@@ -499,13 +499,21 @@ __constant__ int g_k1_band = 0;
 // parallel.  The per-thread chain is then the 4x4 T recurrence alone: with
 // the outputs inside the chain a 1,250-channel shard spent 2.3 us per run
 // step on one wave per 7 SIMDs.
-template <int NS, bool RUNS, bool DEFER = false, int DFT = SCAN_DF, int DBT = SCAN_DB>
+// SEGM (segmented chains, run mode with DEFER): 1 = the head only: the state
+// entering run r0 and the FIR-history corrections go to SC, then return (the
+// forward chain is k_seg_fwd's); 2 = the tail only, from the state after the
+// chunk's last run (SC, from k_seg_fwd): pad + tail forward, the reverse over
+// them, the T entering the last run into SC, then return (the backward chain
+// is k_seg_bwd's).  SC layout: [chunk][SC_* slot][ch64].
+constexpr int SC_HS = 0, SC_SE = 4, SC_TE = 8, SC_CORR = 12, SC_N = SC_N_HOST;
+template <int NS, bool RUNS, bool DEFER = false, int DFT = SCAN_DF, int DBT = SCAN_DB, int SEGM = 0>
 __global__ __launch_bounds__(256) void k_chunk_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
     const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
     const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
     int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
-    const double *__restrict__ Y0, double *__restrict__ TR = nullptr, double *__restrict__ CR = nullptr) {
+    const double *__restrict__ Y0, double *__restrict__ TR = nullptr, double *__restrict__ CR = nullptr,
+    double *__restrict__ SC = nullptr) {
   constexpr int N = 2 * NS;
   constexpr int J = 2 * NS;
   constexpr int NF = 2 * N + 1;
@@ -554,8 +562,23 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
   };
 
-  // ---- left edge: odd extension (float32 like numpy), steady state of ext[0]
+  const int64_t ch64 = (g.n_ch + 63) / 64 * 64;
+  auto sc_at = [&](int slot) -> double & { return SC[(c * SC_N + slot) * ch64 + ch]; };
+  // head / tail / reverse walks: 8 samples' loads issued together (a per-step
+  // load left every step waiting on memory latency: the off-sample grids'
+  // heads and tails are up to L - 1 samples)
+  constexpr int SB = 8;
   double S[N], h[J];
+  double corr[NF];
+  const int64_t nF = NF;
+  if constexpr (SEGM == 2) {
+    // (segmented chains) the state after the chunk's last run
+#pragma unroll
+    for (int i = 0; i < N; ++i) S[i] = sc_at(SC_SE + i);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) corr[i] = 0.0;
+  } else {
+  // ---- left edge: odd extension (float32 like numpy), steady state of ext[0]
   const float xl = xc[G.s0 * s_t];
   // head skip (run mode, ChunkGeom::hskip): the head is block kb-1 without
   // its samples [lo, s0), so the state entering block kb is
@@ -608,10 +631,6 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       for (int j = 0; j < J; ++j) h[j] = (double)xc[(G.head_end - 1 - j) * s_t];
     }
   }
-  // head / tail / reverse walks: 8 samples' loads issued together (a per-step
-  // load left every step waiting on memory latency: the off-sample grids'
-  // heads and tails are up to L - 1 samples)
-  constexpr int SB = 8;
   if (!(LFD_DG(g_scan_diag) & 1) && !hs) {
     int64_t t = G.s0;
     for (; t + SB <= G.head_end; t += SB) {
@@ -626,7 +645,6 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 
   // ---- FIR-history correction of block kb: K1 used the raw samples before
   // head_end (0 before the channel start); this chunk saw pad / head values.
-  double corr[NF];
   {
     double dh[J];
 #pragma unroll
@@ -652,9 +670,15 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   }
 
   if (DEFER) CR[c * ((g.n_ch + 63) / 64 * 64) + ch] = corr[2 * N];
+  if constexpr (SEGM == 1) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) sc_at(SC_HS + i) = S[i];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) sc_at(SC_CORR + i) = corr[i];
+    return;
+  }
   // ---- forward scan over the full blocks (run mode: over runs; SF holds S_in
   // per run, F holds the run aggregates)
-  const int64_t nF = NF;
   if constexpr (RUNS) {
     static_assert(N == RUN_N, "run mode is 4th order");
     const RunConst &rc = rcs[0];
@@ -721,6 +745,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
     for (int i = 0; i < N; ++i) S[i] = ns[i];
   }
+  }  // SEGM != 2
 
   // ---- right edge: tail samples + odd extension, forward, stored
 #pragma unroll
@@ -792,6 +817,11 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   }
 
   // ---- backward scan, outputs at block starts
+  if constexpr (SEGM == 2) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) sc_at(SC_TE + i) = T[i];
+    return;
+  }
   if constexpr (RUNS) {
     const RunConst &rc = rcs[0];
     // software-pipelined like the forward scan: run r-1's inputs (S_in,
@@ -4444,6 +4474,195 @@ __global__ __launch_bounds__(256) void k_fold_runs(const double *__restrict__ F,
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_seg_fwd / k_seg_bwd — the run chains of the deferred scan cut into
+// segments (SegGeom): a workgroup = one chunk x 64 channels, wave w = segment
+// w, lane = channel.  Forward: each segment's aggregate from a zero state,
+// the entering state S_w = P_{w-1} (... (P_0 S_head + A_0) ...) + A_{w-1}
+// over the earlier segments (LDS), then the segment again from S_w writing
+// S_in of every run (SR); the chunk's last segment leaves the state after the
+// last run for the tail (SC).  Backward the same with T from the right:
+// T(ks) = PhiR^len T + E_r + C[len] S_in (+ the FIR-history correction at
+// run r0), writing the T entering every run (TR).  Between the two, the
+// head and the tail run in k_chunk_scan<..., SEGM = 1 / 2>.  Each thread's
+// chain shrinks from a chunk's runs to a segment's (lattice plans: ~1,350 ->
+// ~85 runs).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_seg_fwd(BlockGeom g, const ChunkGeom *__restrict__ cgs, RunGeom rg,
+                                                  const SegGeom *__restrict__ sgs, int seg_max,
+                                                  const double *__restrict__ AG, double *__restrict__ SR,
+                                                  double *__restrict__ SC) {
+  constexpr int N = RUN_N;
+  __shared__ double sPF[RUN_R + 1][16];
+  __shared__ double agg[SEG_MAX][64][N];
+  for (int i = threadIdx.x; i < (RUN_R + 1) * 16; i += blockDim.x) (&sPF[0][0])[i] = (&rg.rc->PhiFp[0][0])[i];
+  __syncthreads();
+  const int64_t n_c64 = (g.n_ch + 63) / 64, ch64 = n_c64 * 64;
+  const int64_t c = blockIdx.x / n_c64, c64 = blockIdx.x % n_c64;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t ch = c64 * 64 + lane;
+  const bool valid = ch < g.n_ch;
+  const int64_t chc = valid ? ch : g.n_ch - 1;
+  const ChunkGeom &G = cgs[c];
+  const SegGeom &sg = sgs[c * seg_max + wv];
+  const int64_t ra = sg.ra, rb = sg.rb;
+  const double *agb = AG + (((chc >> 4) * rg.n_runs) * 8) * 16 + (chc & 15);
+  double cf[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) cf[i] = ra == G.r0 ? SC[(c * SC_N + SC_CORR + i) * ch64 + chc] : 0.0;
+  auto step = [&](int64_t r, double (&S)[N]) {
+    const int len = rg.run_len[r];
+    const double *P = sPF[len];
+    double ns[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double acc = agb[(r * 8 + i) * 16] + (r == G.r0 ? cf[i] : 0.0);
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
+      ns[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) S[i] = ns[i];
+  };
+  double a[N] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t r = ra; r < rb; ++r) step(r, a);
+#pragma unroll
+  for (int i = 0; i < N; ++i) agg[wv][lane][i] = a[i];
+  __syncthreads();
+  if (ra >= rb) return;
+  double S[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) S[i] = SC[(c * SC_N + SC_HS + i) * ch64 + chc];
+  for (int k = 0; k < wv; ++k) {
+    const SegGeom &sk = sgs[c * seg_max + k];
+    if (sk.ra >= sk.rb) continue;
+    double ns[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double acc = agg[k][lane][i];
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fma(sk.P[i * 4 + j], S[j], acc);
+      ns[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) S[i] = ns[i];
+  }
+  for (int64_t r = ra; r < rb; ++r) {
+    if (valid) {
+      double *sr = SR + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
+#pragma unroll
+      for (int i = 0; i < N; ++i) sr[i * SF_ISTRIDE] = S[i];
+    }
+    step(r, S);
+  }
+  if (sg.last && valid)
+#pragma unroll
+    for (int i = 0; i < N; ++i) SC[(c * SC_N + SC_SE + i) * ch64 + ch] = S[i];
+}
+
+__global__ __launch_bounds__(1024) void k_seg_bwd(BlockGeom g, const ChunkGeom *__restrict__ cgs, RunGeom rg,
+                                                  const SegGeom *__restrict__ sgs, int seg_max,
+                                                  const double *__restrict__ AG, const double *__restrict__ SR,
+                                                  double *__restrict__ TR, const double *__restrict__ SC) {
+  constexpr int N = RUN_N;
+  __shared__ double sPR[RUN_R + 1][16], sC[RUN_R + 1][16];
+  __shared__ double agg[SEG_MAX][64][N];
+  for (int i = threadIdx.x; i < (RUN_R + 1) * 16; i += blockDim.x) {
+    (&sPR[0][0])[i] = (&rg.rc->PhiRp[0][0])[i];
+    (&sC[0][0])[i] = (&rg.rc->C[0][0])[i];
+  }
+  __syncthreads();
+  const int64_t n_c64 = (g.n_ch + 63) / 64, ch64 = n_c64 * 64;
+  const int64_t c = blockIdx.x / n_c64, c64 = blockIdx.x % n_c64;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t ch = c64 * 64 + lane;
+  const bool valid = ch < g.n_ch;
+  const int64_t chc = valid ? ch : g.n_ch - 1;
+  const ChunkGeom &G = cgs[c];
+  const SegGeom &sg = sgs[c * seg_max + wv];
+  const int64_t ra = sg.ra, rb = sg.rb;
+  const double *agb = AG + (((chc >> 4) * rg.n_runs) * 8) * 16 + (chc & 15);
+  double cr[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) cr[i] = ra == G.r0 ? SC[(c * SC_N + SC_CORR + N + i) * ch64 + chc] : 0.0;
+  auto step = [&](int64_t r, double (&T)[N]) {
+    const int len = rg.run_len[r];
+    const double *PR = sPR[len], *CC = sC[len];
+    const double *sr = SR + sf_index(G.sr_off + (r - G.r0), 0, chc, rg.n_sr, N);
+    double sin[N], nt[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) sin[i] = sr[i * SF_ISTRIDE];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double acc = agb[(r * 8 + 4 + i) * 16] + (r == G.r0 ? cr[i] : 0.0);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        acc = fma(PR[i * 4 + j], T[j], acc);
+        acc = fma(CC[i * 4 + j], sin[j], acc);
+      }
+      nt[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) T[i] = nt[i];
+  };
+  double b[N] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t r = rb - 1; r >= ra; --r) step(r, b);
+#pragma unroll
+  for (int i = 0; i < N; ++i) agg[wv][lane][i] = b[i];
+  __syncthreads();
+  if (ra >= rb) return;
+  double T[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) T[i] = SC[(c * SC_N + SC_TE + i) * ch64 + chc];
+  for (int k = seg_max - 1; k > wv; --k) {
+    const SegGeom &sk = sgs[c * seg_max + k];
+    if (sk.ra >= sk.rb) continue;
+    double nt[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double acc = agg[k][lane][i];
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fma(sk.Q[i * 4 + j], T[j], acc);
+      nt[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) T[i] = nt[i];
+  }
+  for (int64_t r = rb - 1; r >= ra; --r) {
+    if (valid) {
+      double *tr = TR + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
+#pragma unroll
+      for (int i = 0; i < N; ++i) tr[i * SF_ISTRIDE] = T[i];
+    }
+    step(r, T);
+  }
+}
+
+// head -> segmented forward -> tail -> segmented backward (CR and the
+// deferred outputs as in the unsegmented deferred scan)
+static hipError_t launch_seg_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
+                                  const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
+                                  const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
+                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR, double *CR,
+                                  const SegGeom *seg, int seg_max, double *SC) {
+  const int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
+  const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
+  k_chunk_scan<2, true, true, SCAN_DF, SCAN_DB, 1><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG,
+                                                                       SR, TP, tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR,
+                                                                       SC);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const unsigned nwg = (unsigned)(n_chunks * ((g.n_ch + 63) / 64));
+  k_seg_fwd<<<nwg, 64 * seg_max, 0, st>>>(g, cg, rg, seg, seg_max, AG, SR, SC);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  k_chunk_scan<2, true, true, SCAN_DF, SCAN_DB, 2><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG,
+                                                                       SR, TP, tp_len, y, ys_ch, ys_t, rg, Y0, TR, CR,
+                                                                       SC);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  k_seg_bwd<<<nwg, 64 * seg_max, 0, st>>>(g, cg, rg, seg, seg_max, AG, SR, TR, SC);
+  return hipGetLastError();
+}
+
 hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,
                             double *AG, hipStream_t st) {
   if (g.nF != 2 * RUN_N + 1 || rg.n_runs < 1) return hipErrorInvalidValue;
@@ -4457,7 +4676,7 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   const ChunkGeom *cg, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
                                   float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR,
-                                  double *CR, const int *slot_chunk) {
+                                  double *CR, const int *slot_chunk, const SegGeom *seg, int seg_max, double *SC) {
   // deferred outputs (k_run_outputs) when the scan has few (chunk, channel)
   // threads and is latency-bound: 1,250 ch x 7 chunks (an 8-GPU shard of
   // cfg3) 0.247 -> 0.152 ms, 2,500 ch 0.263 -> 0.191, 5,000 ch equal, 10,000
@@ -4480,6 +4699,22 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     }
   }
 #endif
+  // segmented chains (option scan_defer = 3, or automatically for long chains
+  // on few threads: >= 128 runs per chunk and < 40,000 (chunk, channel)
+  // threads — the 3 kHz lattice line's state scan 0.42 -> 0.31 ms; with
+  // 40,000 threads (dt = 10 s at 10,000 channels) the unsegmented deferred
+  // scan is faster, 0.60 vs 0.72 ms)
+  const int64_t o_defer = option(LFD_OPT_SCAN_DEFER);
+  const bool segm = seg && SC && seg_max >= 1 && TR && CR && slot_chunk &&
+                    (o_defer == 3 || (o_defer == 0 && n_chunks * g.n_ch < 40000 && rg.n_sr >= 128 * n_chunks));
+  if (segm) {
+    hipError_t e = launch_seg_scan(x, s_ch, s_t, g, padlen, sc, rg, cg, n_chunks, Y0, AG, SR, TP, tp_len, y, ys_ch,
+                                   ys_t, st, TR, CR, seg, seg_max, SC);
+    if (e != hipSuccess) return e;
+    const int64_t waves = ((g.n_ch + 63) / 64) * rg.n_sr;
+    k_run_outputs<<<nblk(waves, 4), 256, 0, st>>>(g, cg, rg, slot_chunk, Y0, SR, TR, CR, y, ys_ch, ys_t);
+    return hipGetLastError();
+  }
   if (TR && CR && slot_chunk && defer) {
     // narrow shards: 64-thread workgroups (one wave per CU instead of four
     // sharing one): 1,250 channels 0.150 -> 0.126 ms, bit-identical
@@ -4631,11 +4866,18 @@ hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const 
                                const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
                                double *TR, double *CR, const int *slot_chunk, int n_off, const RunConst *rc_off,
-                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st) {
+                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st,
+                               const SegGeom *seg, int seg_max, double *SC) {
   if (n_off < 1 || n_off > LAT_MAX_OFF || !TR || !CR || !slot_chunk) return hipErrorInvalidValue;
   const int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
   const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
-  if (rg.n_sr >= 128 * n_chunks)
+  const int64_t o_defer = option(LFD_OPT_SCAN_DEFER);
+  if (seg && SC && seg_max >= 1 &&
+      (o_defer == 3 || (o_defer == 0 && n_chunks * g.n_ch < 40000 && rg.n_sr >= 128 * n_chunks))) {
+    const hipError_t e = launch_seg_scan(x, s_ch, s_t, g, padlen, sc, rg, cg, n_chunks, Y0, AG, SR, TP, tp_len, y,
+                                         ys_ch, 1, st, TR, CR, seg, seg_max, SC);
+    if (e != hipSuccess) return e;
+  } else if (rg.n_sr >= 128 * n_chunks)
     k_chunk_scan<2, true, true, 16, 8><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                                             tp_len, y, ys_ch, 1, rg, Y0, TR, CR);
   else

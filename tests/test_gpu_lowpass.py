@@ -527,6 +527,38 @@ def test_scan_deferred_outputs_bit_identical(off_ns):
         assert _relrms(y[:, oa:ob], r) < 1e-4
 
 
+@pytest.mark.parametrize("cfg", [
+    (500.0, 1.0, 60, 7, 70, 400.0, 0, False),          # short chains (~8 runs per chunk)
+    (500.0, 1.0, 600, 7, 33, 1500.0, 123_457, False),  # off-sample grid, head skip
+    (1000.0, 10.0, 30, 6, 20, 3000.0, 0, True),        # dt = 10 s: long chains (sub-blocks), a null
+])
+def test_scan_segmented_chains_match_deferred(cfg):
+    """Segmented run chains (option scan_defer = 3: head, per-segment
+    forward aggregates + combine, tail, per-segment backward; chosen
+    automatically for chunks of >= 128 runs) against the unsegmented deferred
+    scan (= 2): the same states up to summation order — the float32 outputs
+    differ by last-bit roundings at most (relRMS 1e-7), identical NaN
+    footprint — and both against the oracle (1e-4)."""
+    fs, dt_out, P, B, n_ch, dur, off_ns, null = cfg
+    x = (np.random.default_rng(9).standard_normal((n_ch, int(dur * fs))) + 3.0).astype(np.float32)
+    if null:
+        x[4, int(dur * fs) // 3] = np.nan
+    out = {}
+    for mode in (2, 3):
+        with kernel_options(scan_defer=mode):
+            out[mode] = _run(x, fs, dt_out, P, B, "tc", off_ns=off_ns)
+        assert _run.last_kernel == "mfma_runs"
+    a, b = out[2][0], out[3][0]
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    f = np.isfinite(a)
+    assert _relrms(b[f], a[f]) < 1e-7
+    y, ref, sched = out[3]
+    for (tt, r), (lo, hi, oa, ob) in zip(ref, sched):
+        fr = np.isfinite(r)
+        np.testing.assert_array_equal(np.isnan(y[:, oa:ob]), ~fr)
+        assert _relrms(y[:, oa:ob][fr], r[fr]) < 1e-4
+
+
 @pytest.mark.parametrize("which", ["lo", "head_first", "head_last", "fir_history"])
 def test_offsample_head_skip_nulls(which):
     """Off-sample grids skip the chunk head with K1's one-block run kb-1
