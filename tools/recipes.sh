@@ -97,6 +97,13 @@ case "$1" in
         echo "== $c ${e:-default}"; grep -h "chunk_scan\|run_outputs\|runs_mfma" $d/*/tr_kernel_stats.csv $d/tr_kernel_stats.csv 2>/dev/null
       done
     done ;;
+  seg_scan) # segmented run chains vs the unsegmented deferred scan (profiles/r04y_ab_seg_scan.txt)
+    timeout -k 10 300 python tools/ab_plan.py --fs 1000 --dt 10 --P 120 --B 6 --ch 2000 --reps 4 "" "LFD_SCAN_DEFER=2" &&
+    timeout -k 10 300 python tools/ab_plan.py --fs 3000 --dt 1 --seconds 1800 --P 600 --B 7 --ch 2000 --reps 4 "" \
+        "LFD_SCAN_DEFER=2" &&
+    for c in 1250 2500; do
+      timeout -k 10 240 python tools/ab_plan.py --ch $c --reps 4 "" "LFD_SCAN_DEFER=3" || exit 1
+    done ;;
   fr_mb)    # full-rate: medium-block path vs the big-block path (profiles/r04d_fr_ab_mfma_output_vs_bigblock.txt)
     for e in "" "LFD_FULLRATE_BIGBLOCK=1"; do
       echo "== $e"; env $e timeout -k 10 120 python tools/fr_bench.py || exit 1
@@ -133,5 +140,5 @@ case "$1" in
     timeout -k 10 400 python bench.py --gpus 2 --one-device --steps 3 --warmup 1 --no-cpu --no-rolling --no-extra ;;
   *) echo "recipes: k1 units scan offgrid tm_r02 rolling_r02 mfma tm tm_ubench narrow longscan rolling fir fir_pmc"
      echo "         fullrate lattice multi persist narrow_units scan_trace fr_mb fr_out fr_pmc lattice_pmc tm_wg"
-     echo "         cm_wg fir_strip final rehearsal"; exit 2 ;;
+     echo "         cm_wg fir_strip final rehearsal seg_scan"; exit 2 ;;
 esac
