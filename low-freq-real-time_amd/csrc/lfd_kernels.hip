@@ -5058,7 +5058,13 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                float *y, int64_t ys_ch, int64_t ys_t,
                                hipStream_t st) {
   const int64_t n_out = (n_t + S - 1) / S;
-  const int64_t cap = 256 * 32;  // workgroups of the grid-stride launches
+  // workgroups of the grid-stride launches: the running-sum scan (S < W / 2)
+  // keeps 8,192 (4.54 vs 4.66 ms uncapped on cfg2 at S = 1); the segment-sum
+  // and direct-window kernels up to 65,536 groups, one unit per wave at cfg2
+  // (S = 250: 2.61 -> 2.45
+  // ms, S = W: 2.16 -> 2.13; profiles/r04aa_ab_roll_cap.txt)
+  int64_t cap = 256 * 32, cap_unit = 65536;
+  if (const char *v = knob("LFD_ROLL_CAP")) cap = cap_unit = std::atoll(v) > 0 ? std::atoll(v) : INT32_MAX;  // (diag A/B; 0 = none)
   // step < window: the running-sum scan reads each sample twice (x[t] and,
   // from cache, x[t - W]) and scans every position; summing each window
   // directly reads it W/S times from L2/L1 (W/S = 4: 5.25 ms vs 3.81 ms on
@@ -5087,7 +5093,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
       const int64_t seg_out = std::max<int64_t>(1, span / S);
       const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
       int64_t blocks = (units + 3) / 4;
-      if (blocks > cap) blocks = cap;
+      if (blocks > cap_unit) blocks = cap_unit;
       const size_t lds = sizeof(double) * 2 * (size_t)ring * 4;
       static bool attr = false;
       if (!attr) {
@@ -5105,7 +5111,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // windows overlap little or not at all: each is summed directly by one wave
     const int64_t waves = n_ch * n_out;
     int64_t blocks = (waves + 3) / 4;
-    if (blocks > cap) blocks = cap;
+    if (blocks > cap_unit) blocks = cap_unit;
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     k_rolling_tc<<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, n_t, s_ch, W, S, y,
                                                    ys_ch, ys_t, vec);
