@@ -5060,9 +5060,9 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
   const int64_t n_out = (n_t + S - 1) / S;
   // workgroups of the grid-stride launches: the running-sum scan (S < W / 2)
   // keeps 8,192 (4.54 vs 4.66 ms uncapped on cfg2 at S = 1); the segment-sum
-  // and direct-window kernels up to 65,536 groups, one unit per wave at cfg2
-  // (S = 250: 2.61 -> 2.45
-  // ms, S = W: 2.16 -> 2.13; profiles/r04aa_ab_roll_cap.txt)
+  // and direct-window kernels take up to 65,536 groups (cfg2, S = 250: one
+  // unit per wave, 2.61 -> 2.45 ms; S = W: 2.16 -> 2.13 ms at 16,384 groups;
+  // profiles/r04aa_ab_roll_cap.txt)
   int64_t cap = 256 * 32, cap_unit = 65536;
   if (const char *v = knob("LFD_ROLL_CAP")) cap = cap_unit = std::atoll(v) > 0 ? std::atoll(v) : INT32_MAX;  // (diag A/B; 0 = none)
   // step < window: the running-sum scan reads each sample twice (x[t] and,
