@@ -3945,6 +3945,7 @@ hipError_t launch_block_runs_mfma_tm_ab(const float *x, int64_t s_t, int64_t n_t
       if (const char *wv = knob("LFD_TM_W")) {
         if (std::atoi(wv) == 3) return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 3>, 256);
         if (std::atoi(wv) == 21) return go(&k_block_runs_mfma_tm<1, 128, false, 2, true, false, true, 0, true, 2>, 128);
+        if (std::atoi(wv) == 22) return go(&k_block_runs_mfma_tm<2, 256, false, 2, true, false, true, 0, true, 2>, 256);
         if (std::atoi(wv) == 512) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
       }
       if (pfb == 1) return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 2>, 256);
