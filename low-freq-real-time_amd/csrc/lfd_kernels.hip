@@ -1292,6 +1292,10 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
 // the 16x16x4 A register with quad r of every 16-lane row broadcast to its
 // four quads: ds_swizzle bit-mask mode (and 0x13, or 4r: lane bits 0, 1, 4
 // kept, bits 2, 3 = r), a lane crossbar with no memory access.
+// quad r of every 16-lane row broadcast to the row's four quads (ds_swizzle
+// bit-mask mode: and 0x13, or 4r — lane bits 0, 1, 4 kept, bits 2, 3 = r):
+// the 4x4x4_4b A operand of functional group r from a 16x16x4 A register
+// (mfma_k4, mf_iter_s)
 template <int FG>
 __device__ __forceinline__ double quad_bcast(double v) {
   constexpr int pat = 0x13 | ((FG << 2) << 5);
@@ -2747,6 +2751,32 @@ __device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o0, int lo, i
     }
 }
 
+
+// (M4S) the same 16 MFMA steps as 4 x 4 v_mfma_f64_4x4x4_4b with A from the
+// lane's 16x16x4 taps through quad_bcast: the D layout stays acc0/acc1's
+template <bool M4S>
+__device__ __forceinline__ void mf_iter_s(const double *kt, int kstride, const f4v (&cur)[4], d4v &acc0, d4v &acc1) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double2 b01 = *reinterpret_cast<const double2 *>(kt + j * kstride);
+    const double2 b23 = *reinterpret_cast<const double2 *>(kt + j * kstride + 2);
+    const double a[4] = {b01.x, b01.y, b23.x, b23.y};
+    const double bv[4] = {(double)cur[j].x, (double)cur[j].y, (double)cur[j].z, (double)cur[j].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      d4v &acc = (e & 1) ? acc1 : acc0;
+      if constexpr (M4S) {
+        acc[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<0>(a[e]), bv[e], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<1>(a[e]), bv[e], acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<2>(a[e]), bv[e], acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<3>(a[e]), bv[e], acc[3], 0, 0, 0);
+      } else {
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], bv[e], acc, 0, 0, 0);
+      }
+    }
+  }
+}
+
 // 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur.
 // Lanes of A rows c >= nc read a copy of row nc-1 instead of zeros: MFMA rows
 // are independent (D[c][:] depends on A[c][:] only) and rows >= nc of D are
@@ -2820,7 +2850,7 @@ __device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<c
 // invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
 // ceiling of the x stream + F stores; 3 = no MFMA and no F stores = the
 // x-stream ceiling alone.
-template <int PF, int MODE>
+template <int PF, int MODE, bool M4S = false>
 __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs,
@@ -2925,7 +2955,10 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
           const int v = (int)(s & 3);
           mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
         }
-        mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+        if constexpr (M4S)
+          mf_iter_s<true>(kt + (4 * it) * kstride, kstride, buf[u], acc0, acc1);
+        else
+          mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
       }
       if (++it == nit) {
         if (MODE == 6) {  // diagnostic: same stores into a 64 KB L2-resident window
@@ -4104,7 +4137,16 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
                                                                    n_runs, bpw)
 #ifdef LFD_DIAG
-  if (mode == 1)
+  if (knob_flag("LFD_MF_M4S")) {
+    static bool attr_s = false;
+    if (!attr_s) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0, true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
+      if (e != hipSuccess) return e;
+      attr_s = true;
+    }
+    k_block_functionals_mfma<2, 0, true><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, n_runs, bpw);
+  } else if (mode == 1)
     LFD_MF(2, 1);
   else if (mode == 3)
     LFD_MF(2, 3);
