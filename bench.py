@@ -605,8 +605,8 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
     .data -> scipy sosfiltfilt): 2,000 ch x 10 min @ 1 kHz, 8th-order
     Butterworth band-pass (4 sections), float32 in, float64 out (SciPy's
     dtype).  Algorithmic bytes 4 + 8 per channel-sample.  The dominant
-    kernel is the output pass k_fullrate_wave<4, true> (x read + y written
-    over the big blocks, 12 B per sample)."""
+    kernel is the output pass k_fullrate_out_mb<4> (x read + y written over
+    the medium blocks, 12 B per sample)."""
     import torch
     import oracle
     from lfdas.design import pass_filter_sos
@@ -636,9 +636,9 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
         kt.append(sosfiltfilt_last_timing_ms())
     set_timing(False)
     kt = np.mean(np.array(kt), axis=0)
-    L = 2048
-    nb = (n - 1) // L
-    gbs_out = n_ch * nb * L * 12 / (kt[2] * 1e-3) / 1e9
+    LB = 512  # medium block: the output pass covers M = (n - 1) // 512 of them
+    n_out_s = (n - 1) // LB * LB
+    gbs_out = n_ch * n_out_s * 12 / (kt[2] * 1e-3) / 1e9
     gbs_all = n_ch * n * 12 / (ms * 1e-3) / 1e9
     # parity spot check outside the timed region (3 channels vs the oracle)
     rows = [0, n_ch // 2, n_ch - 1]
@@ -670,10 +670,10 @@ def bench_fullrate(dev, n_ch=2000, n=600_000, fs=1000.0, band=(1.0, 10.0), reps=
                       f"(corners=4, {sos.shape[0]} sections), zero-phase, full rate",
             "kernels_ms": {"k_block_functionals_mfma (medium-block functionals, fp64 MFMA)": kt[0],
                            "k_fullrate_scan_seg<4> (segmented scan)": kt[1],
-                           "k_fullrate_wave<4,true> (output)": kt[2]},
-            "roofline": {"bound": "hbm", "kernel": "k_fullrate_wave<4,true>", "achieved": gbs_out,
+                           "k_fullrate_out_mb<4> (output)": kt[2]},
+            "roofline": {"bound": "hbm", "kernel": "k_fullrate_out_mb<4>", "achieved": gbs_out,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs_out / HBM_PEAK_GBS,
-                         "alg_bytes_per_sample": 12, "samples_per_launch": n_ch * nb * L},
+                         "alg_bytes_per_sample": 12, "samples_per_launch": n_ch * n_out_s},
             "pipeline_hbm_frac": gbs_all / HBM_PEAK_GBS,
             "relrms_vs_oracle_3ch": rel,
             "serial_kernel_ms_tenth": serial_ms,
