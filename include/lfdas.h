@@ -129,8 +129,8 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *plan);
 int lfd_set_timing(int enable);
 /* Which block-functional kernel the last execute ran: LFD_K1_MFMA (fp64
  * matrix cores over the plan's block taps; time-contiguous float32 rows,
- * 16-B aligned, channel stride a multiple of 4) or LFD_K1_RECURRENCE (any
- * strides, or cascades above 6th order); 0 before the first execute. */
+ * any channel stride) or LFD_K1_RECURRENCE (strided time, or cascades above
+ * 6th order); 0 before the first execute. */
 #define LFD_K1_RECURRENCE 1
 #define LFD_K1_MFMA 2
 #define LFD_K1_MFMA_RUNS 3 /* MFMA + in-register run folding (4th-order cascades) */

@@ -806,7 +806,7 @@ struct lfd_lowpass_plan {
   size_t off_tmp = 0;
   int64_t *d_bj = nullptr, *d_bi = nullptr;  // grid index; scratch index of y[lo], y[lo + 1] (-1: w == 0)
   double *d_bw = nullptr;
-  // one-pass alternative (channel-major, 16-B aligned rows): one lattice plan
+  // one-pass alternative (channel-major, time-contiguous rows): one lattice plan
   // for every phase (n_off offsets), slot-major scratch [n_off * n_grid][n_ch]
   lfd_lowpass_plan *lat = nullptr;
   int64_t *d_bi_lat = nullptr;
@@ -1530,7 +1530,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
   if (!p->subs.empty()) {
     float *tmp = reinterpret_cast<float *>(ws + p->off_tmp);
     const lfd_lowpass_plan *L = p->lat;
-    p->last_onepass = L && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+    p->last_onepass = L && s_t == 1 && (reinterpret_cast<uintptr_t>(x) & 3) == 0 &&
                       !lfd::option(LFD_OPT_LATTICE_PHASES);
     if (p->last_onepass) {
       // one pass: K1 with every phase's outputs (ev[0] .. ev[1]), then the
@@ -1571,8 +1571,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
   }
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
   const bool rec = lfd::option(LFD_OPT_K1_RECURRENCE) != 0;
-  const bool mfma = p->d_taps && s_t == 1 && (s_ch % 4 == 0 || p->n_ch == 1) &&
-                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && !rec;
+  // (any row stride: the MFMA kernels load 4-B aligned 16-B pieces)
+  const bool mfma = p->d_taps && s_t == 1 && (reinterpret_cast<uintptr_t>(x) & 3) == 0 && !rec;
   const bool runs = p->run_ok && !lfd::option(LFD_OPT_NO_RUNS);
   const bool mfma_runs = runs && mfma && p->run_mfma_ok;
   // (time, channel) rows (the real files' layout): the time-major MFMA kernel
@@ -1872,10 +1872,9 @@ int lfd_sosfiltfilt_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
   if (nb > 0 && !lfd::option(LFD_OPT_FULLRATE_SERIAL)) {
     std::shared_ptr<const FrEntry> fe;
     if (int e = fullrate_entry(sos, n_sec, c, &fe)) return e;
-    // medium-block path (time-contiguous, 16-B aligned rows): the functionals
+    // medium-block path (time-contiguous rows, any stride): the functionals
     // on the fp64 matrix cores and the segmented scan
-    const bool mb = s_t == 1 && (s_ch % 4 == 0 || n_ch == 1) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-                    !lfd::option(LFD_OPT_FULLRATE_BIGBLOCK);
+    const bool mb = s_t == 1 && (reinterpret_cast<uintptr_t>(x) & 3) == 0 && !lfd::option(LFD_OPT_FULLRATE_BIGBLOCK);
     const FrLayout lo = mb ? fullrate_layout_mb(n_ch, n_t, padlen, n_sec)
                            : fullrate_layout(n_ch, n_t, padlen, n_sec, nb);
     char *ws = static_cast<char *>(workspace);

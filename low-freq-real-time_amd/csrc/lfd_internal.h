@@ -143,8 +143,8 @@ constexpr int SF_ISTRIDE = 64;  // element stride between states of one (block, 
 
 // Block taps of the MFMA block-functional kernel.  The functionals are linear
 // in the block's extended samples: F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p]
-// (lfd_capi.cpp block_taps).  Block k's row is read from the 16-B aligned
-// sample floor4(base + k*L - J), i.e. shifted by v = (base + k*L - J) mod 4;
+// (lfd_capi.cpp block_taps).  Block k's row is read from the row's sample
+// floor4(base + k*L - J) (16-B pieces, 4-B aligned on odd strides), i.e. shifted by v = (base + k*L - J) mod 4;
 // the device table holds the taps for each shift that occurs (nvar = 1 when
 // L % 4 == 0, else 4), zero-padded to Lp samples:
 //   taps[v][((t*4 + q)*nc + c)*4 + e] = Kx[c][16t + 4q + e - v]
@@ -281,7 +281,7 @@ hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t
                                 int64_t n_t, int64_t nb, int padlen, const FRConst *fc, const double *F,
                                 double *SF, double *ST, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
                                 hipStream_t st);
-// MFMA block functionals: s_t == 1, s_ch % 4 == 0, 16-B aligned x.
+// MFMA block functionals: s_t == 1 (any channel stride).
 hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n_t,
                                          const BlockGeom &g, const double *taps,
                                          const TapGeom &tg, double *F, hipStream_t st);

@@ -36,6 +36,13 @@ namespace lfd {
 namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+// the same vectors at the alignment of their element (4-B / 8-B aligned row
+// pieces: rows whose stride is not a multiple of 4 samples).  gfx950 serves
+// such accesses with the same global_load_dwordx4 / store (unaligned access
+// mode), so one kernel covers every row stride
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
 
 // Nulls (SciPy semantics): a NaN / inf sample poisons every output of the
 // chunks that contain it and nothing else.  A block's functionals also read
@@ -1381,23 +1388,24 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
 #pragma unroll 8
       for (int u = lane; u < L; u += 64) tile[(u >> 5) * TS + (u & 31)] = u < nvs ? row[u] : 0.0f;
     } else if constexpr (T36) {
-      float4 v[L / 256];
+      // (rows need not be 16-B aligned: f4u pieces)
+      f4v v[L / 256];
 #pragma unroll
-      for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const float4 *>(row + 4 * lane + 256 * i);
+      for (int i = 0; i < L / 256; ++i) v[i] = *reinterpret_cast<const f4u *>(row + 4 * lane + 256 * i);
 #pragma unroll
       for (int i = 0; i < L / 256; ++i) {
         const int u = 4 * lane + 256 * i;
-        *reinterpret_cast<float4 *>(tile + u + 4 * (u >> 5)) = v[i];
+        *reinterpret_cast<f4v *>(tile + u + 4 * (u >> 5)) = v[i];
       }
     } else {
       // instruction i: lane quarter g = lane >> 4 reads sub-block 16 g + i
       // (4 x 128-B pieces), 2 samples per lane
       const int g = lane >> 4, e2 = 2 * (lane & 15);
-      float2 v[16];
+      f2u v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const float2 *>(row + (16 * g + i) * LS + e2);
+      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const f2u *>(row + (16 * g + i) * LS + e2);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) *reinterpret_cast<float2 *>(tile + (16 * g + i) * TS + e2) = v[i];
+      for (int i = 0; i < 16; ++i) *reinterpret_cast<f2u *>(tile + (16 * g + i) * TS + e2) = v[i];
     }
   }
   __syncthreads();
@@ -1560,12 +1568,12 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       o[12] = yacc[mt][nt][3];
     }
     __syncthreads();
-    if (ys_t == 1 && (reinterpret_cast<uintptr_t>(yr) & 15) == 0) {
+    if (ys_t == 1) {  // 16-B pieces, 8-B aligned on rows of odd length (d2u)
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int r = LAY == 1 ? it * 8 + (lane >> 3) : it + 8 * (lane >> 3), c2 = 2 * (lane & 7);
         if (r < nsb)
-          *reinterpret_cast<double2 *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const double2 *>(ob + r * OSTR + c2);
+          *reinterpret_cast<d2u *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const d2u *>(ob + r * OSTR + c2);
       }
     } else {
 #pragma unroll
@@ -2321,7 +2329,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         if (full) {
 #pragma unroll
           for (int h = 0; h < RS_E / 4; ++h) {
-            const f4v a = *reinterpret_cast<const f4v *>(row + t + 4 * h);
+            const f4v a = *reinterpret_cast<const f4u *>(row + t + 4 * h);
 #pragma unroll
             for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
           }
@@ -2337,11 +2345,11 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
 #pragma unroll
         for (int h = 0; h < RS_E / 4; ++h) {
           const int tc = tb + 4 * lane + 256 * h;
-          const f4v a = *reinterpret_cast<const f4v *>(row + tc);
+          const f4v a = *reinterpret_cast<const f4u *>(row + tc);
 #pragma unroll
           for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
           if ((W & 3) == 0) {
-            const f4v b = *reinterpret_cast<const f4v *>(row + tc - W);
+            const f4v b = *reinterpret_cast<const f4u *>(row + tc - W);
 #pragma unroll
             for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
           } else {
@@ -2352,11 +2360,11 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
       } else if (VEC && full) {
 #pragma unroll
         for (int h = 0; h < RS_E / 4; ++h) {
-          const f4v a = *reinterpret_cast<const f4v *>(row + t + 4 * h);
+          const f4v a = *reinterpret_cast<const f4u *>(row + t + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
           if ((W & 3) == 0) {
-            const f4v b = *reinterpret_cast<const f4v *>(row + t + 4 * h - W);
+            const f4v b = *reinterpret_cast<const f4u *>(row + t + 4 * h - W);
 #pragma unroll
             for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
           } else {
@@ -2621,7 +2629,7 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
       if (tb >= pos0 && tb + RG_P - 1 <= pend) {
 #pragma unroll
         for (int h = 0; h < RG_E / 4; ++h) {
-          const f4v a = *reinterpret_cast<const f4v *>(row + p + 4 * h);
+          const f4v a = *reinterpret_cast<const f4u *>(row + p + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) T.v[4 * h + e] = a[e];
         }
@@ -2844,7 +2852,7 @@ __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, doubl
 // (non-temporal loads of the sample stream were measured 40 % slower on cfg3:
 // 18.5 vs 13.1 ms — the 64-B row pieces of consecutive iterations no longer
 // meet in L2)
-__device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<const f4v *>(p); }
+__device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<const f4u *>(p); }
 
 // MODE 0: production.  Diagnostic modes (timing experiments only, results
 // invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
@@ -5126,8 +5134,9 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     const int64_t g = ga;
     int ring = 16;
     while (ring < W / g + RG_P / g + 3) ring *= 2;
+    // (rows of any stride: 4-B aligned 16-B pieces, f4u)
     bool seg = s_t == 1 && S > 1 && S < W && g >= 16 && ring <= 1024 && n_t < (int64_t)INT32_MAX - 2 * RG_P &&
-               (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
+               (reinterpret_cast<uintptr_t>(x) & 3) == 0;
     if (const char *v = knob("LFD_ROLL_SEGSUM")) seg = seg && std::atoi(v) != 0;
     if (seg) {
       int64_t span = std::max<int64_t>(32768, 8 * W);
@@ -5169,7 +5178,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
     int64_t blocks = (units + 3) / 4;
     if (blocks > cap) blocks = cap;
-    const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
+    const bool vec = (reinterpret_cast<uintptr_t>(x) & 3) == 0;  // (any row stride: f4u loads)
     const bool vec_out = vec && ys_t == 1 && ys_ch % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
     // stage 2 (lanes load their 8 positions directly, outputs leave through
     // LDS as coalesced float4 stores) measured best on cfg2 at S = 1: 4.77 ms

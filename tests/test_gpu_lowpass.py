@@ -135,11 +135,12 @@ def _plan_cfg(fs, dt_out, P, B, n_ch, n):
     (250.0, 0.2, 40, 6, 37, 6000),      # L = 50: four row-shift tap tables
     (500.0, 1.0, 600, 7, 33, 750_000),  # L = 500
     (200.0, 10.0, 100, 7, 5, 600_000),  # R = 2000: 4 sub-blocks of 500
-    (1000.0, 0.5, 40, 4, 18, 100_003),  # L = 500, odd n_t (channel stride % 4 != 0 -> recurrence)
+    (1000.0, 0.5, 40, 4, 18, 100_003),  # L = 500, odd n_t (channel stride % 4 != 0: rows 4-B aligned)
 ])
 def test_k1_mfma_matches_recurrence(cfg):
     """Both block-functional kernels feed the same scan: outputs agree to
-    float32 rounding; the dispatch picks MFMA only for aligned rows."""
+    float32 rounding; the dispatch picks MFMA for every time-contiguous row
+    stride (odd record lengths load 4-B aligned 16-B pieces)."""
     import torch
     fs, dt_out, P, B, n_ch, n = cfg
     rng = np.random.default_rng(7)
@@ -156,9 +157,8 @@ def test_k1_mfma_matches_recurrence(cfg):
             plan.execute(xd, yd, ws)
         torch.cuda.synchronize()
         out[mode] = (yd.cpu().numpy(), plan.last_kernel())
-    aligned = n % 4 == 0
-    assert out["default"][1] == ("mfma_runs" if aligned else "recurrence_fold")
-    assert out["noruns"][1] == ("mfma" if aligned else "recurrence")
+    assert out["default"][1] == "mfma_runs"
+    assert out["noruns"][1] == "mfma"
     assert out["rec"][1] == "recurrence"
     assert out["recfold"][1] == "recurrence_fold"
     b = out["rec"][0]
@@ -170,8 +170,9 @@ def test_k1_mfma_matches_recurrence(cfg):
 
 
 def test_k1_unaligned_base_pointer():
-    """A view starting one sample in (not 16-B aligned) takes the recurrence
-    kernel (+ run fold) and still matches the aligned MFMA path."""
+    """A view starting one sample in (rows not 16-B aligned) runs the same
+    MFMA run kernel as an aligned copy of the same rows — bit-identical
+    outputs — and matches the recurrence kernel."""
     import torch
     fs, dt_out, P, B = 500.0, 1.0, 60, 7
     n_ch, n = 9, 40_000
@@ -182,15 +183,21 @@ def test_k1_unaligned_base_pointer():
     xd = full[:, 1:n + 1]
     yd = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
     plan.execute(xd, yd, plan.alloc_workspace())
-    assert plan.last_kernel() == "recurrence_fold"
+    assert plan.last_kernel() == "mfma_runs"
     y_ok = yd.cpu().numpy()
+    yr = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
+    with kernel_options(k1_recurrence=1):
+        plan.execute(xd, yr, plan.alloc_workspace())
+    assert plan.last_kernel() == "recurrence_fold"
+    y_rec = yr.cpu().numpy()
     xa = torch.from_numpy(np.ascontiguousarray(x[:, 1:n + 1])).cuda()
     yd2 = torch.full((n_ch, n_grid), float("nan"), dtype=torch.float32, device="cuda")
     plan.execute(xa, yd2, plan.alloc_workspace())
     assert plan.last_kernel() == "mfma_runs"
     y2 = yd2.cpu().numpy()
     m = ~np.isnan(y2)
-    assert _relrms(y_ok[m], y2[m]) < 1e-6
+    np.testing.assert_array_equal(y_ok, y2)
+    assert _relrms(y_rec[m], y2[m]) < 1e-6
 
 
 def test_cfg1_random_das():
@@ -353,7 +360,8 @@ def test_full_rate_blocked_parity(case, bigblock):
     """lfd_sosfiltfilt_f32's blocked paths against SciPy's sosfiltfilt
     restatement, relRMS < 1e-10 per channel: the medium-block path (matrix-core
     functionals -> k_fullrate_scan_seg -> row-scan output pass, the default
-    for time-contiguous rows) and the big-block path (k_fullrate_wave
+    for time-contiguous rows of any stride: the odd n_t cases run it on rows
+    that are not 16-B aligned) and the big-block path (k_fullrate_wave
     functionals -> k_fullrate_scan -> k_fullrate_wave outputs)."""
     import torch
     from lfdas._lib import kernel_options
