@@ -1758,15 +1758,24 @@ __global__ __launch_bounds__(64) void k_fullrate_scan(
 //      from zi * y_f[-1] (T_end, the tail's outputs)
 //   A' each segment's reverse aggregate from zero T: T <- PhiB T + Z + MB S_f
 //   -> entering T from the right, C' the true T at every medium block (STm).
-// The output pass (k_fullrate_wave<NS, true, true>) reads SFm / STm per row.
+// The output pass (k_fullrate_out_mb) reads SFm / STm per row.
 // 16 x G threads per channel group instead of one thread per channel walking
 // every block: the walks are G times shorter (latency-bound chains).
+// Edge windows in LDS (xl > 0): the workgroup stages the record's last xl
+// samples (tail + what the right pad reflects) and first E + 1 samples of its
+// channels at the start, and the tail's forward outputs stay in LDS, so the
+// serial edge walks (left pad; tail + right pad forward, then reverse) read
+// LDS instead of waiting one global latency per batch of samples (2,000 x
+// 600,000, tail 448: 0.484 -> 0.392 ms; profiles/r04ah_fr_scan_lds_edges.txt).
+// xl = 0 (windows too large for LDS, or diag knob LFD_FR_TAIL_GLOBAL): the
+// global-memory walks through TP.  (Batches of 6 / 3 blocks in the walks
+// instead of 4 / 2 measured the same: 0.391 ms.)
 template <int NS, int CW = 16>
 __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t, int64_t M, int padlen,
     const FRConst *__restrict__ fc, const double *__restrict__ F2, double *__restrict__ SFm,
     double *__restrict__ STm, double *__restrict__ TP, double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
-    FRSeg sg) {
+    FRSeg sg, int xl) {
   constexpr int N = 2 * NS;
   __shared__ double cPB[N * N], cMB[N * N], cPS[N * N], cPT[N * N];
   static_assert(CW == 16 || CW == 8, "16 or 8 channels per workgroup");
@@ -1779,6 +1788,27 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     cMB[i] = fc->MB[r * MAX_N + c];
     cPS[i] = sg.pseg[r * MAX_N + c];
     cPT[i] = sg.plast[r * MAX_N + c];
+  }
+  const int E = padlen;
+  const int64_t nt_tail = n_t - M * FR_LB;  // tail samples (1 .. FR_LB)
+  // LDS windows after agg: tail outputs yw [nt + E][CW] (double), samples
+  // xw [xl][CW] (the record's last xl), head xh [E + 1][CW]
+  double *yw = agg + (size_t)sg.G * CW * N;
+  float *xw = reinterpret_cast<float *>(yw + (size_t)(nt_tail + E) * CW);
+  float *xh = xw + (size_t)xl * CW;
+  const int64_t lo_w = n_t - xl;
+  if (xl > 0) {
+    const int64_t c_base = (int64_t)blockIdx.x * CW;
+    for (int i = tid; i < CW * xl; i += blockDim.x) {
+      const int c = i / xl, t = i - c * xl;  // consecutive threads: consecutive samples
+      const int64_t chn = c_base + c < n_ch ? c_base + c : n_ch - 1;
+      xw[t * CW + c] = x[chn * s_ch + (lo_w + t) * s_t];
+    }
+    for (int i = tid; i < CW * (E + 1); i += blockDim.x) {
+      const int c = i / (E + 1), t = i - c * (E + 1);
+      const int64_t chn = c_base + c < n_ch ? c_base + c : n_ch - 1;
+      xh[t * CW + c] = x[chn * s_ch + t * s_t];
+    }
   }
   __syncthreads();
   const int64_t ch = (int64_t)blockIdx.x * CW + col;
@@ -1832,14 +1862,16 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
 #pragma unroll
   for (int n = 0; n < N; ++n) ag[n] = a[n];
   const float *xc = x + chc * s_ch;
-  const int E = padlen;
-  const float x0 = xc[0], xn = xc[(n_t - 1) * s_t];
+  // sample t of this channel: from the LDS windows when staged
+  auto xhead = [&](int64_t t) { return xl > 0 ? xh[t * CW + col] : xc[t * s_t]; };
+  auto xend = [&](int64_t t) { return xl > 0 ? xw[(t - lo_w) * CW + col] : xc[t * s_t]; };
+  const float x0 = xhead(0), xn = xend(n_t - 1);
   if (active && seg == 0) {  // SciPy's left edge: zi * ext[0], then the odd extension
     double z[N];
-    const double e0 = (double)(2.0f * x0 - xc[E * s_t]);
+    const double e0 = (double)(2.0f * x0 - xhead(E));
 #pragma unroll
     for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * e0;
-    for (int t = 0; t < E; ++t) (void)fr.step(z, (double)(2.0f * x0 - xc[(E - t) * s_t]));
+    for (int t = 0; t < E; ++t) (void)fr.step(z, (double)(2.0f * x0 - xhead(E - t)));
 #pragma unroll
     for (int n = 0; n < N; ++n) slotL[col][n] = z[n];
   }
@@ -1875,8 +1907,31 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
         }
       }
     }
-    if (seg == sg.Gu - 1) {
-      // tail samples [nb FR_L, n_t) and the right pad forward (TP), then the
+    if (seg == sg.Gu - 1 && xl > 0) {
+      // (LDS windows) tail [M FR_LB, n_t) + right pad forward into yw, then
+      // the reverse from zi * y_f[-1] over pad + tail (the tail's outputs)
+      const int64_t t_tail = M * FR_LB, nt = nt_tail;
+      double yl = 0.0;
+      for (int64_t i = 0; i < nt; ++i) {
+        yl = fr.step(z, (double)xend(t_tail + i));
+        yw[i * CW + col] = yl;
+      }
+      for (int64_t i = 0; i < E; ++i) {
+        yl = fr.step(z, (double)(2.0f * xn - xend(n_t - 2 - i)));
+        yw[(nt + i) * CW + col] = yl;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) z[i] = fc->zi.v[i] * yl;
+      for (int64_t i = nt + E - 1; i >= nt; --i) (void)fr.step(z, yw[i * CW + col]);
+      double *yt = y + ch * ys_ch + t_tail * ys_t;
+      for (int64_t i = nt - 1; i >= 0; --i) yt[i * ys_t] = fr.step(z, yw[i * CW + col]);
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        slotR[col][n] = z[n];
+        STm[(M * N + n) * n_ch + ch] = z[n];
+      }
+    } else if (seg == sg.Gu - 1) {
+      // tail samples [M FR_LB, n_t) and the right pad forward (TP), then the
       // reverse from zi * y_f[-1] over pad + tail (the tail's outputs); the
       // reverse re-reads TP in batches of B (one latency per batch)
       constexpr int B = 8;
@@ -5033,6 +5088,9 @@ hipError_t launch_fullrate_scan(int n_sec, const float *x, int64_t s_ch, int64_t
   return hipGetLastError();
 }
 
+// dynamic LDS cap of k_fullrate_scan_seg (agg + edge windows; 160 KB per CU
+// minus the static matrices and slots)
+constexpr size_t FR_SEG_LDS_MAX = 148 * 1024;
 hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int64_t s_t, int64_t n_ch, int64_t n_t,
                                     int64_t M, int padlen, const FRConst *fc, const double *F2, double *SFm,
                                     double *STm, double *TP, double *y, int64_t ys_ch, int64_t ys_t,
@@ -5041,7 +5099,18 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
       M < 1)
     return hipErrorInvalidValue;
   const unsigned g = nblk(n_ch, sg.cw);
-  const size_t lds = sizeof(double) * (size_t)sg.G * sg.cw * 2 * n_sec;
+  size_t lds = sizeof(double) * (size_t)sg.G * sg.cw * 2 * n_sec;
+  // edge windows in LDS when they fit (SciPy's padlen < n_t): the last xl
+  // samples cover the tail and the samples the right pad reflects
+  const int64_t nt_tail = n_t - M * FR_LB;
+  int64_t xl = std::max<int64_t>(nt_tail, (int64_t)padlen + 1);
+  const size_t wb = (size_t)sg.cw * (sizeof(double) * (size_t)(nt_tail + padlen) + sizeof(float) * (size_t)xl +
+                                     sizeof(float) * (size_t)(padlen + 1));
+  if (xl > n_t || lds + wb > FR_SEG_LDS_MAX || knob_flag("LFD_FR_TAIL_GLOBAL")) {
+    xl = 0;  // (diag A/B knob: the global-memory edge walks)
+  } else {
+    lds += wb;
+  }
   static bool attr = false;  // (dynamic LDS above 64 KB with the static part)
   if (!attr) {
     for (const void *fn : {reinterpret_cast<const void *>(&k_fullrate_scan_seg<1>),
@@ -5052,7 +5121,7 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
                            reinterpret_cast<const void *>(&k_fullrate_scan_seg<2, 8>),
                            reinterpret_cast<const void *>(&k_fullrate_scan_seg<3, 8>),
                            reinterpret_cast<const void *>(&k_fullrate_scan_seg<4, 8>)}) {
-      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FR_SEG_LDS_MAX);
       if (e != hipSuccess) return e;
     }
     attr = true;
@@ -5060,10 +5129,10 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
 #define LFD_FRSS(NS)                                                                                               \
   if (sg.cw == 8)                                                                                                  \
     k_fullrate_scan_seg<NS, 8><<<g, sg.cw * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, M, padlen, fc, F2, SFm, STm, \
-                                                            TP, y, ys_ch, ys_t, sg);                               \
+                                                            TP, y, ys_ch, ys_t, sg, (int)xl);                      \
   else                                                                                                             \
     k_fullrate_scan_seg<NS><<<g, sg.cw * sg.G, lds, st>>>(x, s_ch, s_t, n_ch, n_t, M, padlen, fc, F2, SFm, STm, TP,  \
-                                                         y, ys_ch, ys_t, sg)
+                                                         y, ys_ch, ys_t, sg, (int)xl)
   switch (n_sec) {
     case 1: LFD_FRSS(1); break;
     case 2: LFD_FRSS(2); break;
