@@ -195,7 +195,7 @@ def time_plan(plan, x, y, wsb, stream, steps, warmup, barrier=None):
 
 
 def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_major=False, steps=5,
-                       label=""):
+                       label="", warmup=1):
     """One extra low-pass workload, timed like the headline (inputs in HBM,
     K1 roofline from its HIP-event time)."""
     import torch
@@ -211,7 +211,7 @@ def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_majo
     y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
     wsb = plan.alloc_workspace(dev)
     stream = torch.cuda.current_stream(dev)
-    el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, steps, 1)
+    el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, steps, warmup)
     R = int(round(fs * dt_out))
     k1 = float(np.mean(k1_ms))
     gbs = n_ch * n * (4.0 + 4.0 / R) / (k1 * 1e-3) / 1e9
@@ -914,8 +914,10 @@ def main():
         shards = {}
         for n_gpu in (2, 4, 8):
             c = -(-args.channels // n_gpu)
+            # (2-7 ms steps: 20 timed after 3 warmups, so one slow launch does
+            # not decide the projection)
             r = bench_lowpass_line(dev, c, args.fs, args.seconds, args.dt_out, args.patch_size, args.edge_buff,
-                                   steps=5, label=f"{c:,}-channel shard of cfg3 ({n_gpu} GPUs)")
+                                   steps=20, warmup=3, label=f"{c:,}-channel shard of cfg3 ({n_gpu} GPUs)")
             shards[f"n{n_gpu}"] = {"channels": c, "ms_per_step": r["ms_per_step"],
                                    "kernel_ms": r["roofline"]["kernel_ms"],
                                    "scan_kernel_ms": r["roofline"]["scan_kernel_ms"],

@@ -124,7 +124,7 @@ case "$1" in
     timeout -k 10 400 python tools/ab_plan.py --reps 5 "" "LFD_K1_WG=256" "LFD_K1_WG=2561" &&
     timeout -k 10 300 python tools/ab_plan.py --ch 1250 --reps 5 "" "LFD_K1_WG=256" ;;
   fir_strip) # FIR tiles per workgroup (profiles: DESIGN §9)
-    for e in "" "LFD_FIR_STRIP=4" "LFD_FIR_STRIP=6" "LFD_FIR_STRIP=12"; do
+    for e in "" "LFD_FIR_STRIP=4" "LFD_FIR_STRIP=6" "LFD_FIR_STRIP=12" "LFD_FIR_STRIP=16" "LFD_FIR_STRIP=30"; do
       echo "${e:-default}"; env $e timeout -k 10 120 python tools/fir_bench.py | grep "q= 10" || exit 1
     done ;;
   final)    # the driver's round-end steps: GPU suite, smoke, default bench line (product library)
