@@ -5458,7 +5458,8 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
   const int64_t nb = (int64_t)gridDim.x;
   // XCD-aware order: consecutive strips of one channel group on one XCD
   // (their input halos meet in that XCD's L2)
-  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  // (diag bit 128: dispatch order, no XCD remap)
+  if ((nb & 7) == 0 && !(diag & 128)) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
   const int64_t cg = bid / n_strips;
   const int64_t t_begin = (bid % n_strips) * strip;
   const int64_t t_end = t_begin + strip < tiles_o ? t_begin + strip : tiles_o;
