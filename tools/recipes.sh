@@ -127,6 +127,21 @@ case "$1" in
     for e in "" "LFD_FIR_STRIP=4" "LFD_FIR_STRIP=6" "LFD_FIR_STRIP=12" "LFD_FIR_STRIP=16" "LFD_FIR_STRIP=30"; do
       echo "${e:-default}"; env $e timeout -k 10 120 python tools/fir_bench.py | grep "q= 10" || exit 1
     done ;;
+  odd_strides) # rows of any stride on the MFMA kernels (profiles/r04ag_ab_odd_strides.txt)
+    for n in 599553 599800 600000 600063; do
+      timeout -k 10 120 python tools/fr_bench.py $n || exit 1
+    done &&
+    for p in 1 0 2; do echo "== pad $p"; timeout -k 10 200 python tools/ab_plan.py --pad $p --reps 3 "" || exit 1; done ;;
+  fr_scan_edges) # full-rate scan edge walks: LDS windows vs global (profiles/r04ah_fr_scan_lds_edges.txt)
+    for e in "" "LFD_FR_TAIL_GLOBAL=1"; do
+      echo "== $e"; env $e timeout -k 10 120 python tools/fr_bench.py 600000 || exit 1
+    done ;;
+  fir_xcd)  # FIR strip length and the XCD remap (diag bit 128) (profiles/r04am_fir_xcd.txt)
+    for r in 1 2 3; do
+      for e in "" "LFD_FIR_DIAG=128" "LFD_FIR_STRIP=16" "LFD_FIR_STRIP=4 LFD_FIR_DIAG=128" "LFD_FIR_STRIP=30 LFD_FIR_DIAG=128"; do
+        echo "${e:-default} $(env $e timeout -k 10 120 python tools/fir_bench.py 2>/dev/null | grep "q= 10")" || exit 1
+      done
+    done ;;
   final)    # the driver's round-end steps: GPU suite, smoke, default bench line (product library)
     unset LFDAS_LIB
     timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
@@ -140,5 +155,5 @@ case "$1" in
     timeout -k 10 400 python bench.py --gpus 2 --one-device --steps 3 --warmup 1 --no-cpu --no-rolling --no-extra ;;
   *) echo "recipes: k1 units scan offgrid tm_r02 rolling_r02 mfma tm tm_ubench narrow longscan rolling fir fir_pmc"
      echo "         fullrate lattice multi persist narrow_units scan_trace fr_mb fr_out fr_pmc lattice_pmc tm_wg"
-     echo "         cm_wg fir_strip final rehearsal seg_scan"; exit 2 ;;
+     echo "         cm_wg fir_strip final rehearsal seg_scan odd_strides fr_scan_edges fir_xcd"; exit 2 ;;
 esac
