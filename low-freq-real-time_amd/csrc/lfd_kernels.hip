@@ -1357,7 +1357,12 @@ __device__ __forceinline__ void mfma_k4(double av, const double (&b)[4], fr_d4v 
 // bound, profiles/r04h_fr_ab_lds_layout.txt); 2 (diag) = the 36-float tile
 // with the r / r + 8 row reads (4.17 ms)
 // M4: every product as 4x4x4_4b steps (mfma16x4)
-template <int NS, bool DIRECT = false, int LAY = 1, bool M4 = false>
+// PRE: the entering states SF (PRE >= 1) and ST (PRE = 2, production) are
+// loaded at the kernel start with the tile, so their latency hides behind
+// the tile's and the KAZ products instead of stalling the row scans: 3.92
+// vs 3.98 ms (PRE 0) and 4.00 (PRE 1) at 2,000 x 600,000
+// (profiles/r04ao_fr_ab_early_states.txt; diag knob LFD_FR_PRE=0 / 1)
+template <int NS, bool DIRECT = false, int LAY = 1, bool M4 = false, int PRE = 2>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
@@ -1382,6 +1387,17 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
   const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
   const int64_t a = k * L;
   const int nvs = (int)(n_mb - 4 * k < 4 ? (n_mb - 4 * k) * FR_LB : L);
+  const int64_t m_row = 4 * k + (lane >> 4);
+  const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
+  double SinE[PRE >= 1 ? N : 1], TinE[PRE >= 2 ? N : 1];
+  if constexpr (PRE >= 1) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) SinE[n] = SF[(m * N + n) * n_ch + ch];
+  }
+  if constexpr (PRE >= 2) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) TinE[n] = ST[((m + 1) * N + n) * n_ch + ch];
+  }
   {
     const float *row = x + ch * s_ch + a;
     if (nvs < L) {
@@ -1454,14 +1470,12 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     }
   };
   // ---- 2. row scans (row = medium block m, lane jr = its sub-block)
-  const int64_t m_row = 4 * k + (lane >> 4);
-  const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
   double W[K];  // (S_j, T_{j+1})
   {
     double Sin[N], vf[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      Sin[n] = SF[(m * N + n) * n_ch + ch];
+      Sin[n] = PRE >= 1 ? SinE[n] : SF[(m * N + n) * n_ch + ch];
       vf[n] = A[n];
     }
     if (jr == 0) matvec_add(fc->PhiP[0], Sin, vf, true);
@@ -1490,7 +1504,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     matvec_add(fc->M32, Sj, vb, false);
     double Tin[N];
 #pragma unroll
-    for (int n = 0; n < N; ++n) Tin[n] = ST[((m + 1) * N + n) * n_ch + ch];
+    for (int n = 0; n < N; ++n) Tin[n] = PRE >= 2 ? TinE[n] : ST[((m + 1) * N + n) * n_ch + ch];
     if (jr == 15) matvec_add(fc->PhiP[0], Tin, vb, true);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -5038,12 +5052,26 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
   static const bool fr_direct = knob_flag("LFD_FR_OUT_DIRECT");
   static const int fr_lay = knob("LFD_FR_LAYOUT") ? std::atoi(knob("LFD_FR_LAYOUT")) : 1;
   static const bool fr_m4 = knob_flag("LFD_FR_M4");
+  static const int fr_pre = knob("LFD_FR_PRE") ? std::atoi(knob("LFD_FR_PRE")) : -1;
 #else
   constexpr bool fr_direct = false;
   constexpr int fr_lay = 1;
   constexpr bool fr_m4 = false;
 #endif
+#ifdef LFD_DIAG
+#define LFD_FR_PRE_AB(NS)                                                                                           \
+  if (out && mb && fr_pre == 1)                                                                                    \
+    k_fullrate_out_mb<NS, false, 1, false, 1><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
+                                                                            ys_ch, ys_t);                          \
+  else if (out && mb && fr_pre == 0)                                                                               \
+    k_fullrate_out_mb<NS, false, 1, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
+                                                                            ys_ch, ys_t);                          \
+  else
+#else
+#define LFD_FR_PRE_AB(NS)
+#endif
 #define LFD_FR2(NS)   \
+  LFD_FR_PRE_AB(NS) \
   if (out && mb && fr_m4)      \
     k_fullrate_out_mb<NS, false, 1, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out && mb && fr_direct)      \
