@@ -1398,6 +1398,11 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
 #pragma unroll
     for (int n = 0; n < N; ++n) TinE[n] = ST[((m + 1) * N + n) * n_ch + ch];
   }
+  double kazE[PRE >= 3 ? LS / 4 : 1];  // (PRE 3, diag: the KAZ column too)
+  if constexpr (PRE >= 3) {
+#pragma unroll
+    for (int ks = 0; ks < LS / 4; ++ks) kazE[ks] = fc->KAZ[ks][lane];
+  }
   {
     const float *row = x + ch * s_ch + a;
     if (nvs < L) {
@@ -1434,7 +1439,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     for (int nt = 0; nt < 4; ++nt) acc[nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int ks = 0; ks < LS / 4; ++ks) {
-      const double av = fc->KAZ[ks][lane];
+      const double av = PRE >= 3 ? kazE[ks] : fc->KAZ[ks][lane];
       double bk[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) bk[nt] = (double)tb[TS * 16 * nt + 4 * ks];
@@ -5062,6 +5067,9 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
 #define LFD_FR_PRE_AB(NS)                                                                                           \
   if (out && mb && fr_pre == 1)                                                                                    \
     k_fullrate_out_mb<NS, false, 1, false, 1><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
+                                                                            ys_ch, ys_t);                          \
+  else if (out && mb && fr_pre == 3)                                                                               \
+    k_fullrate_out_mb<NS, false, 1, false, 3><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
                                                                             ys_ch, ys_t);                          \
   else if (out && mb && fr_pre == 0)                                                                               \
     k_fullrate_out_mb<NS, false, 1, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
