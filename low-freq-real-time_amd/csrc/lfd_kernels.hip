@@ -1366,7 +1366,7 @@ template <int NS, bool DIRECT = false, int LAY = 1, bool M4 = false, int PRE = 2
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
-    double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+    double *__restrict__ y, int64_t ys_ch, int64_t ys_t, int ord = 0) {
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L, K = 2 * N, KS = K / 4, OSTR = 18;
   static_assert(N % 2 == 0 && K % 4 == 0, "state components in groups of 4");
   // LDS banks (gfx950: 32 banks for 4-B accesses, 64 for 8 / 16 B): the
@@ -1384,7 +1384,16 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
   float *tile = reinterpret_cast<float *>(lds);
   const int lane = threadIdx.x;
   const int col = lane & 15, q = lane >> 4, jr = lane & 15;
-  const int64_t ch = blockIdx.x / nb, k = blockIdx.x % nb;
+  // ord: 0 = channel-major (consecutive groups = consecutive big blocks of
+  // one channel); 1 = block-major (consecutive groups = the same big block of
+  // consecutive channels, whose SF / ST entries share cache lines); 2
+  // (production) = block-major with the groups of one XCD contiguous: HBM
+  // reads 9.55 -> 5.08 GB per launch at 2,000 x 600,000 (x 4.8 GB + SF / ST
+  // 0.3 GB algorithmic; channel-major re-fetched each 128-B line of states
+  // once per channel), 3.89 -> 3.84 ms (profiles/r04au_fr_ab_block_order.txt)
+  int64_t bid = blockIdx.x;
+  if (ord == 2 && (gridDim.x & 7) == 0) bid = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+  const int64_t ch = ord ? bid % n_ch : bid / nb, k = ord ? bid / n_ch : bid % nb;
   const int64_t a = k * L;
   const int nvs = (int)(n_mb - 4 * k < 4 ? (n_mb - 4 * k) * FR_LB : L);
   const int64_t m_row = 4 * k + (lane >> 4);
@@ -5058,10 +5067,12 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
   static const int fr_lay = knob("LFD_FR_LAYOUT") ? std::atoi(knob("LFD_FR_LAYOUT")) : 1;
   static const bool fr_m4 = knob_flag("LFD_FR_M4");
   static const int fr_pre = knob("LFD_FR_PRE") ? std::atoi(knob("LFD_FR_PRE")) : -1;
+  static const int fr_ord = knob("LFD_FR_ORDER") ? std::atoi(knob("LFD_FR_ORDER")) : 2;
 #else
   constexpr bool fr_direct = false;
   constexpr int fr_lay = 1;
   constexpr bool fr_m4 = false;
+  constexpr int fr_ord = 2;
 #endif
 #ifdef LFD_DIAG
 #define LFD_FR_PRE_AB(NS)                                                                                           \
@@ -5089,7 +5100,7 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
   else if (out && mb && fr_lay == 2)      \
     k_fullrate_out_mb<NS, false, 2><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
   else if (out && mb)      \
-    k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
+    k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t, fr_ord); \
   else if (out)       \
     LFD_FR(NS, true); \
   else                \
