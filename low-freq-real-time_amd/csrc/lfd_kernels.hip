@@ -5270,6 +5270,25 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
         if (e != hipSuccess) return e;
         attr = true;
       }
+#ifdef LFD_DIAG
+      // (diag A/B: tiles in flight per wave)
+      if (const char *v = knob("LFD_ROLL_SEG_PF")) {
+        const int pf = std::atoi(v);
+        if (pf == 1 || pf == 3) {
+          const void *fn = pf == 1 ? reinterpret_cast<const void *>(&k_rolling_seg<1>)
+                                   : reinterpret_cast<const void *>(&k_rolling_seg<3>);
+          hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+          if (e != hipSuccess) return e;
+          if (pf == 1)
+            k_rolling_seg<1><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y,
+                                                                 ys_ch, ys_t, (int)seg_out, ring - 1);
+          else
+            k_rolling_seg<3><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y,
+                                                                 ys_ch, ys_t, (int)seg_out, ring - 1);
+          return hipGetLastError();
+        }
+      }
+#endif
       k_rolling_seg<2><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y, ys_ch,
                                                            ys_t, (int)seg_out, ring - 1);
       return hipGetLastError();
