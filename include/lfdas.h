@@ -64,7 +64,7 @@ int lfd_device_count(int *count);
 #define LFD_OPT_NO_RUNS 1         /* block plans: per-block functionals, no run folding   */
 #define LFD_OPT_K1_RECURRENCE 2   /* block plans: recurrence K1 instead of fp64 MFMA      */
 #define LFD_OPT_TM_NO_PAIRS 3     /* time-major MFMA K1: one dword per channel, no pairs  */
-#define LFD_OPT_SCAN_DEFER 4      /* run scan outputs: 1 in the chain, 2 deferred, 3 deferred + segmented chains */
+#define LFD_OPT_SCAN_DEFER 4      /* run scan: 1 outputs in the chain, 2 deferred, 3 deferred + segmented chains, 4 fused segmented (one launch) */
 #define LFD_OPT_FULLRATE_SERIAL 5 /* lfd_sosfiltfilt_f32: one thread per channel          */
 #define LFD_OPT_NO_LATTICE 6      /* drifting grids: LFD_EUNSUPPORTED (per-chunk path)    */
 #define LFD_OPT_NO_HEAD_SKIP 7    /* off-sample grids: walk chunk heads                   */

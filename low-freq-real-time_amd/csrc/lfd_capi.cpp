@@ -44,6 +44,10 @@ bool lfd::timing_enabled() { return g_timing.load() != 0; }
 namespace {
 constexpr int N_OPT = 11;  // LFD_OPT_* ids are 1 .. N_OPT - 1
 std::atomic<int64_t> g_opt[N_OPT];
+// set explicitly through lfd_set_option (then the diagnostic build's
+// environment names are not read, so lfd_set_option(id, 0) restores the
+// library's choice even while an A/B variable is exported)
+std::atomic<bool> g_opt_set[N_OPT];
 #ifdef LFD_DIAG
 // the A/B environment names the tools/ recipes of rounds 1-3 use
 const char *const k_opt_env[N_OPT] = {nullptr,          "LFD_NO_RUNS",    "LFD_K1_REC",
@@ -57,10 +61,14 @@ int64_t lfd::option(int id) {
   if (id <= 0 || id >= N_OPT) return 0;
   const int64_t v = g_opt[id].load(std::memory_order_relaxed);
 #ifdef LFD_DIAG
-  if (v == 0 && k_opt_env[id]) {
+  if (!g_opt_set[id].load(std::memory_order_relaxed) && k_opt_env[id]) {
     if (const char *e = std::getenv(k_opt_env[id])) {
-      // LFD_SCAN_DEFER=0/1 meant in-chain / deferred (3: segmented chains)
-      if (id == LFD_OPT_SCAN_DEFER) return std::atoi(e) == 3 ? 3 : (std::atoi(e) != 0 ? 2 : 1);
+      // LFD_SCAN_DEFER=0/1 meant in-chain / deferred (3: segmented chains,
+      // 4: the fused one-launch segmented scan)
+      if (id == LFD_OPT_SCAN_DEFER) {
+        const int d = std::atoi(e);
+        return d == 3 || d == 4 ? d : (d != 0 ? 2 : 1);
+      }
       return std::atoll(e);
     }
   }
@@ -772,6 +780,10 @@ struct lfd_lowpass_plan {
   std::vector<lfd::SegGeom> segs;
   lfd::SegGeom *d_segs = nullptr;
   int seg_max = 0;
+  // the fused one-launch scan (k_scan_fused): [n_chunks][nw_fu] segments
+  std::vector<lfd::SegGeom> segs_fu;
+  lfd::SegGeom *d_segs_fu = nullptr;
+  int nw_fu = 0;
   size_t off_SC = 0;
   // lattice one-pass plan (n_off > 0; built by plan_create_composite): the
   // grid is the lattice at its lowest phase, K1 forms the outputs at offsets
@@ -793,7 +805,7 @@ struct lfd_lowpass_plan {
   mutable int64_t n_exec = 0;
   mutable int last_ring = 0;  // ring size of the last timed execute (0: ev)
   mutable bool timed = false;
-  mutable int last_k1 = 0;
+  mutable std::atomic<int> last_k1{0};  // (plans may be executed from several host threads)
   // Composite plan (grids that are not one uniform lattice with one fraction
   // w: 3 kHz data on integer-ns times, jittered archives): one uniform,
   // sample-aligned sub-plan per lattice phase d (positions lo0 + j R + d),
@@ -811,7 +823,7 @@ struct lfd_lowpass_plan {
   lfd_lowpass_plan *lat = nullptr;
   int64_t *d_bi_lat = nullptr;
   size_t off_tmp_lat = 0;
-  mutable bool last_onepass = false;
+  mutable std::atomic<bool> last_onepass{false};
 };
 
 extern "C" {
@@ -827,9 +839,10 @@ int lfd_device_count(int *count) {
 
 int lfd_set_option(int option, int64_t value) {
   if (option <= 0 || option >= N_OPT) return fail(LFD_EINVAL, "unknown option " + std::to_string(option));
-  if (value < 0 || (option == LFD_OPT_SCAN_DEFER ? value > 3 : value > 1))
+  if (value < 0 || (option == LFD_OPT_SCAN_DEFER ? value > 4 : value > 1))
     return fail(LFD_EINVAL, "option " + std::to_string(option) + ": value out of range");
   g_opt[option].store(value);
+  g_opt_set[option].store(true);
   return LFD_OK;
 }
 
@@ -1126,43 +1139,52 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     for (int i = 0; i < 4; ++i)
       for (int q = 0; q < lfd::HSKIP_MAX; ++q)
         p->rc.KfH[i][q] = (nc > i && q < row) ? (double)Kx[(size_t)i * row + q] : 0.0;
-    // segmented chains: each chunk's runs in <= SEG_MAX segments of >=
-    // SEG_MIN_RUNS runs; P / Q = PhiF / PhiR to the segment's block count
+    // segmented chains: each chunk's runs in <= gmax segments of >= min_runs
+    // runs; P / Q = PhiF / PhiR to the segment's block count
     {
-      int64_t gmax = 1;
-      for (const auto &G : p->chunks)
-        gmax = std::max<int64_t>(gmax, std::min<int64_t>(lfd::SEG_MAX, (G.r1 - G.r0) / lfd::SEG_MIN_RUNS));
-      p->seg_max = (int)gmax;
-      p->segs.assign((size_t)(n_chunks * gmax), lfd::SegGeom{});
       Mat PF(4), PR(4);
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
           PF.a[i][j] = p->sc.PhiF[i * MAX_N + j];
           PR.a[i][j] = p->sc.PhiR[i * MAX_N + j];
         }
-      for (int64_t ci = 0; ci < n_chunks; ++ci) {
-        const auto &G = p->chunks[ci];
-        const int64_t nr = G.r1 - G.r0;
-        const int64_t gc = std::max<int64_t>(1, std::min<int64_t>(gmax, nr / lfd::SEG_MIN_RUNS));
-        const int64_t per = (nr + gc - 1) / gc;
-        for (int64_t k = 0; k < gmax; ++k) {
-          lfd::SegGeom &sgm = p->segs[(size_t)(ci * gmax + k)];
-          sgm.ra = std::min(G.r1, G.r0 + k * per);
-          sgm.rb = std::min(G.r1, sgm.ra + per);
-          if (k >= gc || sgm.ra >= sgm.rb) {
-            sgm.ra = sgm.rb = G.r1;
-            continue;
-          }
-          sgm.last = (k == gc - 1 || G.r0 + (k + 1) * per >= G.r1) ? 1 : 0;
-          const int64_t blocks = p->run_ks[sgm.rb - 1] + p->run_len[sgm.rb - 1] - p->run_ks[sgm.ra];
-          const Mat Pk = mpow(PF, (int)blocks), Qk = mpow(PR, (int)blocks);
-          for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) {
-              sgm.P[i * 4 + j] = (double)Pk.a[i][j];
-              sgm.Q[i * 4 + j] = (double)Qk.a[i][j];
+      auto build_segs = [&](int64_t gmax, int64_t min_runs, std::vector<lfd::SegGeom> &segs) {
+        segs.assign((size_t)(n_chunks * gmax), lfd::SegGeom{});
+        for (int64_t ci = 0; ci < n_chunks; ++ci) {
+          const auto &G = p->chunks[ci];
+          const int64_t nr = G.r1 - G.r0;
+          const int64_t gc = std::max<int64_t>(1, std::min<int64_t>(gmax, nr / min_runs));
+          const int64_t per = (nr + gc - 1) / gc;
+          for (int64_t k = 0; k < gmax; ++k) {
+            lfd::SegGeom &sgm = segs[(size_t)(ci * gmax + k)];
+            sgm.ra = std::min(G.r1, G.r0 + k * per);
+            sgm.rb = std::min(G.r1, sgm.ra + per);
+            if (k >= gc || sgm.ra >= sgm.rb) {
+              sgm.ra = sgm.rb = G.r1;
+              continue;
             }
+            sgm.last = (k == gc - 1 || G.r0 + (k + 1) * per >= G.r1) ? 1 : 0;
+            const int64_t blocks = p->run_ks[sgm.rb - 1] + p->run_len[sgm.rb - 1] - p->run_ks[sgm.ra];
+            const Mat Pk = mpow(PF, (int)blocks), Qk = mpow(PR, (int)blocks);
+            for (int i = 0; i < 4; ++i)
+              for (int j = 0; j < 4; ++j) {
+                sgm.P[i * 4 + j] = (double)Pk.a[i][j];
+                sgm.Q[i * 4 + j] = (double)Qk.a[i][j];
+              }
+          }
         }
-      }
+      };
+      // the multi-launch segmented scan (k_seg_fwd / k_seg_bwd)
+      int64_t gmax = 1;
+      for (const auto &G : p->chunks)
+        gmax = std::max<int64_t>(gmax, std::min<int64_t>(lfd::SEG_MAX, (G.r1 - G.r0) / lfd::SEG_MIN_RUNS));
+      p->seg_max = (int)gmax;
+      build_segs(gmax, lfd::SEG_MIN_RUNS, p->segs);
+      // the fused one-launch scan (k_scan_fused): a workgroup of nw_fu waves
+      // per (chunk, 64 channels), one segment of >= 2 runs per wave; 16 waves
+      // when the launch is narrow (<= 512 workgroups: one per CU), else 8
+      p->nw_fu = n_chunks * ((n_ch + 63) / 64) <= 512 ? 16 : 8;
+      build_segs(p->nw_fu, 2, p->segs_fu);
     }
     if (n_off > 0) {
       // per offset d: the output's responses to the states (G0_d, H0_d) and
@@ -1264,6 +1286,12 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
       e = hipMalloc(&p->d_segs, sizeof(lfd::SegGeom) * p->segs.size());
       if (e == hipSuccess)
         e = hipMemcpy(p->d_segs, p->segs.data(), sizeof(lfd::SegGeom) * p->segs.size(), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && !p->segs_fu.empty()) {
+      e = hipMalloc(&p->d_segs_fu, sizeof(lfd::SegGeom) * p->segs_fu.size());
+      if (e == hipSuccess)
+        e = hipMemcpy(p->d_segs_fu, p->segs_fu.data(), sizeof(lfd::SegGeom) * p->segs_fu.size(),
+                      hipMemcpyHostToDevice);
     }
     if (e == hipSuccess && n_off > 0) {
       e = hipMalloc(&p->d_rc_off, sizeof(lfd::RunConst) * n_off);
@@ -1566,7 +1594,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     LFD_HIP(lfd::launch_blend_grid(tmp, p->comp_T, p->n_ch, p->d_bj, p->d_bi, p->d_bw, p->n_blend, y, ys_ch,
                                    ys_t, st, gen));
     if (timed) LFD_HIP(hipEventRecord(ev[2], st));
-    p->last_k1 = p->subs[0]->last_k1;
+    p->last_k1 = p->subs[0]->last_k1.load();
     return LFD_OK;
   }
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
@@ -1604,7 +1632,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
                                         AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st,
                                         reinterpret_cast<double *>(ws + p->off_TR),
                                         reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk, p->d_segs,
-                                        p->seg_max, reinterpret_cast<double *>(ws + p->off_SC)));
+                                        p->seg_max, reinterpret_cast<double *>(ws + p->off_SC), p->d_segs_fu,
+                                        p->nw_fu));
     if (timed) LFD_HIP(hipEventRecord(ev[2], st));
     return LFD_OK;
   }
@@ -1719,7 +1748,7 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
   for (auto *sp : p->subs) lfd_lowpass_plan_destroy(sp);
   if (p->lat) lfd_lowpass_plan_destroy(p->lat);
   for (void *d : {(void *)p->d_bj, (void *)p->d_bi, (void *)p->d_bw, (void *)p->d_bi_lat, (void *)p->d_rc_off,
-                  (void *)p->d_chunks_off, (void *)p->d_segs})
+                  (void *)p->d_chunks_off, (void *)p->d_segs, (void *)p->d_segs_fu})
     if (d) (void)hipFree(d);
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);

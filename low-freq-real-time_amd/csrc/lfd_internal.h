@@ -315,14 +315,16 @@ hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &
                             double *AG, hipStream_t st);
 // Run-mode scan.  With TR / CR / slot_chunk (per run slot: its chunk) the
 // outputs are deferred to k_run_outputs (TR: T entering every run, SR's
-// layout; CR: [chunk][ch64] p0 corrections).
+// layout; CR: [chunk][ch64] p0 corrections).  seg_fu / nw_fu: the fused
+// one-launch segmented scan's table ([n_chunks][nw_fu], nw_fu = 8 or 16).
 hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg_dev, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
                                   float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR = nullptr,
                                   double *CR = nullptr, const int *slot_chunk = nullptr,
-                                  const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr);
+                                  const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr,
+                                  const SegGeom *seg_fu = nullptr, int nw_fu = 0);
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g,
                                     const BlockConst &kc, double *F,

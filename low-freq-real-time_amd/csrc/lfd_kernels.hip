@@ -24,9 +24,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "../../include/lfdas.h"
@@ -488,6 +491,8 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 // 8 the backward run scan.
 #ifdef LFD_DIAG
 __constant__ int g_scan_diag = 0;
+// k_scan_fused phase stamps (LFD_FU_TIMES): [wg < 4096][wave < 16][8]
+__device__ uint64_t g_fu_times[4096 * 16 * 8];
 // K1 unit order (see k_block_runs_mfma; 0 = channel-group-major)
 __constant__ int g_k1_band = 0;
 #endif
@@ -500,91 +505,21 @@ __constant__ int g_k1_band = 0;
 #define LFD_DG(v) 0
 #endif
 
-// DEFER (run mode): the backward run scan only carries T and stores the T
-// entering every run (TR, laid out like SR) and the chunk's p0 correction
-// (CR [chunk][ch64]); k_run_outputs then forms the outputs of every run in
-// parallel.  The per-thread chain is then the 4x4 T recurrence alone: with
-// the outputs inside the chain a 1,250-channel shard spent 2.3 us per run
-// step on one wave per 7 SIMDs.
-// SEGM (segmented chains, run mode with DEFER): 1 = the head only: the state
-// entering run r0 and the FIR-history corrections go to SC, then return (the
-// forward chain is k_seg_fwd's); 2 = the tail only, from the state after the
-// chunk's last run (SC, from k_seg_fwd): pad + tail forward, the reverse over
-// them, the T entering the last run into SC, then return (the backward chain
-// is k_seg_bwd's).  SC layout: [chunk][SC_* slot][ch64].
-constexpr int SC_HS = 0, SC_SE = 4, SC_TE = 8, SC_CORR = 12, SC_N = SC_N_HOST;
-template <int NS, bool RUNS, bool DEFER = false, int DFT = SCAN_DF, int DBT = SCAN_DB, int SEGM = 0>
-__global__ __launch_bounds__(256) void k_chunk_scan(
-    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
-    const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
-    const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
-    int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
-    const double *__restrict__ Y0, double *__restrict__ TR = nullptr, double *__restrict__ CR = nullptr,
-    double *__restrict__ SC = nullptr) {
-  constexpr int N = 2 * NS;
-  constexpr int J = 2 * NS;
-  constexpr int NF = 2 * N + 1;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n_thr = n_chunks * g.n_ch;
-  // run mode: the run-algebra constants live in LDS (read every run step;
-  // from global they put two dependent load latencies on each step)
-  __shared__ RunConst rcs[1];
-  // run-mode output staging: a wave's 64 channels x one run's <= 8 outputs,
-  // written back as 8 rows x 8 consecutive samples per store instruction
-  // instead of 64 scattered 4-B stores (0.2 ms of the cfg3 scan)
-  __shared__ float outs[RUNS ? 4 : 1][64][RUN_R + 1];
-  if constexpr (RUNS) {
-    // the fields this scan reads: PhiFp, PhiRp, C (+ A, B for in-chain
-    // outputs) and KfH — not the whole 12 KB RunConst (a 64-thread group of
-    // a narrow shard loaded 24 doubles per thread before its first step)
-    const double *src = &rg.rc->PhiFp[0][0];
-    double *dst = &rcs[0].PhiFp[0][0];
-    constexpr int n_head = (int)((offsetof(RunConst, A) - offsetof(RunConst, PhiFp)) / sizeof(double));
-    constexpr int n_ab = (int)((offsetof(RunConst, PhiF) - offsetof(RunConst, A)) / sizeof(double));
-    constexpr int o_kfh = (int)((offsetof(RunConst, KfH) - offsetof(RunConst, PhiFp)) / sizeof(double));
-    constexpr int n_copy = n_head + (DEFER ? 0 : n_ab);
-    for (int i = threadIdx.x; i < n_copy; i += blockDim.x) dst[i] = src[i];
-    for (int i = threadIdx.x; i < 4 * HSKIP_MAX; i += blockDim.x) dst[o_kfh + i] = src[o_kfh + i];
-    __syncthreads();
-  }
-  // whole wave active and inside one chunk: outputs leave through LDS (above)
-  const int lane = threadIdx.x & 63;
-  const int64_t tid_w = tid - lane;
-  const bool coal = RUNS && tid_w + 63 < n_thr && tid_w / g.n_ch == (tid_w + 63) / g.n_ch;
-  const int64_t ch_w = tid_w % g.n_ch;
-  if (tid >= n_thr) return;
-  const int64_t ch = tid % g.n_ch;
-  const int64_t c = tid / g.n_ch;
-  const ChunkGeom G = cgs[c];
-  const float *xc = x + ch * s_ch;
-  const int E = padlen;
-  const SeqR<NS> R(sc.r);
-  (void)tp_len;
-  // output blocks: kout0, kout0 + kstep, ... (kstep > 1: sub-blocks)
-  const int kst = (int)G.kstep;
-  auto is_out = [&](int64_t k) {
-    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
-  };
-  auto out_j = [&](int64_t k) -> int64_t {
-    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
-  };
-
-  const int64_t ch64 = (g.n_ch + 63) / 64 * 64;
-  auto sc_at = [&](int slot) -> double & { return SC[(c * SC_N + slot) * ch64 + ch]; };
-  // head / tail / reverse walks: 8 samples' loads issued together (a per-step
-  // load left every step waiting on memory latency: the off-sample grids'
-  // heads and tails are up to L - 1 samples)
+// ---- scan edges (k_chunk_scan and k_scan_fused) ----
+// Left edge of chunk G for channel row xc: SciPy's odd extension (formed in
+// float32, like numpy on float32 input) from the steady state of ext[0], then
+// the chunk's samples before block kb (run mode: or the head skip, see
+// ChunkGeom::hskip).  Leaves S = the forward state entering block kb and corr
+// = the FIR-history corrections of block kb's functionals (K1 used the raw
+// samples before head_end; this chunk saw pad / head values).
+template <int NS, bool RUNS>
+__device__ __forceinline__ void scan_head(const float *__restrict__ xc, int64_t s_t, const ChunkGeom &G, int L, int E,
+                                          const SeqR<NS> &R, const ScanConst &sc, const RunConst *rcl,
+                                          const double *__restrict__ AG, const RunGeom &rg, int64_t ch,
+                                          double (&S)[2 * NS], double (&corr)[4 * NS + 1]) {
+  constexpr int N = 2 * NS, J = 2 * NS, NF = 2 * N + 1;
   constexpr int SB = 8;
-  double S[N], h[J];
-  double corr[NF];
-  const int64_t nF = NF;
-  if constexpr (SEGM == 2) {
-    // (segmented chains) the state after the chunk's last run
-#pragma unroll
-    for (int i = 0; i < N; ++i) S[i] = sc_at(SC_SE + i);
-#pragma unroll
-    for (int i = 0; i < NF; ++i) corr[i] = 0.0;
-  } else {
+  double h[J];
   // ---- left edge: odd extension (float32 like numpy), steady state of ext[0]
   const float xl = xc[G.s0 * s_t];
   // head skip (run mode, ChunkGeom::hskip): the head is block kb-1 without
@@ -593,7 +528,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // with S(lo) the state after the pad's samples before lo: K1 already summed
   // the head.  A null in [lo, s0) (outside this chunk) poisons e_f(kb-1), so
   // such a (chunk, channel) walks its head instead.
-  const int64_t lo_h = G.head_end - g.L;
+  const int64_t lo_h = G.head_end - L;
   bool hs = false;
   if constexpr (RUNS) {
     if (G.hskip && E > 0 && !(LFD_DG(g_scan_diag) & 1)) {
@@ -612,8 +547,8 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   if constexpr (RUNS) {
     if (hs) {
       static_assert(N == RUN_N, "run mode is 4th order");
-      const RunConst &rc = rcs[0];
-      const double *agh = F + ((((ch >> 4) * rg.n_runs) + (G.r0 - 1)) * 8) * 16 + (ch & 15);
+      const RunConst &rc = *rcl;
+      const double *agh = AG + ((((ch >> 4) * rg.n_runs) + (G.r0 - 1)) * 8) * 16 + (ch & 15);
       double ns[N];
 #pragma unroll
       for (int i = 0; i < N; ++i) {
@@ -676,6 +611,176 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     }
   }
 
+}
+
+// Right edge: the tail samples after block ke-1 and SciPy's odd extension,
+// forward from S (the state after the chunk's last full block) into tp
+// (stride tp_stride), then the reverse pass over them from the steady state
+// of the last forward output; the output inside the tail (ChunkGeom::
+// tail_out_j) is stored.  Leaves T = the reverse state entering block ke-1
+// from the right.
+template <int NS>
+__device__ __forceinline__ void scan_tail(const float *__restrict__ xc, int64_t s_t, const ChunkGeom &G, int E,
+                                          const SeqR<NS> &R, const ScanConst &sc, double (&S)[2 * NS],
+                                          double *__restrict__ tp, int64_t tp_stride, float *__restrict__ y,
+                                          int64_t ch, int64_t ys_ch, int64_t ys_t, double (&T)[2 * NS],
+                                          bool store = true) {
+  constexpr int J = 2 * NS;
+  constexpr int SB = 8;
+  double h[J];
+  // ---- right edge: tail samples + odd extension, forward, stored
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int64_t t = G.tail_begin - 1 - j;
+    h[j] = (double)xc[t * s_t];
+  }
+  int64_t ntp = 0;
+  double ylast = 0.0;
+  if (!(LFD_DG(g_scan_diag) & 4)) {
+    int64_t t = G.tail_begin;
+    for (; t + SB <= G.s1 + 1; t += SB) {
+      float xv[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) xv[u] = xc[(t + u) * s_t];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        ylast = R.fwd(S, h, (double)xv[u]);
+        tp[(ntp + u) * tp_stride] = ylast;
+      }
+      ntp += SB;
+    }
+    for (; t <= G.s1; ++t) {
+      ylast = R.fwd(S, h, (double)xc[t * s_t]);
+      tp[(ntp++) * tp_stride] = ylast;
+    }
+  }
+  const float xr = xc[G.s1 * s_t];
+  for (int i = 0; i < E && !(LFD_DG(g_scan_diag) & 4); ++i) {
+    ylast = R.fwd(S, h, (double)(2.0f * xr - xc[(G.s1 - 1 - i) * s_t]));
+    tp[(ntp++) * tp_stride] = ylast;
+  }
+
+  // ---- reverse pass over pad + tail from the steady state of y_f[-1]
+  double qw[J];  // qw[j] = q_last[m+1+j] (future values for the FIR)
+  {
+    const double qss = R.steady(T, ylast, false);
+#pragma unroll
+    for (int j = 0; j < J; ++j) qw[j] = qss;
+  }
+  double y_next = 0.0;  // zero-phase output one sample after the tail output
+  auto rev_step = [&](int64_t i, double v) {
+    const double q = R.rev(T, v);
+    if (G.tail_out_j >= 0 && (G.tail_begin + i == G.tail_out_pos || G.tail_begin + i == G.tail_out_pos + 1)) {
+      double acc = q;  // c[0] = 1
+#pragma unroll
+      for (int j = 1; j <= J; ++j) acc = fma(sc.r.c64[j], qw[j - 1], acc);
+      acc *= sc.r.G;
+      if (G.tail_begin + i == G.tail_out_pos + 1)
+        y_next = acc;
+      else if (store)  // interp1d between the two samples (w = sc.ow)
+        y[ch * ys_ch + G.tail_out_j * ys_t] = (float)fma(sc.ow, y_next - acc, acc);
+    }
+#pragma unroll
+    for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
+    qw[0] = q;
+  };
+  {
+    int64_t i = ntp - 1;
+    for (; i + 1 >= SB; i -= SB) {
+      double tv[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) tv[u] = tp[(i - u) * tp_stride];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) rev_step(i - u, tv[u]);
+    }
+    for (; i >= 0; --i) rev_step(i, tp[i * tp_stride]);
+  }
+
+}
+
+// DEFER (run mode): the backward run scan only carries T and stores the T
+// entering every run (TR, laid out like SR) and the chunk's p0 correction
+// (CR [chunk][ch64]); k_run_outputs then forms the outputs of every run in
+// parallel.  The per-thread chain is then the 4x4 T recurrence alone: with
+// the outputs inside the chain a 1,250-channel shard spent 2.3 us per run
+// step on one wave per 7 SIMDs.
+// SEGM (segmented chains, run mode with DEFER): 1 = the head only: the state
+// entering run r0 and the FIR-history corrections go to SC, then return (the
+// forward chain is k_seg_fwd's); 2 = the tail only, from the state after the
+// chunk's last run (SC, from k_seg_fwd): pad + tail forward, the reverse over
+// them, the T entering the last run into SC, then return (the backward chain
+// is k_seg_bwd's).  SC layout: [chunk][SC_* slot][ch64].
+constexpr int SC_HS = 0, SC_SE = 4, SC_TE = 8, SC_CORR = 12, SC_N = SC_N_HOST;
+template <int NS, bool RUNS, bool DEFER = false, int DFT = SCAN_DF, int DBT = SCAN_DB, int SEGM = 0>
+__global__ __launch_bounds__(256) void k_chunk_scan(
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
+    const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
+    const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
+    int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
+    const double *__restrict__ Y0, double *__restrict__ TR = nullptr, double *__restrict__ CR = nullptr,
+    double *__restrict__ SC = nullptr) {
+  constexpr int N = 2 * NS;
+  constexpr int NF = 2 * N + 1;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n_thr = n_chunks * g.n_ch;
+  // run mode: the run-algebra constants live in LDS (read every run step;
+  // from global they put two dependent load latencies on each step)
+  __shared__ RunConst rcs[1];
+  // run-mode output staging: a wave's 64 channels x one run's <= 8 outputs,
+  // written back as 8 rows x 8 consecutive samples per store instruction
+  // instead of 64 scattered 4-B stores (0.2 ms of the cfg3 scan)
+  __shared__ float outs[RUNS ? 4 : 1][64][RUN_R + 1];
+  if constexpr (RUNS) {
+    // the fields this scan reads: PhiFp, PhiRp, C (+ A, B for in-chain
+    // outputs) and KfH — not the whole 12 KB RunConst (a 64-thread group of
+    // a narrow shard loaded 24 doubles per thread before its first step)
+    const double *src = &rg.rc->PhiFp[0][0];
+    double *dst = &rcs[0].PhiFp[0][0];
+    constexpr int n_head = (int)((offsetof(RunConst, A) - offsetof(RunConst, PhiFp)) / sizeof(double));
+    constexpr int n_ab = (int)((offsetof(RunConst, PhiF) - offsetof(RunConst, A)) / sizeof(double));
+    constexpr int o_kfh = (int)((offsetof(RunConst, KfH) - offsetof(RunConst, PhiFp)) / sizeof(double));
+    constexpr int n_copy = n_head + (DEFER ? 0 : n_ab);
+    for (int i = threadIdx.x; i < n_copy; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 4 * HSKIP_MAX; i += blockDim.x) dst[o_kfh + i] = src[o_kfh + i];
+    __syncthreads();
+  }
+  // whole wave active and inside one chunk: outputs leave through LDS (above)
+  const int lane = threadIdx.x & 63;
+  const int64_t tid_w = tid - lane;
+  const bool coal = RUNS && tid_w + 63 < n_thr && tid_w / g.n_ch == (tid_w + 63) / g.n_ch;
+  const int64_t ch_w = tid_w % g.n_ch;
+  if (tid >= n_thr) return;
+  const int64_t ch = tid % g.n_ch;
+  const int64_t c = tid / g.n_ch;
+  const ChunkGeom G = cgs[c];
+  const float *xc = x + ch * s_ch;
+  const int E = padlen;
+  const SeqR<NS> R(sc.r);
+  (void)tp_len;
+  // output blocks: kout0, kout0 + kstep, ... (kstep > 1: sub-blocks)
+  const int kst = (int)G.kstep;
+  auto is_out = [&](int64_t k) {
+    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
+  };
+  auto out_j = [&](int64_t k) -> int64_t {
+    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
+  };
+
+  const int64_t ch64 = (g.n_ch + 63) / 64 * 64;
+  auto sc_at = [&](int slot) -> double & { return SC[(c * SC_N + slot) * ch64 + ch]; };
+  // (scan_head / scan_tail: the edges' sample walks issue 8 samples' loads
+  // together — a per-step load left every step waiting on memory latency)
+  double S[N];
+  double corr[NF];
+  const int64_t nF = NF;
+  if constexpr (SEGM == 2) {
+    // (segmented chains) the state after the chunk's last run
+#pragma unroll
+    for (int i = 0; i < N; ++i) S[i] = sc_at(SC_SE + i);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) corr[i] = 0.0;
+  } else {
+  scan_head<NS, RUNS>(xc, s_t, G, g.L, E, R, sc, RUNS ? &rcs[0] : nullptr, F, rg, ch, S, corr);
   if (DEFER) CR[c * ((g.n_ch + 63) / 64 * 64) + ch] = corr[2 * N];
   if constexpr (SEGM == 1) {
 #pragma unroll
@@ -754,74 +859,8 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   }
   }  // SEGM != 2
 
-  // ---- right edge: tail samples + odd extension, forward, stored
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int64_t t = G.tail_begin - 1 - j;
-    h[j] = (double)xc[t * s_t];
-  }
-  double *tp = TP + tid;
-  int64_t ntp = 0;
-  double ylast = 0.0;
-  if (!(LFD_DG(g_scan_diag) & 4)) {
-    int64_t t = G.tail_begin;
-    for (; t + SB <= G.s1 + 1; t += SB) {
-      float xv[SB];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) xv[u] = xc[(t + u) * s_t];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        ylast = R.fwd(S, h, (double)xv[u]);
-        tp[(ntp + u) * n_thr] = ylast;
-      }
-      ntp += SB;
-    }
-    for (; t <= G.s1; ++t) {
-      ylast = R.fwd(S, h, (double)xc[t * s_t]);
-      tp[(ntp++) * n_thr] = ylast;
-    }
-  }
-  const float xr = xc[G.s1 * s_t];
-  for (int i = 0; i < E && !(LFD_DG(g_scan_diag) & 4); ++i) {
-    ylast = R.fwd(S, h, (double)(2.0f * xr - xc[(G.s1 - 1 - i) * s_t]));
-    tp[(ntp++) * n_thr] = ylast;
-  }
-
-  // ---- reverse pass over pad + tail from the steady state of y_f[-1]
-  double T[N], qw[J];  // qw[j] = q_last[m+1+j] (future values for the FIR)
-  {
-    const double qss = R.steady(T, ylast, false);
-#pragma unroll
-    for (int j = 0; j < J; ++j) qw[j] = qss;
-  }
-  double y_next = 0.0;  // zero-phase output one sample after the tail output
-  auto rev_step = [&](int64_t i, double v) {
-    const double q = R.rev(T, v);
-    if (G.tail_out_j >= 0 && (G.tail_begin + i == G.tail_out_pos || G.tail_begin + i == G.tail_out_pos + 1)) {
-      double acc = q;  // c[0] = 1
-#pragma unroll
-      for (int j = 1; j <= J; ++j) acc = fma(sc.r.c64[j], qw[j - 1], acc);
-      acc *= sc.r.G;
-      if (G.tail_begin + i == G.tail_out_pos + 1)
-        y_next = acc;
-      else  // interp1d between the two samples (w = sc.ow)
-        y[ch * ys_ch + G.tail_out_j * ys_t] = (float)fma(sc.ow, y_next - acc, acc);
-    }
-#pragma unroll
-    for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
-    qw[0] = q;
-  };
-  {
-    int64_t i = ntp - 1;
-    for (; i + 1 >= SB; i -= SB) {
-      double tv[SB];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) tv[u] = tp[(i - u) * n_thr];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) rev_step(i - u, tv[u]);
-    }
-    for (; i >= 0; --i) rev_step(i, tp[i * n_thr]);
-  }
+  double T[N];
+  scan_tail<NS>(xc, s_t, G, E, R, sc, S, TP + tid, n_thr, y, ch, ys_ch, ys_t, T);
 
   // ---- backward scan, outputs at block starts
   if constexpr (SEGM == 2) {
@@ -4772,6 +4811,379 @@ __global__ __launch_bounds__(1024) void k_seg_bwd(BlockGeom g, const ChunkGeom *
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_scan_fused — the run-mode chunk scan in ONE launch.  A workgroup = one
+// chunk x 64 channels (lane = channel); wave w = segment w of the chunk's
+// runs (SegGeom table: <= NW segments per chunk, segment 0 from run r0):
+//   1. wave 0 runs the left edge (scan_head: S_head and the corrections);
+//      every active wave the forward aggregate of its segment from a zero
+//      state (segment 0 with the forward correction at r0);
+//   2. each wave folds the earlier segments (P_k S + a_k) into S_head and
+//      walks its segment again from that state, writing S_in of every run
+//      (SR); the chunk's last segment's wave then runs the right edge
+//      (scan_tail: T entering the last run from the right, the tail output);
+//   3. each wave the backward aggregate of its segment from a zero T;
+//   4. each wave folds the later segments (Q_k T + b_k) into T_end and walks
+//      its runs backward with the true T, forming the outputs of every run,
+//      y(ks + p) = y0(ks + p) + A[len][p] S_in + B[len-1-p] T_in (+ the
+//      chunk's p0 correction at block kb), staged through LDS so that a store
+//      instruction writes 8 rows x 8 consecutive samples.
+// The same algebra as k_chunk_scan<2, true, true> + k_run_outputs (segment
+// 0 and the last segment bit-identical; the others differ by the combine's
+// summation order, like k_seg_fwd / k_seg_bwd).  A thread's chain is its
+// segment (cfg3: ~5 runs instead of the chunk's ~75, walked twice each way)
+// and the outputs need no second launch: the 1,250-channel share of an
+// 8-GPU cfg3 run spent ~0.1 ms in the two-launch deferred scan.
+// ---------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_scan_fused(
+    const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen, const ScanConst sc,
+    const ChunkGeom *__restrict__ cgs, int64_t n_chunks, RunGeom rg, const SegGeom *__restrict__ sgs,
+    const double *__restrict__ Y0, const double *__restrict__ AG, double *__restrict__ SR,
+    double *__restrict__ TP, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+  constexpr int N = RUN_N, NF = 2 * N + 1;
+#ifdef LFD_DIAG
+  // (diag LFD_FU_TIMES) phase stamps of every wave, 100 MHz s_memrealtime
+  uint64_t *fu_t = g_fu_times + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8;
+  int fu_i = 0;
+#define FU_STAMP()                                                          \
+  do {                                                                      \
+    if (blockIdx.x < 4096) {                                                \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                 \
+      if ((threadIdx.x & 63) == 0) fu_t[fu_i] = t_;                         \
+    }                                                                       \
+    ++fu_i;                                                                 \
+  } while (0)
+#else
+#define FU_STAMP() \
+  do {             \
+  } while (0)
+#endif
+  FU_STAMP();
+  // dynamic LDS (scan_fused_lds bytes; > 64 KB at NW = 16, which a static
+  // allocation may not request): RunConst, the segment aggregates, the edge
+  // states, the corrections, the output staging
+  extern __shared__ double lds_fu[];
+  RunConst &rcs = *reinterpret_cast<RunConst *>(lds_fu);
+  double(*aggf)[N][64] = reinterpret_cast<double(*)[N][64]>(lds_fu + sizeof(RunConst) / sizeof(double));
+  double(*aggb)[N][64] = aggf + NW;
+  double(*edge)[N][64] = aggb + NW;
+  double(*corr)[64] = reinterpret_cast<double(*)[64]>(edge + 2);
+  float(*outs)[64][RUN_R + 1] = reinterpret_cast<float(*)[64][RUN_R + 1]>(corr + NF);
+  for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x)
+    (&rcs.PhiFp[0][0])[i] = (&rg.rc->PhiFp[0][0])[i];
+  const int64_t n_c64 = (g.n_ch + 63) / 64;
+  const int64_t c = blockIdx.x / n_c64, c64 = blockIdx.x % n_c64;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t ch = c64 * 64 + lane;
+  const bool valid = ch < g.n_ch;
+  const int64_t chc = valid ? ch : g.n_ch - 1;
+  const bool full = c64 * 64 + 63 < g.n_ch;  // all 64 lanes valid: staged stores
+  const ChunkGeom G = cgs[c];
+  const SegGeom *sgc = sgs + c * NW;
+  const int64_t ra = sgc[w].ra, rb = sgc[w].rb;
+  const bool act = ra < rb;
+  // the wave that runs the right edge: the chunk's last segment (wave 0 when
+  // the chunk has no full blocks)
+  const bool tailw = act ? sgc[w].last != 0 : (w == 0 && G.r0 >= G.r1);
+  const float *xc = x + chc * s_ch;
+  const SeqR<2> R(sc.r);
+  const double *agb = AG + (((chc >> 4) * rg.n_runs) * 8) * 16 + (chc & 15);
+  const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
+  const int kst = (int)G.kstep;
+  auto is_out = [&](int64_t k) {
+    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
+  };
+  auto out_j = [&](int64_t k) -> int64_t {
+    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
+  };
+  auto sr_at = [&](int64_t r) { return SR + sf_index(G.sr_off + (r - G.r0), 0, chc, rg.n_sr, N); };
+  __syncthreads();
+  FU_STAMP();
+
+  // the chunk's corrections (wave 0's left edge) in LDS: read only at run r0
+  // and block kb, and kept out of the registers of every other step
+  double S[N] = {0.0, 0.0, 0.0, 0.0};
+  // forward walk over this wave's runs from St (STORE: S_in of every run to SR);
+  // 4 runs' inputs loaded together (clamped to the segment)
+  auto fwd_walk = [&](double (&St)[N], bool store) {
+    for (int64_t r4 = ra; r4 < rb; r4 += 4) {
+      double e[4][N];
+      int len[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = min(r4 + u, rb - 1);
+        len[u] = rg.run_len[r];
+#pragma unroll
+        for (int i = 0; i < N; ++i) e[u][i] = agb[(r * 8 + i) * 16];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = r4 + u;
+        if (r >= rb) break;
+        if (store && valid) {
+          double *sr = sr_at(r);
+#pragma unroll
+          for (int i = 0; i < N; ++i) sr[i * SF_ISTRIDE] = St[i];
+        }
+        const double *P = rcs.PhiFp[len[u]];
+        double ns[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          double acc = e[u][i] + (r == G.r0 ? corr[i][lane] : 0.0);
+#pragma unroll
+          for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], St[j], acc);
+          ns[i] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) St[i] = ns[i];
+      }
+    }
+  };
+  // one backward run step: T(ks) = PhiR^len T + E_r + C[len] S_in (+ corr at r0)
+  auto bwd_step = [&](double (&Tt)[N], const double (&sin)[N], const double (&er)[N], int len, int64_t r) {
+    const double *PR = rcs.PhiRp[len], *CC = rcs.C[len];
+    double nr[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double acc = er[i] + (r == G.r0 ? corr[N + i][lane] : 0.0);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        acc = fma(PR[i * 4 + j], Tt[j], acc);
+        acc = fma(CC[i * 4 + j], sin[j], acc);
+      }
+      nr[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) Tt[i] = nr[i];
+  };
+
+  // ---- 1. left edge (wave 0), forward segment aggregates
+  if (w == 0) {
+    double cr[NF];
+    scan_head<2, true>(xc, s_t, G, g.L, padlen, R, sc, &rcs, AG, rg, chc, S, cr);
+#pragma unroll
+    for (int i = 0; i < N; ++i) edge[0][i][lane] = S[i];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) corr[i][lane] = cr[i];
+    // (wave-private until the first __syncthreads: only wave 0 reads them
+    // before it — its own segment 0 holds run r0)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  {
+    double a[N] = {0.0, 0.0, 0.0, 0.0};
+    if (act) fwd_walk(a, false);
+#pragma unroll
+    for (int i = 0; i < N; ++i) aggf[w][i][lane] = a[i];
+  }
+  FU_STAMP();
+  __syncthreads();
+  FU_STAMP();
+
+  // ---- 2. true forward states of the segment's runs; right edge
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) S[i] = edge[0][i][lane];
+    for (int k = 0; k < w; ++k) {
+      if (sgc[k].ra >= sgc[k].rb) continue;
+      const double *P = sgc[k].P;
+      double ns[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double acc = aggf[k][i][lane];
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
+        ns[i] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) S[i] = ns[i];
+    }
+    fwd_walk(S, true);
+  }
+  double T[N] = {0.0, 0.0, 0.0, 0.0};
+  if (tailw) {
+    scan_tail<2>(xc, s_t, G, padlen, R, sc, S, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t,
+                 T, valid);
+#pragma unroll
+    for (int i = 0; i < N; ++i) edge[1][i][lane] = T[i];
+  }
+
+  FU_STAMP();
+  // ---- 3. backward segment aggregates (from a zero T, with the true S_in)
+  {
+    double b[N] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t r4 = rb - 1; act && r4 >= ra; r4 -= 2) {
+      double sv[2][N], ev[2][N];
+      int len[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t r = max(r4 - u, ra);
+        len[u] = rg.run_len[r];
+        const double *sr = sr_at(r);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          sv[u][i] = sr[i * SF_ISTRIDE];
+          ev[u][i] = agb[(r * 8 + 4 + i) * 16];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t r = r4 - u;
+        if (r < ra) break;
+        bwd_step(b, sv[u], ev[u], len[u], r);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) aggb[w][i][lane] = b[i];
+  }
+  FU_STAMP();
+  __syncthreads();
+  FU_STAMP();
+
+  // ---- 4. true reverse states from the right; outputs of every run
+  if (act) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) T[i] = edge[1][i][lane];
+  for (int k = NW - 1; k > w; --k) {
+    if (sgc[k].ra >= sgc[k].rb) continue;
+    const double *Q = sgc[k].Q;
+    double nt[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double acc = aggb[k][i][lane];
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc = fma(Q[i * 4 + j], T[j], acc);
+      nt[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) T[i] = nt[i];
+  }
+  float(*wl)[RUN_R + 1] = outs[w];
+  for (int64_t r2 = rb - 1; r2 >= ra; r2 -= 2) {
+    double sv[2][N], ev[2][N];
+    int len[2];
+    int64_t ksv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t r = max(r2 - u, ra);
+      len[u] = rg.run_len[r];
+      ksv[u] = rg.run_ks[r];
+      const double *sr = sr_at(r);
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        sv[u][i] = sr[i * SF_ISTRIDE];
+        ev[u][i] = agb[(r * 8 + 4 + i) * 16];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t r = r2 - u;
+      if (r < ra) break;
+      const int ln = len[u];
+      const int64_t ks = ksv[u];
+      double yv[RUN_R];
+#pragma unroll
+      for (int pp = 0; pp < RUN_R; ++pp) yv[pp] = y0b[min(ks + pp, g.nb - 1) * 16];
+      float ov[RUN_R];
+#pragma unroll
+      for (int pp = 0; pp < RUN_R; ++pp) {
+        const int64_t k = ks + pp;
+        ov[pp] = 0.f;
+        if (pp >= ln || !is_out(k)) continue;
+        double acc = yv[pp] + (k == G.kb ? corr[2 * N][lane] : 0.0);
+        const double *A = rcs.A[ln][pp];
+        const double *B = rcs.B[ln - 1 - pp];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          acc = fma(A[j], sv[u][j], acc);
+          acc = fma(B[j], T[j], acc);
+        }
+        ov[pp] = (float)acc;
+      }
+      if (full) {
+#pragma unroll
+        for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int e = lane & 7;
+        const int64_t k = ks + e;
+        const bool ok = e < ln && is_out(k);
+        float *yb = y + (c64 * 64) * ys_ch + (ok ? out_j(k) : 0) * ys_t;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const int row = m * 8 + (lane >> 3);
+          const float v = wl[row][e];
+          if (ok) yb[row * ys_ch] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (valid) {
+#pragma unroll
+        for (int pp = 0; pp < RUN_R; ++pp) {
+          const int64_t k = ks + pp;
+          if (pp < ln && is_out(k)) y[ch * ys_ch + out_j(k) * ys_t] = ov[pp];
+        }
+      }
+      bwd_step(T, sv[u], ev[u], ln, r);
+    }
+  }
+  }  // act
+  FU_STAMP();
+#undef FU_STAMP
+}
+
+template <int NW>
+hipError_t launch_scan_fused(unsigned nwg, const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
+                             const ScanConst &sc, const ChunkGeom *cg, int64_t n_chunks, const RunGeom &rg,
+                             const SegGeom *seg_fu, const double *Y0, const double *AG, double *SR, double *TP,
+                             float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+  constexpr size_t lds = sizeof(RunConst) + sizeof(double) * (2 * NW + 2) * RUN_N * 64 +
+                         sizeof(double) * (2 * RUN_N + 1) * 64 + sizeof(float) * NW * 64 * (RUN_R + 1);
+  static_assert(lds <= (size_t)TAP_LDS_MAX, "k_scan_fused LDS");
+  static std::once_flag attr;
+  hipError_t e = hipSuccess;
+  std::call_once(attr, [&] {
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_scan_fused<NW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  });
+  if (e != hipSuccess) return e;
+  k_scan_fused<NW><<<nwg, 64 * NW, lds, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0, AG, SR, TP,
+                                              y, ys_ch, ys_t);
+#ifdef LFD_DIAG
+  if (knob_flag("LFD_FU_TIMES")) {
+    // phase durations (us) averaged over workgroups: per wave slot, stamps
+    // 0 start, 1 RunConst in LDS, 2 phase 1 done, 3 after sync 1, 4 phase 2
+    // (+ tail) done, 5 phase 3 done, 6 after sync 2, 7 end
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    const unsigned nw = std::min(nwg, 4096u);
+    std::vector<uint64_t> t((size_t)nw * 16 * 8);
+    e = hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_fu_times), t.size() * sizeof(uint64_t));
+    if (e != hipSuccess) return e;
+    uint64_t t0 = ~0ull, t1 = 0;
+    for (unsigned b = 0; b < nw; ++b) {
+      t0 = std::min(t0, t[(size_t)b * 16 * 8]);
+      for (int w = 0; w < NW; ++w) t1 = std::max(t1, t[((size_t)b * 16 + w) * 8 + 7]);
+    }
+    for (int w : {0, NW / 2, NW - 1}) {
+      double d[7] = {0};
+      for (unsigned b = 0; b < nw; ++b)
+        for (int i = 0; i < 7; ++i)
+          d[i] += 0.01 * (double)(t[((size_t)b * 16 + w) * 8 + i + 1] - t[((size_t)b * 16 + w) * 8 + i]);
+      fprintf(stderr, "k_scan_fused<%d> wave %2d us: rc %.2f ph1 %.2f sync1 %.2f ph2 %.2f ph3 %.2f sync2 %.2f ph4 %.2f\n",
+              NW, w, d[0] / nw, d[1] / nw, d[2] / nw, d[3] / nw, d[4] / nw, d[5] / nw, d[6] / nw);
+    }
+    fprintf(stderr, "k_scan_fused<%d> first start -> last end %.2f us over %u workgroups\n", NW, 0.01 * (double)(t1 - t0), nw);
+  }
+#endif
+  return hipGetLastError();
+}
+
 // head -> segmented forward -> tail -> segmented backward (CR and the
 // deferred outputs as in the unsegmented deferred scan)
 static hipError_t launch_seg_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
@@ -4810,7 +5222,8 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   const ChunkGeom *cg, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
                                   float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR,
-                                  double *CR, const int *slot_chunk, const SegGeom *seg, int seg_max, double *SC) {
+                                  double *CR, const int *slot_chunk, const SegGeom *seg, int seg_max, double *SC,
+                                  const SegGeom *seg_fu, int nw_fu) {
   // deferred outputs (k_run_outputs) when the scan has few (chunk, channel)
   // threads and is latency-bound: 1,250 ch x 7 chunks (an 8-GPU shard of
   // cfg3) 0.247 -> 0.152 ms, 2,500 ch 0.263 -> 0.191, 5,000 ch equal, 10,000
@@ -4833,6 +5246,15 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     }
   }
 #endif
+  // the fused one-launch segmented scan (option scan_defer = 4)
+  if (seg_fu && (nw_fu == 8 || nw_fu == 16) && option(LFD_OPT_SCAN_DEFER) == 4) {
+    const unsigned nwg = (unsigned)(n_chunks * ((g.n_ch + 63) / 64));
+    hipError_t e = nw_fu == 16 ? launch_scan_fused<16>(nwg, x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0,
+                                                        AG, SR, TP, y, ys_ch, ys_t, st)
+                               : launch_scan_fused<8>(nwg, x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0,
+                                                       AG, SR, TP, y, ys_ch, ys_t, st);
+    return e;
+  }
   // segmented chains (option scan_defer = 3, or automatically for long chains
   // on few threads: >= 128 runs per chunk and < 40,000 (chunk, channel)
   // threads — the 3 kHz lattice line's state scan 0.42 -> 0.31 ms; with

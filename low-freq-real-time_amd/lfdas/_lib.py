@@ -104,6 +104,16 @@ def load():
         raise LFDLibraryError(
             f"{LIB_PATH} not found: the HIP extension is not built (run "
             "__graft_entry__.build()); lfdas has no CPU fallback")
+    # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME
+    # libamdhip64.so.7); loaded first, it also serves this library's NEEDED
+    # libamdhip64.so.7, so torch's streams, graphs and allocations are the
+    # library's own.  Loaded after this library, torch (whose NEEDED entry is
+    # the file name libamdhip64.so) brings a second runtime copy, and whichever
+    # initialises second finds no GPU ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # a torch-free caller: the system runtime alone
+        pass
     try:
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover

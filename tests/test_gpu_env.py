@@ -6,7 +6,7 @@ in liblfdas_diag.so (-DLFD_DIAG, loaded by tools/ through LFDAS_LIB); the
 product reads no environment variable.  This test sets every knob a previous
 round's library honoured — the five invalidating diagnostics included — and
 checks the cfg1 plan (both layouts), the rolling mean, the full-rate filter
-and the FIR decimation against the oracle (relRMS 1e-4 / 1e-6 / 1e-7 / 1e-9)."""
+and the FIR decimation against the oracle (relRMS 1e-4 / 1e-6 / 1e-10 / 1e-9)."""
 import numpy as np
 import pytest
 
@@ -81,7 +81,9 @@ def test_env_knobs_do_not_change_results(monkeypatch, time_major):
     xf = (np.random.default_rng(13).standard_normal((6, 30_000))).astype(np.float32)
     sos = pass_filter_sos(1000.0, 1.0, 10.0)
     got = sosfiltfilt_device(torch.from_numpy(xf).cuda(), sos).cpu().numpy()
-    assert _relrms(got, oracle.sosfiltfilt(sos, xf.astype(np.float64))) < 1e-7  # (1 Hz at 1 kHz: ~5e-9)
+    # float32 samples to the oracle: SciPy forms the odd extension in the input
+    # dtype (_signaltools.py:4684), as the device does
+    assert _relrms(got, oracle.sosfiltfilt(sos, xf)) < 1e-10
     # FIR decimation on the matrix cores (q = 10)
     taps, delay = fir_decimate_design(10)
     got = fir_decimate_device(torch.from_numpy(xf).cuda(), taps, 10, delay).cpu().numpy()

@@ -567,6 +567,40 @@ def test_scan_segmented_chains_match_deferred(cfg):
         assert _relrms(y[:, oa:ob][fr], r[fr]) < 1e-4
 
 
+@pytest.mark.parametrize("cfg", [
+    (500.0, 1.0, 60, 7, 70, 400.0, 0, False, "tc"),          # short chains (~8 runs per chunk), ragged 64-groups
+    (500.0, 1.0, 600, 7, 130, 1500.0, 123_457, False, "tc"),  # off-sample grid, head skip, 3 x 64-groups
+    (1000.0, 10.0, 30, 6, 20, 3000.0, 0, True, "tc"),        # dt = 10 s: long chains (sub-blocks), a null
+    (500.0, 1.0, 600, 7, 64, 1200.0, 0, True, "cc"),         # (time, channel) storage, one full 64-group
+    (250.0, 0.2, 40, 6, 24, 24.0, 0, False, "tc"),           # cfg1 geometry: 1-run chunks
+])
+def test_scan_fused_matches_deferred(cfg):
+    """The fused one-launch segmented scan (option scan_defer = 4:
+    k_scan_fused, one workgroup per chunk x 64 channels, a segment of the
+    run chain per wave, the outputs formed in the backward walk) against the
+    deferred two-launch scan (= 2): the same states up to summation order
+    (relRMS 1e-7 on the float32 outputs, identical NaN footprint), and both
+    against the oracle (1e-4)."""
+    fs, dt_out, P, B, n_ch, dur, off_ns, null, layout = cfg
+    x = (np.random.default_rng(19).standard_normal((n_ch, int(dur * fs))) + 3.0).astype(np.float32)
+    if null:
+        x[3, int(dur * fs) // 3] = np.nan
+    out = {}
+    for mode in (2, 4):
+        with kernel_options(scan_defer=mode):
+            out[mode] = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
+        assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
+    a, b = out[2][0], out[4][0]
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    f = np.isfinite(a)
+    assert _relrms(b[f], a[f]) < 1e-7
+    y, ref, sched = out[4]
+    for (tt, r), (lo, hi, oa, ob) in zip(ref, sched):
+        fr = np.isfinite(r)
+        np.testing.assert_array_equal(np.isnan(y[:, oa:ob]), ~fr)
+        assert _relrms(y[:, oa:ob][fr], r[fr]) < 1e-4
+
+
 @pytest.mark.parametrize("which", ["lo", "head_first", "head_last", "fir_history"])
 def test_offsample_head_skip_nulls(which):
     """Off-sample grids skip the chunk head with K1's one-block run kb-1

@@ -72,7 +72,7 @@ def test_kernel_options_roundtrip_and_validation():
     assert v.value == 0
     assert lib.lfd_set_option(99, 1) == _lib.LFD_EINVAL
     assert lib.lfd_set_option(_lib.OPTIONS["no_runs"], 3) == _lib.LFD_EINVAL
-    assert lib.lfd_set_option(_lib.OPTIONS["scan_defer"], 4) == _lib.LFD_EINVAL
+    assert lib.lfd_set_option(_lib.OPTIONS["scan_defer"], 5) == _lib.LFD_EINVAL
 
 
 def test_design_matches_oracle():

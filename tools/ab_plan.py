@@ -40,6 +40,10 @@ ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--replan", action="store_true", help="rebuild the plan per spec (plan-time knobs)")
 ap.add_argument("--pad", type=int, default=0, help="channel rows padded by this many samples (row stride)")
+ap.add_argument("--alloc-ch", type=int, default=0,
+                help="allocate this many channel rows and run the plan on the first --ch of them "
+                     "(a narrow shard inside a wide allocation: placement vs width)")
+ap.add_argument("--alloc-off", type=int, default=0, help="first channel row of the view (with --alloc-ch)")
 ap.add_argument("specs", nargs="*")
 a = ap.parse_args()
 specs = a.specs or [""]
@@ -51,9 +55,9 @@ if a.tm:
     bench.synth_fill_time_major(xs, a.fs, 77)
     x = xs.t()
 else:
-    xp = torch.empty((a.ch, n + a.pad), dtype=torch.float32, device=dev)
+    xp = torch.empty((max(a.ch + a.alloc_off, a.alloc_ch), n + a.pad), dtype=torch.float32, device=dev)
     bench.synth_fill(xp, a.fs, 77)
-    x = xp[:, :n]
+    x = xp[a.alloc_off:a.alloc_off + a.ch, :n]
 y = torch.empty((a.ch, plan.n_grid), dtype=torch.float32, device=dev)
 wsb = plan.alloc_workspace(dev)
 st = torch.cuda.current_stream(dev)
