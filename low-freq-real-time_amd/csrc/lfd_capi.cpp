@@ -780,7 +780,7 @@ struct lfd_lowpass_plan {
   std::vector<lfd::SegGeom> segs;
   lfd::SegGeom *d_segs = nullptr;
   int seg_max = 0;
-  // the fused one-launch scan (k_scan_fused): [n_chunks][nw_fu] segments
+  // the fused one-launch scan (k_scan_fused): [n_chunks][FU_SEG_HOST] segments
   std::vector<lfd::SegGeom> segs_fu;
   lfd::SegGeom *d_segs_fu = nullptr;
   int nw_fu = 0;
@@ -1180,11 +1180,12 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
         gmax = std::max<int64_t>(gmax, std::min<int64_t>(lfd::SEG_MAX, (G.r1 - G.r0) / lfd::SEG_MIN_RUNS));
       p->seg_max = (int)gmax;
       build_segs(gmax, lfd::SEG_MIN_RUNS, p->segs);
-      // the fused one-launch scan (k_scan_fused): a workgroup of nw_fu waves
-      // per (chunk, 64 channels), one segment of >= 2 runs per wave; 16 waves
-      // when the launch is narrow (<= 512 workgroups: one per CU), else 8
-      p->nw_fu = n_chunks * ((n_ch + 63) / 64) <= 512 ? 16 : 8;
-      build_segs(p->nw_fu, 2, p->segs_fu);
+      // the fused one-launch scan (k_scan_fused): FU_SEG_HOST segments per
+      // chunk, each held in registers (<= FU_SEGR_HOST runs)
+      int64_t nr_max = 0;
+      for (const auto &G : p->chunks) nr_max = std::max<int64_t>(nr_max, G.r1 - G.r0);
+      p->nw_fu = nr_max <= (int64_t)lfd::FU_SEG_HOST * lfd::FU_SEGR_HOST ? lfd::FU_SEG_HOST : 0;
+      if (p->nw_fu) build_segs(lfd::FU_SEG_HOST, 1, p->segs_fu);
     }
     if (n_off > 0) {
       // per offset d: the output's responses to the states (G0_d, H0_d) and

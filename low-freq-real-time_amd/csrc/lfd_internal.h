@@ -191,6 +191,9 @@ constexpr int LAT_MAX_OFF = 8;  // output offsets of a lattice one-pass K1 (MFMA
 // transition across it: powers of one matrix, so the run order does not
 // matter); last = the chunk's last segment.  Inactive slots: ra == rb.
 constexpr int SEG_MAX = 16, SEG_MIN_RUNS = 8;
+// the fused one-launch scan (k_scan_fused): FU_SEG_HOST segments per chunk of
+// <= FU_SEGR_HOST runs (chunks of more runs take the multi-launch scans)
+constexpr int FU_SEG_HOST = 16, FU_SEGR_HOST = 5;
 constexpr int SC_N_HOST = 24;  // doubles per (chunk, channel) of the segmented scan's scratch (k_chunk_scan SC_N)
 struct SegGeom {
   int64_t ra, rb, last;
@@ -316,7 +319,8 @@ hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &
 // Run-mode scan.  With TR / CR / slot_chunk (per run slot: its chunk) the
 // outputs are deferred to k_run_outputs (TR: T entering every run, SR's
 // layout; CR: [chunk][ch64] p0 corrections).  seg_fu / nw_fu: the fused
-// one-launch segmented scan's table ([n_chunks][nw_fu], nw_fu = 8 or 16).
+// one-launch scan's table ([n_chunks][FU_SEG_HOST]; nw_fu = FU_SEG_HOST when
+// every chunk fits, else 0).
 hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g,
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg_dev, int64_t n_chunks, const double *Y0,

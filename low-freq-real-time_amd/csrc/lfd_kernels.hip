@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -62,6 +63,20 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Compute units of the current device, cached per device (256 on MI355X;
+// host launch sizing only)
+int cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
 }
 
 // ---------------------------------------------------------------------------
@@ -491,8 +506,6 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 // 8 the backward run scan.
 #ifdef LFD_DIAG
 __constant__ int g_scan_diag = 0;
-// k_scan_fused phase stamps (LFD_FU_TIMES): [wg < 4096][wave < 16][8]
-__device__ uint64_t g_fu_times[4096 * 16 * 8];
 // K1 unit order (see k_block_runs_mfma; 0 = channel-group-major)
 __constant__ int g_k1_band = 0;
 #endif
@@ -4235,13 +4248,7 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   // full round: the full-rate functionals of 2,000 x 600,000 ran 4,625 units
   // of 32 blocks = 1.13 rounds; 12 blocks make 2.99 rounds)
   const int64_t n_cg = (g.n_ch + 15) / 16;
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, n_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
-      n_cu = 256;
-    slots = 16 * n_cu;
-  }
+  const int slots = 16 * cu_count();
   const int bmax = (int)std::max<int64_t>(1, std::min<int64_t>(MF_RUN, n_cg * g.nb / slots));
   int bpw = bmax;
   {
@@ -4813,45 +4820,58 @@ __global__ __launch_bounds__(1024) void k_seg_bwd(BlockGeom g, const ChunkGeom *
 
 
 // ---------------------------------------------------------------------------
-// k_scan_fused — the run-mode chunk scan in ONE launch.  A workgroup = one
-// chunk x 64 channels (lane = channel); wave w = segment w of the chunk's
-// runs (SegGeom table: <= NW segments per chunk, segment 0 from run r0):
-//   1. wave 0 runs the left edge (scan_head: S_head and the corrections);
-//      every active wave the forward aggregate of its segment from a zero
-//      state (segment 0 with the forward correction at r0);
-//   2. each wave folds the earlier segments (P_k S + a_k) into S_head and
-//      walks its segment again from that state, writing S_in of every run
-//      (SR); the chunk's last segment's wave then runs the right edge
-//      (scan_tail: T entering the last run from the right, the tail output);
-//   3. each wave the backward aggregate of its segment from a zero T;
-//   4. each wave folds the later segments (Q_k T + b_k) into T_end and walks
-//      its runs backward with the true T, forming the outputs of every run,
-//      y(ks + p) = y0(ks + p) + A[len][p] S_in + B[len-1-p] T_in (+ the
-//      chunk's p0 correction at block kb), staged through LDS so that a store
-//      instruction writes 8 rows x 8 consecutive samples.
-// The same algebra as k_chunk_scan<2, true, true> + k_run_outputs (segment
-// 0 and the last segment bit-identical; the others differ by the combine's
-// summation order, like k_seg_fwd / k_seg_bwd).  A thread's chain is its
-// segment (cfg3: ~5 runs instead of the chunk's ~75, walked twice each way)
-// and the outputs need no second launch: the 1,250-channel share of an
-// 8-GPU cfg3 run spent ~0.1 ms in the two-launch deferred scan.
+// k_scan_fused — the run-mode chunk scan in ONE launch, latency-lean.  A
+// 256-thread workgroup = one chunk x 16 channels (one K1 channel group);
+// lane (col = l & 15, s = l >> 4) owns channel col and segment s of the
+// chunk's runs (FU_SEG = 16 segments of <= FU_SEGR runs: SegGeom table).  A
+// lane holds its segment's run inputs in registers, so every chain below is
+// FMAs on registers / LDS and the whole scan costs a handful of memory round
+// trips instead of one per run step:
+//   1. every lane loads its runs' E_f (one round trip); RunConst and the
+//      segments' transitions P / Q go to LDS; segment 0's lanes run the left
+//      edge (scan_head: S_head, the corrections);
+//   2. forward aggregate of the segment from a zero state (segment 0: with
+//      the forward correction at r0), to LDS;
+//   3. S entering the segment = the earlier segments folded into S_head
+//      (P_k S + a_k); the segment again from it: S_in of every run (kept, and
+//      stored to SR); the chunk's last segment's lanes then run the right edge
+//      (scan_tail: T_end, the tail output);
+//   4. E_r loaded; backward aggregate from a zero T, to LDS;
+//   5. T entering the segment from the right (Q_k T + b_k folded into T_end);
+//      the segment backward: T_in of every run to TR;
+//   6. all 256 lanes form the chunk's outputs in parallel, one (run, channel)
+//      per lane and step: y(ks + p) = y0(ks + p) + A[len][p] S_in +
+//      B[len-1-p] T_in (+ the p0 correction at block kb).
+// Same algebra as k_chunk_scan<2, true, true> + k_run_outputs (segment 0 and
+// the last segment bit-identical; the others differ by the combine's
+// summation order, like k_seg_fwd / k_seg_bwd).  Chunks of more than
+// FU_SEG x FU_SEGR runs take the multi-launch scans.
 // ---------------------------------------------------------------------------
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_scan_fused(
+constexpr int FU_SEG = 16;  // segments per chunk (lfd_internal.h FU_SEG_HOST)
+constexpr int FU_SEGR = 5;  // runs per segment held in registers
+static_assert(FU_SEG == FU_SEG_HOST && FU_SEGR == FU_SEGR_HOST, "fused scan geometry");
+#ifdef LFD_DIAG
+// k_scan_fused timing-only variants (LFD_FU_DIAG, results invalid): bit 1 no
+// y stores in the T walk, 2 no y0 loads
+__constant__ int g_fu_diag = 0;
+// k_scan_fused phase stamps (LFD_FU_TIMES): [wg < 8192][wave < 4][8]
+__device__ uint64_t g_fu_times[8192 * 4 * 8];
+#endif
+__global__ __launch_bounds__(256, 2) void k_scan_fused(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen, const ScanConst sc,
     const ChunkGeom *__restrict__ cgs, int64_t n_chunks, RunGeom rg, const SegGeom *__restrict__ sgs,
     const double *__restrict__ Y0, const double *__restrict__ AG, double *__restrict__ SR,
-    double *__restrict__ TP, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
-  constexpr int N = RUN_N, NF = 2 * N + 1;
+    double *__restrict__ TR, double *__restrict__ TP, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+  constexpr int N = RUN_N, NF = 2 * N + 1, SR_ = FU_SEGR;
 #ifdef LFD_DIAG
-  // (diag LFD_FU_TIMES) phase stamps of every wave, 100 MHz s_memrealtime
-  uint64_t *fu_t = g_fu_times + ((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 8;
+  // phase stamps of every wave, 100 MHz s_memrealtime
+  uint64_t *fu_t = g_fu_times + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8;
   int fu_i = 0;
 #define FU_STAMP()                                                          \
   do {                                                                      \
-    if (blockIdx.x < 4096) {                                                \
+    if (blockIdx.x < 8192) {                                                \
       const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                 \
-      if ((threadIdx.x & 63) == 0) fu_t[fu_i] = t_;                         \
+      if ((threadIdx.x & 63) == 0 && fu_i < 8) fu_t[fu_i] = t_;             \
     }                                                                       \
     ++fu_i;                                                                 \
   } while (0)
@@ -4861,93 +4881,110 @@ __global__ __launch_bounds__(64 * NW) void k_scan_fused(
   } while (0)
 #endif
   FU_STAMP();
-  // dynamic LDS (scan_fused_lds bytes; > 64 KB at NW = 16, which a static
-  // allocation may not request): RunConst, the segment aggregates, the edge
-  // states, the corrections, the output staging
-  extern __shared__ double lds_fu[];
-  RunConst &rcs = *reinterpret_cast<RunConst *>(lds_fu);
-  double(*aggf)[N][64] = reinterpret_cast<double(*)[N][64]>(lds_fu + sizeof(RunConst) / sizeof(double));
-  double(*aggb)[N][64] = aggf + NW;
-  double(*edge)[N][64] = aggb + NW;
-  double(*corr)[64] = reinterpret_cast<double(*)[64]>(edge + 2);
-  float(*outs)[64][RUN_R + 1] = reinterpret_cast<float(*)[64][RUN_R + 1]>(corr + NF);
-  for (int i = threadIdx.x; i < (int)(sizeof(RunConst) / sizeof(double)); i += blockDim.x)
-    (&rcs.PhiFp[0][0])[i] = (&rg.rc->PhiFp[0][0])[i];
-  const int64_t n_c64 = (g.n_ch + 63) / 64;
-  const int64_t c = blockIdx.x / n_c64, c64 = blockIdx.x % n_c64;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int64_t ch = c64 * 64 + lane;
+  __shared__ RunConst rcs;
+  __shared__ double Ps[FU_SEG][16], Qs[FU_SEG][16];
+  __shared__ double aggf[FU_SEG][N][16], aggb[FU_SEG][N][16], hS[N][16], tT[N][16], corr[NF][16];
+  __shared__ float otile[4][64][RUN_R + 1];  // output staging per wave
+  __shared__ int64_t omk[4][64];             // its run's first block
+  __shared__ int oml[4][64];                 // its run's length (0: nothing to store)
+  const int64_t n_cg = (g.n_ch + 15) / 16;
+  const int64_t c = blockIdx.x / n_cg, cg = blockIdx.x % n_cg;
+  const int col = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int64_t ch = cg * 16 + col;
   const bool valid = ch < g.n_ch;
   const int64_t chc = valid ? ch : g.n_ch - 1;
-  const bool full = c64 * 64 + 63 < g.n_ch;  // all 64 lanes valid: staged stores
   const ChunkGeom G = cgs[c];
-  const SegGeom *sgc = sgs + c * NW;
-  const int64_t ra = sgc[w].ra, rb = sgc[w].rb;
-  const bool act = ra < rb;
-  // the wave that runs the right edge: the chunk's last segment (wave 0 when
-  // the chunk has no full blocks)
-  const bool tailw = act ? sgc[w].last != 0 : (w == 0 && G.r0 >= G.r1);
-  const float *xc = x + chc * s_ch;
-  const SeqR<2> R(sc.r);
+  const SegGeom *sgc = sgs + c * FU_SEG;
+  const int64_t ra = sgc[sg].ra, rb = sgc[sg].rb;
+  const int nrun = (int)(rb - ra);  // 0 .. FU_SEGR
+  // the lanes that run the right edge: the chunk's last active segment
+  // (segment 0 when the chunk has no full blocks)
+  int tail_seg = 0;
+  for (int k = FU_SEG - 1; k > 0; --k)
+    if (sgc[k].ra < sgc[k].rb) {
+      tail_seg = k;
+      break;
+    }
+  // (lanes past n_ch mirror channel n_ch - 1 bit for bit — its aggregates,
+  // samples and edges — so their tail scratch writes, which share that
+  // channel's TP slots, carry the same values; K1 folds that leave the
+  // padding channels' Y0 / AG unwritten (k_fold_runs) are read nowhere)
   const double *agb = AG + (((chc >> 4) * rg.n_runs) * 8) * 16 + (chc & 15);
-  const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
-  const int kst = (int)G.kstep;
-  auto is_out = [&](int64_t k) {
-    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
-  };
-  auto out_j = [&](int64_t k) -> int64_t {
-    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
-  };
-  auto sr_at = [&](int64_t r) { return SR + sf_index(G.sr_off + (r - G.r0), 0, chc, rg.n_sr, N); };
+  (void)SR;
+  (void)TR;
+  // ---- 1. run inputs (E_f) into registers; constants into LDS; the edges'
+  // sample rows touched (their lines and translations warm when the left /
+  // right edge walks run)
+  const float *xc = x + chc * s_ch;
+  float touch = 0.f;  // (consumed by an empty asm at the end: the load stays in flight)
+  if (sg == 0 || sg == tail_seg) {
+    const int64_t t0 = sg == 0 ? G.s0 : max(G.s0, G.s1 - padlen - 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) touch += xc[min(t0 + 16 * i, G.s1) * s_t];
+  }
+  int len[SR_];
+  double ef[SR_][N];
+#pragma unroll
+  for (int u = 0; u < SR_; ++u) {
+    const int64_t r = u < nrun ? ra + u : G.r0;  // (a clamped, unused load past the segment)
+    len[u] = u < nrun ? rg.run_len[r] : 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) ef[u][i] = agb[(r * 8 + i) * 16];
+  }
+  {
+    // (every load issued before the LDS writes: one round trip)
+    constexpr int NRC = (int)(sizeof(RunConst) / sizeof(double)), NRI = (NRC + 255) / 256;
+    double v[NRI];
+#pragma unroll
+    for (int j = 0; j < NRI; ++j) {
+      const int i = (int)threadIdx.x + 256 * j;
+      v[j] = i < NRC ? (&rg.rc->PhiFp[0][0])[i] : 0.0;
+    }
+    const double pv = sgc[threadIdx.x >> 4].P[threadIdx.x & 15], qv = sgc[threadIdx.x >> 4].Q[threadIdx.x & 15];
+#pragma unroll
+    for (int j = 0; j < NRI; ++j) {
+      const int i = (int)threadIdx.x + 256 * j;
+      if (i < NRC) (&rcs.PhiFp[0][0])[i] = v[j];
+    }
+    (&Ps[0][0])[threadIdx.x] = pv;
+    (&Qs[0][0])[threadIdx.x] = qv;
+  }
   __syncthreads();
   FU_STAMP();
-
-  // the chunk's corrections (wave 0's left edge) in LDS: read only at run r0
-  // and block kb, and kept out of the registers of every other step
+  const SeqR<2> R(sc.r);
   double S[N] = {0.0, 0.0, 0.0, 0.0};
-  // forward walk over this wave's runs from St (STORE: S_in of every run to SR);
-  // 4 runs' inputs loaded together (clamped to the segment)
-  auto fwd_walk = [&](double (&St)[N], bool store) {
-    for (int64_t r4 = ra; r4 < rb; r4 += 4) {
-      double e[4][N];
-      int len[4];
+  if (sg == 0) {
+    double cr[NF];
+    scan_head<2, true>(xc, s_t, G, g.L, padlen, R, sc, &rcs, AG, rg, chc, S, cr);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t r = min(r4 + u, rb - 1);
-        len[u] = rg.run_len[r];
+    for (int i = 0; i < N; ++i) hS[i][col] = S[i];
 #pragma unroll
-        for (int i = 0; i < N; ++i) e[u][i] = agb[(r * 8 + i) * 16];
-      }
+    for (int i = 0; i < NF; ++i) corr[i][col] = cr[i];
+  }
+  // (segment 0's lanes wrote corr themselves: a wave reads its own LDS writes
+  // in order; the other segments never reach run r0)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  auto fstep = [&](double (&St)[N], const double (&e)[N], int ln, int64_t r) {
+    const double *P = rcs.PhiFp[ln];
+    double ns[N];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t r = r4 + u;
-        if (r >= rb) break;
-        if (store && valid) {
-          double *sr = sr_at(r);
+    for (int i = 0; i < N; ++i) {
+      double acc = e[i] + (r == G.r0 ? corr[i][col] : 0.0);
 #pragma unroll
-          for (int i = 0; i < N; ++i) sr[i * SF_ISTRIDE] = St[i];
-        }
-        const double *P = rcs.PhiFp[len[u]];
-        double ns[N];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-          double acc = e[u][i] + (r == G.r0 ? corr[i][lane] : 0.0);
-#pragma unroll
-          for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], St[j], acc);
-          ns[i] = acc;
-        }
-#pragma unroll
-        for (int i = 0; i < N; ++i) St[i] = ns[i];
-      }
+      for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], St[j], acc);
+      ns[i] = acc;
     }
+#pragma unroll
+    for (int i = 0; i < N; ++i) St[i] = ns[i];
   };
-  // one backward run step: T(ks) = PhiR^len T + E_r + C[len] S_in (+ corr at r0)
-  auto bwd_step = [&](double (&Tt)[N], const double (&sin)[N], const double (&er)[N], int len, int64_t r) {
-    const double *PR = rcs.PhiRp[len], *CC = rcs.C[len];
+  auto bstep = [&](double (&Tt)[N], const double (&sin)[N], const double (&er)[N], int ln, int64_t r) {
+    const double *PR = rcs.PhiRp[ln], *CC = rcs.C[ln];
     double nr[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      double acc = er[i] + (r == G.r0 ? corr[N + i][lane] : 0.0);
+      double acc = er[i] + (r == G.r0 ? corr[N + i][col] : 0.0);
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         acc = fma(PR[i * 4 + j], Tt[j], acc);
@@ -4958,227 +4995,202 @@ __global__ __launch_bounds__(64 * NW) void k_scan_fused(
 #pragma unroll
     for (int i = 0; i < N; ++i) Tt[i] = nr[i];
   };
-
-  // ---- 1. left edge (wave 0), forward segment aggregates
-  if (w == 0) {
-    double cr[NF];
-    scan_head<2, true>(xc, s_t, G, g.L, padlen, R, sc, &rcs, AG, rg, chc, S, cr);
-#pragma unroll
-    for (int i = 0; i < N; ++i) edge[0][i][lane] = S[i];
-#pragma unroll
-    for (int i = 0; i < NF; ++i) corr[i][lane] = cr[i];
-    // (wave-private until the first __syncthreads: only wave 0 reads them
-    // before it — its own segment 0 holds run r0)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
+  // ---- 2. forward aggregates
   {
     double a[N] = {0.0, 0.0, 0.0, 0.0};
-    if (act) fwd_walk(a, false);
 #pragma unroll
-    for (int i = 0; i < N; ++i) aggf[w][i][lane] = a[i];
+    for (int u = 0; u < SR_; ++u)
+      if (u < nrun) fstep(a, ef[u], len[u], ra + u);
+#pragma unroll
+    for (int i = 0; i < N; ++i) aggf[sg][i][col] = a[i];
   }
-  FU_STAMP();
   __syncthreads();
   FU_STAMP();
-
-  // ---- 2. true forward states of the segment's runs; right edge
-  if (act) {
+  // ---- 3. true forward states; right edge
+  double sin[SR_][N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) S[i] = edge[0][i][lane];
-    for (int k = 0; k < w; ++k) {
-      if (sgc[k].ra >= sgc[k].rb) continue;
-      const double *P = sgc[k].P;
-      double ns[N];
+  for (int i = 0; i < N; ++i) S[i] = hS[i][col];
+  for (int k = 0; k < sg; ++k) {
+    if (sgc[k].ra >= sgc[k].rb) continue;
+    double ns[N];
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        double acc = aggf[k][i][lane];
+    for (int i = 0; i < N; ++i) {
+      double acc = aggf[k][i][col];
 #pragma unroll
-        for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
-        ns[i] = acc;
-      }
-#pragma unroll
-      for (int i = 0; i < N; ++i) S[i] = ns[i];
+      for (int j = 0; j < N; ++j) acc = fma(Ps[k][i * 4 + j], S[j], acc);
+      ns[i] = acc;
     }
-    fwd_walk(S, true);
-  }
-  double T[N] = {0.0, 0.0, 0.0, 0.0};
-  if (tailw) {
-    scan_tail<2>(xc, s_t, G, padlen, R, sc, S, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t,
-                 T, valid);
 #pragma unroll
-    for (int i = 0; i < N; ++i) edge[1][i][lane] = T[i];
+    for (int i = 0; i < N; ++i) S[i] = ns[i];
   }
-
+#pragma unroll
+  for (int u = 0; u < SR_; ++u) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) sin[u][i] = S[i];
+    if (u < nrun) fstep(S, ef[u], len[u], ra + u);
+  }
+  // the segment's y0 (the E_f registers are free now): in flight behind the
+  // right edge, the backward aggregates and the reverse combine
+  const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
+  double yv[SR_][RUN_R];
+  int64_t ksv[SR_];
+#pragma unroll
+  for (int u = 0; u < SR_; ++u) ksv[u] = u < nrun ? rg.run_ks[ra + u] : 0;
+#pragma unroll
+  for (int u = 0; u < SR_; ++u)
+#pragma unroll
+    for (int pp = 0; pp < RUN_R; ++pp)
+      yv[u][pp] = (u >= nrun || pp >= len[u] || (LFD_DG(g_fu_diag) & 2)) ? 0.0 : y0b[(ksv[u] + pp) * 16];
+  if (sg == tail_seg) {
+    double T[N];
+    scan_tail<2>(xc, s_t, G, padlen, R, sc, S, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t, T,
+                 valid);
+#pragma unroll
+    for (int i = 0; i < N; ++i) tT[i][col] = T[i];
+  }
+  // E_r of the segment's runs (after the right edge: fewer live registers there)
+  double er[SR_][N];
+#pragma unroll
+  for (int u = 0; u < SR_; ++u) {
+    const int64_t r = u < nrun ? ra + u : G.r0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) er[u][i] = agb[(r * 8 + 4 + i) * 16];
+  }
   FU_STAMP();
-  // ---- 3. backward segment aggregates (from a zero T, with the true S_in)
+  // ---- 4. backward aggregates
   {
     double b[N] = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t r4 = rb - 1; act && r4 >= ra; r4 -= 2) {
-      double sv[2][N], ev[2][N];
-      int len[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int64_t r = max(r4 - u, ra);
-        len[u] = rg.run_len[r];
-        const double *sr = sr_at(r);
+    for (int u = SR_ - 1; u >= 0; --u)
+      if (u < nrun) bstep(b, sin[u], er[u], len[u], ra + u);
 #pragma unroll
-        for (int i = 0; i < N; ++i) {
-          sv[u][i] = sr[i * SF_ISTRIDE];
-          ev[u][i] = agb[(r * 8 + 4 + i) * 16];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int64_t r = r4 - u;
-        if (r < ra) break;
-        bwd_step(b, sv[u], ev[u], len[u], r);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) aggb[w][i][lane] = b[i];
+    for (int i = 0; i < N; ++i) aggb[sg][i][col] = b[i];
   }
-  FU_STAMP();
   __syncthreads();
   FU_STAMP();
-
-  // ---- 4. true reverse states from the right; outputs of every run
-  if (act) {
+  // ---- 5. true reverse states; the outputs of every run as its T_in is known
+  const int kst = (int)G.kstep;
+  auto is_out = [&](int64_t k) {
+    return k >= G.kout0 && k < G.kout1 && (kst == 1 || (int)(k - G.kout0) % kst == 0);
+  };
+  auto out_j = [&](int64_t k) -> int64_t {
+    return G.jout0 + (kst == 1 ? k - G.kout0 : (int64_t)((int)(k - G.kout0) / kst));
+  };
+  const double crk = corr[2 * N][col];
+  double T[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) T[i] = edge[1][i][lane];
-  for (int k = NW - 1; k > w; --k) {
+  for (int i = 0; i < N; ++i) T[i] = tT[i][col];
+  for (int k = FU_SEG - 1; k > sg; --k) {
     if (sgc[k].ra >= sgc[k].rb) continue;
-    const double *Q = sgc[k].Q;
     double nt[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      double acc = aggb[k][i][lane];
+      double acc = aggb[k][i][col];
 #pragma unroll
-      for (int j = 0; j < N; ++j) acc = fma(Q[i * 4 + j], T[j], acc);
+      for (int j = 0; j < N; ++j) acc = fma(Qs[k][i * 4 + j], T[j], acc);
       nt[i] = acc;
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) T[i] = nt[i];
   }
-  float(*wl)[RUN_R + 1] = outs[w];
-  for (int64_t r2 = rb - 1; r2 >= ra; r2 -= 2) {
-    double sv[2][N], ev[2][N];
-    int len[2];
-    int64_t ksv[2];
+  FU_STAMP();
+  // outputs leave through a per-wave LDS tile: lane g's 8 outputs of run u
+  // (its channel, its segment's run) go out as 8 lanes x 4 consecutive bytes,
+  // so a store instruction writes 8 row pieces of 32 B (one L2 request each)
+  // instead of 64 scattered 4-B lanes
+  const int wv = threadIdx.x >> 6, ln64 = threadIdx.x & 63;
+  float(*tile)[RUN_R + 1] = otile[wv];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t r = max(r2 - u, ra);
-      len[u] = rg.run_len[r];
-      ksv[u] = rg.run_ks[r];
-      const double *sr = sr_at(r);
+  for (int u = SR_ - 1; u >= 0; --u) {
+    const bool live = u < nrun;
+    const int ln = live ? len[u] : 0;
+    const int64_t ks = ksv[u];
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        sv[u][i] = sr[i * SF_ISTRIDE];
-        ev[u][i] = agb[(r * 8 + 4 + i) * 16];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t r = r2 - u;
-      if (r < ra) break;
-      const int ln = len[u];
-      const int64_t ks = ksv[u];
-      double yv[RUN_R];
-#pragma unroll
-      for (int pp = 0; pp < RUN_R; ++pp) yv[pp] = y0b[min(ks + pp, g.nb - 1) * 16];
-      float ov[RUN_R];
-#pragma unroll
-      for (int pp = 0; pp < RUN_R; ++pp) {
-        const int64_t k = ks + pp;
-        ov[pp] = 0.f;
-        if (pp >= ln || !is_out(k)) continue;
-        double acc = yv[pp] + (k == G.kb ? corr[2 * N][lane] : 0.0);
+    for (int pp = 0; pp < RUN_R; ++pp) {
+      const int64_t k = ks + pp;
+      float o = 0.f;
+      if (pp < ln && is_out(k)) {
+        double acc = yv[u][pp] + (k == G.kb ? crk : 0.0);
         const double *A = rcs.A[ln][pp];
         const double *B = rcs.B[ln - 1 - pp];
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-          acc = fma(A[j], sv[u][j], acc);
+          acc = fma(A[j], sin[u][j], acc);
           acc = fma(B[j], T[j], acc);
         }
-        ov[pp] = (float)acc;
+        o = (float)acc;
       }
-      if (full) {
-#pragma unroll
-        for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int e = lane & 7;
-        const int64_t k = ks + e;
-        const bool ok = e < ln && is_out(k);
-        float *yb = y + (c64 * 64) * ys_ch + (ok ? out_j(k) : 0) * ys_t;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const int row = m * 8 + (lane >> 3);
-          const float v = wl[row][e];
-          if (ok) yb[row * ys_ch] = v;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else if (valid) {
-#pragma unroll
-        for (int pp = 0; pp < RUN_R; ++pp) {
-          const int64_t k = ks + pp;
-          if (pp < ln && is_out(k)) y[ch * ys_ch + out_j(k) * ys_t] = ov[pp];
-        }
-      }
-      bwd_step(T, sv[u], ev[u], ln, r);
+      tile[ln64][pp] = o;
     }
+    omk[wv][ln64] = ks;
+    oml[wv][ln64] = valid ? ln : 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int e = ln64 & 7;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int gl = m * 8 + (ln64 >> 3);  // source lane: channel cg*16 + (gl & 15)
+      const int64_t kg = omk[wv][gl] + e;
+      const bool ok = e < oml[wv][gl] && is_out(kg) && !(LFD_DG(g_fu_diag) & 1);
+      if (ok) y[(cg * 16 + (gl & 15)) * ys_ch + out_j(kg) * ys_t] = tile[gl][e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (live) bstep(T, sin[u], er[u], ln, ra + u);
   }
-  }  // act
   FU_STAMP();
 #undef FU_STAMP
+  asm volatile("" ::"v"(touch));
 }
 
-template <int NW>
-hipError_t launch_scan_fused(unsigned nwg, const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
+hipError_t launch_scan_fused(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
                              const ScanConst &sc, const ChunkGeom *cg, int64_t n_chunks, const RunGeom &rg,
-                             const SegGeom *seg_fu, const double *Y0, const double *AG, double *SR, double *TP,
-                             float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
-  constexpr size_t lds = sizeof(RunConst) + sizeof(double) * (2 * NW + 2) * RUN_N * 64 +
-                         sizeof(double) * (2 * RUN_N + 1) * 64 + sizeof(float) * NW * 64 * (RUN_R + 1);
-  static_assert(lds <= (size_t)TAP_LDS_MAX, "k_scan_fused LDS");
-  static std::once_flag attr;
-  hipError_t e = hipSuccess;
-  std::call_once(attr, [&] {
-    e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_scan_fused<NW>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  });
-  if (e != hipSuccess) return e;
-  k_scan_fused<NW><<<nwg, 64 * NW, lds, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0, AG, SR, TP,
-                                              y, ys_ch, ys_t);
+                             const SegGeom *seg_fu, const double *Y0, const double *AG, double *SR, double *TR,
+                             double *TP, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+  const unsigned nwg = (unsigned)(n_chunks * ((g.n_ch + 15) / 16));
+#ifdef LFD_DIAG
+  {
+    static int fu_diag = -1;
+    const char *v = knob("LFD_FU_DIAG");
+    const int want = v ? std::atoi(v) : 0;
+    if (want != fu_diag) {
+      hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_fu_diag), &want, sizeof(int));
+      if (e != hipSuccess) return e;
+      fu_diag = want;
+    }
+  }
+#endif
+  k_scan_fused<<<nwg, 256, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0, AG, SR, TR, TP, y,
+                                    ys_ch, ys_t);
 #ifdef LFD_DIAG
   if (knob_flag("LFD_FU_TIMES")) {
-    // phase durations (us) averaged over workgroups: per wave slot, stamps
-    // 0 start, 1 RunConst in LDS, 2 phase 1 done, 3 after sync 1, 4 phase 2
-    // (+ tail) done, 5 phase 3 done, 6 after sync 2, 7 end
-    e = hipStreamSynchronize(st);
+    // phase durations (us) averaged over workgroups: per wave, stamps 0
+    // start, 1 constants + E_f loaded, 2 forward aggregates (+ left edge),
+    // 3 forward walk (+ right edge, E_r issued), 4 backward aggregates, 5 T
+    // walk + outputs, 6 (unused)
+    hipError_t e = hipStreamSynchronize(st);
     if (e != hipSuccess) return e;
-    const unsigned nw = std::min(nwg, 4096u);
-    std::vector<uint64_t> t((size_t)nw * 16 * 8);
+    const unsigned nw = std::min(nwg, 8192u);
+    std::vector<uint64_t> t((size_t)nw * 4 * 8);
     e = hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_fu_times), t.size() * sizeof(uint64_t));
     if (e != hipSuccess) return e;
     uint64_t t0 = ~0ull, t1 = 0;
-    for (unsigned b = 0; b < nw; ++b) {
-      t0 = std::min(t0, t[(size_t)b * 16 * 8]);
-      for (int w = 0; w < NW; ++w) t1 = std::max(t1, t[((size_t)b * 16 + w) * 8 + 7]);
-    }
-    for (int w : {0, NW / 2, NW - 1}) {
-      double d[7] = {0};
+    for (unsigned b = 0; b < nw; ++b)
+      for (int w = 0; w < 4; ++w) {
+        t0 = std::min(t0, t[((size_t)b * 4 + w) * 8]);
+        t1 = std::max(t1, t[((size_t)b * 4 + w) * 8 + 6]);
+      }
+    for (int w = 0; w < 4; ++w) {
+      double d[6] = {0};
       for (unsigned b = 0; b < nw; ++b)
-        for (int i = 0; i < 7; ++i)
-          d[i] += 0.01 * (double)(t[((size_t)b * 16 + w) * 8 + i + 1] - t[((size_t)b * 16 + w) * 8 + i]);
-      fprintf(stderr, "k_scan_fused<%d> wave %2d us: rc %.2f ph1 %.2f sync1 %.2f ph2 %.2f ph3 %.2f sync2 %.2f ph4 %.2f\n",
-              NW, w, d[0] / nw, d[1] / nw, d[2] / nw, d[3] / nw, d[4] / nw, d[5] / nw, d[6] / nw);
+        for (int i = 0; i < 6; ++i)
+          d[i] += 0.01 * (double)(t[((size_t)b * 4 + w) * 8 + i + 1] - t[((size_t)b * 4 + w) * 8 + i]);
+      fprintf(stderr, "k_scan_fused wave %d us: load %.2f fagg+head %.2f fwalk+tail %.2f bagg %.2f combine %.2f "
+              "twalk+out %.2f\n", w, d[0] / nw, d[1] / nw, d[2] / nw, d[3] / nw, d[4] / nw, d[5] / nw);
     }
-    fprintf(stderr, "k_scan_fused<%d> first start -> last end %.2f us over %u workgroups\n", NW, 0.01 * (double)(t1 - t0), nw);
+    fprintf(stderr, "k_scan_fused first start -> last end %.2f us over %u workgroups\n", 0.01 * (double)(t1 - t0), nw);
   }
 #endif
   return hipGetLastError();
@@ -5246,15 +5258,17 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     }
   }
 #endif
-  // the fused one-launch segmented scan (option scan_defer = 4)
-  if (seg_fu && (nw_fu == 8 || nw_fu == 16) && option(LFD_OPT_SCAN_DEFER) == 4) {
-    const unsigned nwg = (unsigned)(n_chunks * ((g.n_ch + 63) / 64));
-    hipError_t e = nw_fu == 16 ? launch_scan_fused<16>(nwg, x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0,
-                                                        AG, SR, TP, y, ys_ch, ys_t, st)
-                               : launch_scan_fused<8>(nwg, x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0,
-                                                       AG, SR, TP, y, ys_ch, ys_t, st);
-    return e;
-  }
+  // the fused one-launch segmented scan (option scan_defer = 4; by default
+  // when its (chunk, 16-channel) workgroups fit the chip at once, <= 3 per CU:
+  // latency-bound narrow shards — 1,250 channels x 7 chunks (an 8-GPU share
+  // of cfg3): 0.109 -> 0.087 ms; from 2,500 channels (two rounds of
+  // workgroups) the two-launch deferred scan is as fast or faster,
+  // profiles/r05_scan_fused.txt)
+  const int64_t o_scan = option(LFD_OPT_SCAN_DEFER);
+  const bool fused_fits = n_chunks * ((g.n_ch + 15) / 16) <= 3 * (int64_t)cu_count();
+  if (seg_fu && nw_fu == FU_SEG && TR && (o_scan == 4 || (o_scan == 0 && fused_fits)))
+    return launch_scan_fused(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0, AG, SR, TR, TP, y, ys_ch,
+                             ys_t, st);
   // segmented chains (option scan_defer = 3, or automatically for long chains
   // on few threads: >= 128 runs per chunk and < 40,000 (chunk, channel)
   // threads — the 3 kHz lattice line's state scan 0.42 -> 0.31 ms; with

@@ -88,6 +88,10 @@ class LowpassPlan:
     def close(self):
         if getattr(self, "_h", None):
             if getattr(self, "_owned", True):
+                # views handed out by lattice() die with the plan that owns
+                # their C handle
+                for v in getattr(self, "_views", ()):
+                    v._h = None
                 self._lib.lfd_lowpass_plan_destroy(self._h)
             self._h = None
 
@@ -182,6 +186,8 @@ class LowpassPlan:
             view._lib = self._lib
             view._h = inner
             view._owned = False  # owned by this plan
+            view._parent = self  # the parent (owner of the C handle) outlives the view
+            self.__dict__.setdefault("_views", []).append(view)
             view.chunks = self.chunks
             view.n_ch, view.n_t = self.n_ch, self.n_t
         return int(n.value), bool(last.value), view

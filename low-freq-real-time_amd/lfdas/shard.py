@@ -53,6 +53,22 @@ def all_gather_channels(y_local, n_ch: int, group=None):
     return torch.cat(parts, 0)[:n_ch]
 
 
+def gather_channels_to_root(y_local, n_ch: int, group=None, root: int = 0):
+    """Gather every rank's (n_local, n_out) block into (n_ch, n_out) on rank
+    ``root`` only (RCCL gather over xGMI on backend "nccl"); other ranks get
+    ``None``.  Padded to ceil(n_ch/world) rows like ``all_gather_channels``."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    per = -(-int(n_ch) // world)
+    pad = torch.zeros((per,) + tuple(y_local.shape[1:]), dtype=y_local.dtype, device=y_local.device)
+    pad[: y_local.shape[0]] = y_local
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == root else None
+    dist.gather(pad, parts, dst=root, group=group)
+    return torch.cat(parts, 0)[:n_ch] if rank == root else None
+
+
 def shard_spool(sp, world: int, rank: int):
     """Rank ``rank``'s contiguous channel block of a spool, as
     ``Spool.select(distance=(d[c0], d[c1 - 1]))`` (inclusive, DASCore);
@@ -108,15 +124,21 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
     """``LFProc(sp).process_time_range(bgtime, edtime)`` over the ranks of the
     default process group: rank r processes channel block r (``shard_spool``)
     with ``run_shard(sub_spool, bgtime, edtime, params)`` (default
-    ``lfproc_shard``: the device plan), the decimated outputs of every chunk
-    are all-gathered — float32 and HBM to HBM over RCCL on backend "nccl"
-    (one device→host copy of the gathered block after it), through host
-    memory on gloo — and rank 0 writes
-    the reference's files (``LFDAS_<t0>_<t1>.h5``, lf_das.py:230-232) into
-    ``output_folder``.  Returns the full-width output patches (every rank when
-    ``gather``; else this rank's own block).  A failure on any rank (e.g. the
-    gap exception of lf_das.py:18) is raised on every rank, after the
-    collective, so no rank is left waiting."""
+    ``lfproc_shard``: the device plan), and rank 0 writes the reference's
+    full-width files (``LFDAS_<t0>_<t1>.h5``, lf_das.py:230-232) into
+    ``output_folder``.  The decimated float32 outputs move HBM to HBM over
+    RCCL on backend "nccl" (through host memory on gloo):
+
+    * ``gather=True`` (default): gathered to rank 0 only, the one rank that
+      writes; rank 0 returns the full-width patches (one device→host copy of
+      the full block, on rank 0 alone), every other rank its own block's;
+    * ``gather="all"``: all-gathered; every rank returns the full width;
+    * ``gather=False``: no collective; every rank returns its own block (and
+      nothing is written unless the run has one rank).
+
+    A failure on any rank (e.g. the gap exception of lf_das.py:18) is raised
+    on every rank, after the agreement collective, so no rank is left
+    waiting."""
     import torch
 
     from . import schedule as S
@@ -158,14 +180,22 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
         raise err
     else:
         dtype = blk.dtype
+    if gather not in (True, False, "all"):
+        raise ValueError('gather must be True (to rank 0), "all" or False')
+    full = None
     if world > 1 and gather:
         # HBM to HBM over RCCL (backend "nccl"); host tensors over gloo
         t = blk.to(device=_comm_device(group), dtype=dtype)
-        full = all_gather_channels(t, n_ch, group=group).cpu().numpy()
-        dist_coords = np.asarray(p0.coords["distance"])
-    else:
+        if gather == "all":
+            full = all_gather_channels(t, n_ch, group=group).cpu().numpy()
+        else:
+            g = gather_channels_to_root(t, n_ch, group=group)
+            full = g.cpu().numpy() if g is not None else None
+    full_width = full is not None or world == 1
+    if full is None:
         full = blk.cpu().numpy()
-        dist_coords = np.asarray(sub[0].coords["distance"]) if sub is not None else np.zeros(0)
+    dist_coords = (np.asarray(p0.coords["distance"]) if full_width and world > 1 else
+                   np.asarray(sub[0].coords["distance"]) if sub is not None else np.zeros(0))
     res = []
     j = 0
     attrs = p0._attrs_wo_coords()
@@ -177,7 +207,7 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
         out = Patch(data=seg.T.copy() if tdim == 0 else seg, coords=coords, dims=p0.dims,
                     attrs=attrs).update_attrs(d_time=para["output_sample_interval"])
         res.append(out)
-        if rank == 0 and output_folder and (world == 1 or gather):
+        if rank == 0 and output_folder and full_width:
             if verbose:  # the reference's messages (lf_das.py:263,276,290)
                 if kinds[i - 1] == "tail":
                     print(f"Processing patch {i} (Last portion of data)")

@@ -68,17 +68,22 @@ def _sharded_worker(rank, world, port, out_dir, out_q):
     sp = dc.get_example_spool()  # 3 x (300 ch x 2000) @ 250 Hz
     sub, (c0, c1) = shard_spool(sp, world, rank)
     assert sub[0].shape[0] == c1 - c0
+    # default: gathered to rank 0 only (the writer); the others keep their block
     outs = process_time_range_sharded(sp, T1, T2, PARAMS, output_folder=out_dir, run_shard=_oracle_shard,
                                       verbose=False)
-    out_q.put((rank, (c0, c1), [(o.coords["time"].astype(np.int64), o.data) for o in outs]))
+    # gather="all": every rank full width
+    outs_all = process_time_range_sharded(sp, T1, T2, PARAMS, run_shard=_oracle_shard, gather="all", verbose=False)
+    out_q.put((rank, (c0, c1), [(o.coords["time"].astype(np.int64), o.data) for o in outs],
+               [(o.coords["time"].astype(np.int64), o.data) for o in outs_all]))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_gloo_world3_sharded_lfproc_driver(tmp_path):
     """process_time_range_sharded over 3 gloo ranks (300 channels: 100 each):
-    every rank gets the full-width outputs of every chunk, equal to one
-    process over the whole spool; rank 0 wrote the reference's files."""
+    rank 0 gets the full-width outputs of every chunk (the others their own
+    100-channel block), equal to one process over the whole spool, and wrote
+    the reference's files; with gather="all" every rank gets the full width."""
     here = os.path.dirname(os.path.abspath(__file__))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -98,14 +103,18 @@ def test_gloo_world3_sharded_lfproc_driver(tmp_path):
     import lfdas.dc as dc
     sp = dc.get_example_spool()
     ref = _oracle_shard(dc.spool(sp), T1, T2, PARAMS)
-    assert sorted(r for r, _, _ in got) == [0, 1, 2]
-    assert [c for _, c, _ in sorted(got, key=lambda g: g[0])] == [(0, 100), (100, 200), (200, 300)]
-    for _, _, outs in got:
-        assert len(outs) == len(ref) == 4
-        for (t, d), r in zip(outs, ref):
+    assert sorted(r for r, _, _, _ in got) == [0, 1, 2]
+    assert [c for _, c, _, _ in sorted(got, key=lambda g: g[0])] == [(0, 100), (100, 200), (200, 300)]
+    for rank, (c0, c1), outs, outs_all in got:
+        assert len(outs) == len(outs_all) == len(ref) == 4
+        for (t, d), (ta, da), r in zip(outs, outs_all, ref):
             np.testing.assert_array_equal(t, r.coords["time"].astype(np.int64))
-            assert d.shape == (300, len(t))
-            np.testing.assert_allclose(d, r.data, rtol=0, atol=1e-12)
+            np.testing.assert_array_equal(ta, t)
+            assert da.shape == (300, len(t))
+            np.testing.assert_allclose(da, r.data, rtol=0, atol=1e-12)
+            want = r.data if rank == 0 else r.data[c0:c1]
+            assert d.shape == want.shape
+            np.testing.assert_allclose(d, want, rtol=0, atol=1e-12)
     files = sorted(os.listdir(out_dir))
     assert len(files) == 4 and all(f.startswith("LFDAS_2017-09-18T") for f in files)
     back = dc.spool(out_dir)

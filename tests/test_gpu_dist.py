@@ -43,7 +43,7 @@ def _rank(rank, world, port, out_dir, gap, dims, q):
         n0 = PL.launch_count
         try:
             outs = process_time_range_sharded(sp, T1, T2, PARAMS, output_folder=out_dir, device="cuda:0",
-                                              verbose=False)
+                                              gather="all", verbose=False)
             q.put((rank, "ok", PL.launch_count - n0,
                    [(o.coords["time"].astype(np.int64), o.data, o.dims) for o in outs]))
         except Exception as e:  # the agreed error, raised on every rank

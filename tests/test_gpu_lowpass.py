@@ -573,6 +573,7 @@ def test_scan_segmented_chains_match_deferred(cfg):
     (1000.0, 10.0, 30, 6, 20, 3000.0, 0, True, "tc"),        # dt = 10 s: long chains (sub-blocks), a null
     (500.0, 1.0, 600, 7, 64, 1200.0, 0, True, "cc"),         # (time, channel) storage, one full 64-group
     (250.0, 0.2, 40, 6, 24, 24.0, 0, False, "tc"),           # cfg1 geometry: 1-run chunks
+    (250.0, 0.2, 40, 6, 37, 24.0, 0, False, "fold"),         # recurrence K1 + fold (padding channels unwritten)
 ])
 def test_scan_fused_matches_deferred(cfg):
     """The fused one-launch segmented scan (option scan_defer = 4:
@@ -586,10 +587,11 @@ def test_scan_fused_matches_deferred(cfg):
     if null:
         x[3, int(dur * fs) // 3] = np.nan
     out = {}
+    fold = layout == "fold"
     for mode in (2, 4):
-        with kernel_options(scan_defer=mode):
-            out[mode] = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
-        assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
+        with kernel_options(scan_defer=mode, k1_recurrence=int(fold)):
+            out[mode] = _run(x, fs, dt_out, P, B, "tc" if fold else layout, off_ns=off_ns)
+        assert _run.last_kernel == {"tc": "mfma_runs", "cc": "mfma_runs_tm", "fold": "recurrence_fold"}[layout]
     a, b = out[2][0], out[4][0]
     np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
     f = np.isfinite(a)
