@@ -3231,7 +3231,7 @@ struct LatAcc {
   double S0 = 0.0, T1 = 0.0, v0 = 0.0, ya = 0.0, yb = 0.0;
 };
 template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
-          bool PERSIST = false, bool LAT = false>
+          bool PERSIST = false, bool LAT = false, bool WGCG = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -3257,7 +3257,12 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   double *wb = Ks + ntab + RUN_CST + wave * RUN_WB;
   (void)wb;
   const int64_t n_cg = (g.n_ch + 15) / 16;
-  const int64_t n_units = n_cg * rg.n_groups;
+  // WGCG: the workgroup's waves share one channel group (consecutive time
+  // groups of it), workgroups walk the channel groups fastest: a CU's
+  // concurrent sample rows are 2 x 16 instead of 2 x 8 x 16, and rows of one
+  // group are translated once for its 8 waves (TLB reach)
+  constexpr int WPG = NT / 64;
+  const int64_t n_units = WGCG ? n_cg * ((rg.n_groups + WPG - 1) / WPG) * WPG : n_cg * rg.n_groups;
   const int64_t wave_slots = (int64_t)gridDim.x * (blockDim.x >> 6);
   int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   const int lane0 = lane;
@@ -3278,6 +3283,15 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const int64_t rem = unit - b * band * rg.n_groups;
     grp = rem / bw;
     cg = base + rem % bw;
+  } else if constexpr (WGCG) {
+    const int64_t blk = unit / WPG;
+    cg = blk % n_cg;
+    grp = (blk / n_cg) * WPG + unit % WPG;
+    if (grp >= rg.n_groups) {  // (the last time-group row of a channel group)
+      if constexpr (!PERSIST) break;
+      unit += wave_slots;
+      continue;
+    }
   } else {
     cg = unit % n_cg;
     grp = unit / n_cg;
@@ -4303,7 +4317,7 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
 }
 
 template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
-          bool PERSIST = false, bool LAT = false>
+          bool PERSIST = false, bool LAT = false, bool WGCG = false>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
@@ -4311,7 +4325,8 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   const size_t lds = (SEPI || LAT) ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
                           : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  auto kern = &k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI, PERSIST, LAT>;
+  auto kern = &k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI, PERSIST, LAT, WGCG>;
+  if constexpr (WGCG) units = ((g.n_ch + 15) / 16) * ((rg.n_groups + W - 1) / W) * W;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -4399,6 +4414,9 @@ hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, 
       // measured slower at every width (1,250 ch 1.98 vs 1.65 ms, 10,000 ch
       // 14.8 vs 13.6 ms; profiles/r04_ab_k1_persist_*.txt): the unit loop
       // spills 30 VGPRs under the 128-register cap into the sample loop
+      if (knob_flag("LFD_K1_WGCG"))
+        return run_k1<1, 0, 512, false, 4, false, false, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG,
+                                                                             units, st);
       const char *pv = knob("LFD_K1_PERSIST");
       if (pv && std::atoi(pv) != 0)
         return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
