@@ -110,6 +110,11 @@ def launch_or_check(args) -> int | None:
     return subprocess.call(cmd)
 
 
+def device_samples(shape, device):
+    from lfdas.arena import device_samples as ds
+    return ds(shape, device=device)
+
+
 def synth_fill(x, fs, seed):
     """x[c, t] = 0.5 + sin(2*pi*0.05*t/fs + phi_c) + N(0,1), generated on the
     device in channel slices (synthetic; there is no dataset)."""
@@ -206,7 +211,7 @@ def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_majo
         synth_fill_time_major(xs, fs, 77)
         x = xs.t()
     else:
-        x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
+        x = device_samples((n_ch, n), device=dev)
         synth_fill(x, fs, 77)
     y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
     wsb = plan.alloc_workspace(dev)
@@ -790,7 +795,10 @@ def main():
     n_ch = c1 - c0
     plan, sched, sos, t0, dt_ns, tg = build_plan(n_ch, n, args.fs, args.dt_out, args.patch_size,
                                                  args.edge_buff)
-    x = torch.empty((n_ch, n), dtype=torch.float32, device=dev)
+    # the product's sample buffer (lfdas.arena: a rank's 9 GB shard of an
+    # N = 8 run sits in a >= 32 GiB allocation, the translation-friendly
+    # placement; the 72 GB single-GPU input is that size already)
+    x = device_samples((n_ch, n), device=dev)
     synth_fill(x, args.fs, 1234 + rank)
     y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
     wsb = plan.alloc_workspace(dev)
@@ -865,7 +873,7 @@ def main():
         else:
             (o0, o1), o_tot, o_key = channel_range(args.channels, ws, rank), args.channels, "strong_scaling_cfg3"
         plan_w, _, _, _, _, _ = build_plan(o1 - o0, n, args.fs, args.dt_out, args.patch_size, args.edge_buff)
-        xw = torch.empty((o1 - o0, n), dtype=torch.float32, device=dev)
+        xw = device_samples((o1 - o0, n), device=dev)
         synth_fill(xw, args.fs, 4321 + rank)
         yw = torch.empty((o1 - o0, plan_w.n_grid), dtype=torch.float32, device=dev)
         ww = plan_w.alloc_workspace(dev)

@@ -506,8 +506,6 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 // 8 the backward run scan.
 #ifdef LFD_DIAG
 __constant__ int g_scan_diag = 0;
-// K1 unit order (see k_block_runs_mfma; 0 = channel-group-major)
-__constant__ int g_k1_band = 0;
 #endif
 // LFD_DG(v): a diagnostic / A/B value, the constant 0 in the production
 // build (-DLFD_DIAG builds liblfdas_diag.so for tools/), so every branch it
@@ -2940,39 +2938,6 @@ __device__ __forceinline__ void mf_iter(const double *kt, int kstride, bool colv
   }
 }
 
-// The same 16 MFMA steps on v_mfma_f64_4x4x4_4b: 4 blocks of 4x4x4, block b
-// = lanes with (l >> 2) & 3 == b.  Its operands share the 16x16x4 layout's
-// lane mapping (measured, tools/check_mfma4x4.hip): A[i][k] at lane 16k + 4b
-// + i, B[k][j] at lane 16k + 4b + j, D[i][j] at lane 16i + 4b + j.  So with
-// B = this lane's sample (k = q, channel 4b + j = col) unchanged, MFMA m
-// with A = taps of functional 4m + (l & 3) leaves functional 4m + q of
-// channel col on the lane — acc0/acc1's row q + 4m.  Three of them cover the
-// 9 functionals (12 rows; 16x16x4 computes 16): 3 x 18.5 vs 86.6 cycles per
-// step at 4 waves / SIMD (tools/ubench_mfma64b.hip).  kt[m]: the lane's tap
-// column for functional 4m + (l & 3) (clamped to nc - 1).
-__device__ __forceinline__ void mf_iter4(const double *const (&kt)[3], int kstride, const f4v (&cur)[4],
-                                         double (&acc)[2][3]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    double a[3][4];
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const double2 b01 = *reinterpret_cast<const double2 *>(kt[m] + j * kstride);
-      const double2 b23 = *reinterpret_cast<const double2 *>(kt[m] + j * kstride + 2);
-      a[m][0] = b01.x;
-      a[m][1] = b01.y;
-      a[m][2] = b23.x;
-      a[m][3] = b23.y;
-    }
-    const float xv[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int m = 0; m < 3; ++m)
-        acc[e & 1][m] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[m][e], (double)xv[e], acc[e & 1][m], 0, 0, 0);
-  }
-}
-
 // lane holds D[c = q + 4r][ch]: 16 consecutive channels per (block, c)
 __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, double *F, int64_t k,
                                          int nc, int q, int64_t ch, const BlockGeom &g) {
@@ -3204,34 +3169,24 @@ constexpr int RUN_WB = RUN_R * 5 * 16;  // doubles per wave run buffer
 constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 
 // MODE 0: production.  Diagnostics (timing only, results invalid;
-// LFD_RUN_MODE): 1 = VALU sum instead of the MFMAs, 4 = MFMAs but the run
-// epilogue reduced to one store per block.
-// MINW: minimum waves per SIMD the register allocation must allow (0: the
-// compiler's choice; 144 VGPRs at PF 2 / 512 threads = 3 waves per SIMD,
-// fewer than the 4 that two workgroups' LDS allow)
-// BUFL: interior sample loads as buffer loads (descriptor at the wave-uniform
-// row base of the channel group, a constant 32-bit voffset per lane) instead
-// of a 64-bit pointer per lane and iteration (fewer VGPRs under MINW)
-// SEPI: streaming run epilogue (run_block_stream; LDS: taps + RUN_CST_S
-// constants, no run buffers, no backward sweep at run ends)
-// PERSIST: a grid of resident workgroups (as many as fit the chip) whose
-// waves walk units w, w + W, w + 2W ... (W = the grid's waves): a wave that
-// finishes a unit starts its next one at once (with one unit per wave, a
-// workgroup's slot is freed only when its slowest wave is done), and the tap
-// table is loaded once per resident workgroup instead of once per 8 units.
-// The assignment is a pure function of the launch (no counter to reset), so
-// the kernel stays hipGraph-capturable.
+// LFD_RUN_MODE, diagnostic build): 1 = VALU sum instead of the MFMAs, 4 =
+// MFMAs but the run epilogue reduced to one store per block.
+// MINW: minimum waves per SIMD the register allocation must allow (4: 128
+// VGPRs, 16 waves per CU with two 512-thread workgroups' LDS).
 // LAT (lattice one-pass plans): tg.nc = 8 + n_off, MFMA rows 8 + d the
 // outputs at offset d of the block; every run's first block is an output
-// block (the plan cuts runs there), so only its y0 is formed, streamed like
-// SEPI: with v_p as above and S0 = 0 at the run start,
+// block (the plan cuts runs there), so only its y0 is formed, streamed: with
+// v_p = e_r0(p) + M S0(p) and S0 = 0 at the run start,
 //   y0_d(first) = p0_d + H0_d T1,  E_r = v_0 + PhiR T1,  T1 = sum_{p>=1} PhiR^(p-1) v_p.
 // Lane (q, col) holds offsets q (row 8 + q, acc[2]) and 4 + q (acc[3]).
+// (Measured and removed, records in profiles/ and CHANGELOG.md: 4x4x4
+// MFMA steps, buffer-descriptor loads, the streaming epilogue on
+// channel-major rows, persistent waves, band / workgroup-per-channel-group
+// unit orders.)
 struct LatAcc {
   double S0 = 0.0, T1 = 0.0, v0 = 0.0, ya = 0.0, yb = 0.0;
 };
-template <int PF, int MODE = 0, int NT = 1024, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
-          bool PERSIST = false, bool LAT = false, bool WGCG = false>
+template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -3241,12 +3196,11 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   const int ntab = tab * tg.nvar;
   for (int i = 2 * threadIdx.x; i < ntab; i += 2 * blockDim.x)
     *reinterpret_cast<double2 *>(Ks + i) = *reinterpret_cast<const double2 *>(taps + i);
-  double *cst = Ks + ntab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4] (SEPI: + PhiR^p[8][16] + B[8][4])
+  double *cst = Ks + ntab;  // PhiF[16] M[16] PhiR[16] G0[4] H0[4] (LAT: + PhiR^p[8][16] + H0L[8][4])
   for (int i = threadIdx.x; i < 56; i += blockDim.x) cst[i] = (&rg.rc->PhiF[0])[i];
-  if (SEPI || LAT) {
+  if (LAT) {
     for (int i = threadIdx.x; i < RUN_R * 16; i += blockDim.x) cst[56 + i] = (&rg.rc->PhiRp[0][0])[i];
-    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x)
-      cst[184 + i] = LAT ? (&rg.rc->H0L[0][0])[i] : (&rg.rc->B[0][0])[i];
+    for (int i = threadIdx.x; i < RUN_R * 4; i += blockDim.x) cst[184 + i] = (&rg.rc->H0L[0][0])[i];
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -3257,45 +3211,10 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   double *wb = Ks + ntab + RUN_CST + wave * RUN_WB;
   (void)wb;
   const int64_t n_cg = (g.n_ch + 15) / 16;
-  // WGCG: the workgroup's waves share one channel group (consecutive time
-  // groups of it), workgroups walk the channel groups fastest: a CU's
-  // concurrent sample rows are 2 x 16 instead of 2 x 8 x 16, and rows of one
-  // group are translated once for its 8 waves (TLB reach)
-  constexpr int WPG = NT / 64;
-  const int64_t n_units = WGCG ? n_cg * ((rg.n_groups + WPG - 1) / WPG) * WPG : n_cg * rg.n_groups;
-  const int64_t wave_slots = (int64_t)gridDim.x * (blockDim.x >> 6);
-  int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-  const int lane0 = lane;
-  while (unit < n_units) {
-  // the lane id laundered per unit, so that nothing derived from it is
-  // hoisted out of the unit loop and held in registers across it
-  int lane = lane0;
-  if constexpr (PERSIST) asm volatile("" : "+v"(lane));
-  // channel-group-major unit order (time-major measured 2 % slower on cfg3);
-  // g_k1_band > 0 (A/B knob LFD_K1_BAND) walks bands of that many channel
-  // groups, time groups inside a band, so fewer pages are in flight at once
-  int64_t cg, grp;
-  if (LFD_DG(g_k1_band) > 0) {
-    const int64_t band = LFD_DG(g_k1_band);
-    const int64_t b = unit / (band * rg.n_groups);
-    const int64_t base = b * band;
-    const int64_t bw = min(band, n_cg - base);
-    const int64_t rem = unit - b * band * rg.n_groups;
-    grp = rem / bw;
-    cg = base + rem % bw;
-  } else if constexpr (WGCG) {
-    const int64_t blk = unit / WPG;
-    cg = blk % n_cg;
-    grp = (blk / n_cg) * WPG + unit % WPG;
-    if (grp >= rg.n_groups) {  // (the last time-group row of a channel group)
-      if constexpr (!PERSIST) break;
-      unit += wave_slots;
-      continue;
-    }
-  } else {
-    cg = unit % n_cg;
-    grp = unit / n_cg;
-  }
+  const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  if (unit >= n_cg * rg.n_groups) return;
+  // channel-group-major unit order (time-major measured 2 % slower on cfg3)
+  const int64_t cg = unit % n_cg, grp = unit / n_cg;
   int r = __builtin_amdgcn_readfirstlane(rg.group_r0[grp]);
   const int r_end = __builtin_amdgcn_readfirstlane(rg.group_r0[grp + 1]);
   // the unit's run table (<= 32 runs) is held one run per lane and read with
@@ -3317,22 +3236,16 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   const float *xr = x + (ch < g.n_ch ? ch : g.n_ch - 1) * s_ch;
   const bool colv = col < tg.nc;
   const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
-  // (M4) tap columns of functionals 4m + (lane & 3)
-  const double *kl4[3];
-#pragma unroll
-  for (int m = 0; m < 3; ++m) kl4[m] = Ks + (q * tg.nc + min(4 * m + (lane & 3), tg.nc - 1)) * 4;
   const int nit = tg.Lp / 64;
   const int kstride = 16 * tg.nc;
   const int64_t s0 = g.base - tg.J;
   const int L = g.L;
   auto table = [&](int64_t s) { return tg.nvar == 1 ? kl : kl + (int)(s & 3) * tab; };
-  auto tshift = [&](int64_t s) { return tg.nvar == 1 ? 0 : (int)(s & 3) * tab; };
   const double *PhiF = cst, *Mm = cst + 16, *PhiR = cst + 32, *G0 = cst + 48, *H0 = cst + 52;
 
   int64_t rks = k0;
   int rlen = run_len_of(r);
   double S0 = 0.0;  // run prefix state, component q of channel col
-  RunAccS ra;       // (SEPI)
   LatAcc la;        // (LAT)
   auto block_done = [&](const d4v &a, int64_t k) {
     // a[0] = e_f[q], a[1] = e_r0[q], a[2] = p0 (q = 0)
@@ -3379,25 +3292,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
         ag[q * 16] = la.S0;
         ag[(4 + q) * 16] = er;
         la = LatAcc{};
-        ++r;
-        if (r < r_end) {
-          rks = run_ks_of(r);
-          rlen = run_len_of(r);
-        }
-      }
-      return;
-    }
-    if constexpr (SEPI) {
-      const double a3[3] = {a[0], a[1], a[2]};
-      run_block_stream(cst, q, p, a3, ra);
-      if (p + 1 == rlen) {
-        double *y0o = Y0 + (cg * g.nb + rks) * 16 + col;
-        if (q < rlen) y0o[q * 16] = ra.ya;
-        if (q + 4 < rlen) y0o[(q + 4) * 16] = ra.yb;
-        double *ag = AG + ((cg * rg.n_runs + r) * 8) * 16 + col;
-        ag[q * 16] = ra.S0;
-        ag[(4 + q) * 16] = ra.Er;
-        ra = RunAccS{};
         ++r;
         if (r < r_end) {
           rks = run_ks_of(r);
@@ -3456,27 +3350,16 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
     const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
-    const int vsh = tg.nvar == 1 ? 0 : v * tab;
     const int64_t a = s - v + 4 * q;
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    double acc4[2][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     for (int it = 0; it < nit; ++it) {
       f4v cur[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
       if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
-      if (M4) {
-        const double *const kt4[3] = {kl4[0] + vsh + (4 * it) * kstride, kl4[1] + vsh + (4 * it) * kstride,
-                                      kl4[2] + vsh + (4 * it) * kstride};
-        mf_iter4(kt4, kstride, cur, acc4);
-      } else {
-        mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
-      }
+      mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
-    if (M4)
-      block_done(d4v{acc4[0][0] + acc4[1][0], acc4[0][1] + acc4[1][1], acc4[0][2] + acc4[1][2], 0.0}, k);
-    else
-      block_done(acc0 + acc1, k);
+    block_done(acc0 + acc1, k);
   };
 
   int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
@@ -3492,10 +3375,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     int64_t kp = ka, sp = s;
     int itp = 0;
     const float *pp = addr(sp, itp);
-    // (BUFL) the channel group's row base + this lane's constant offset
-    const float *xg = x + uniform64(cg * 16 * s_ch);
-    const uint32_t voff = (uint32_t)(4 * ((xr - xg) + 4 * q));
-    const int nrec = (int)(4 * (16 * s_ch + 64));
     auto produce = [&]() {
       if (kp == kb - 1 && itp == nit - 1) return;
       if (++itp == nit) {
@@ -3503,20 +3382,11 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
         ++kp;
         sp += L;
       }
-      if (!BUFL) pp = addr(sp, itp);
+      pp = addr(sp, itp);
     };
     auto load_iter = [&](f4v (&b)[4]) {
-      if constexpr (BUFL) {
-        const float *ub = xg + uniform64((sp & ~(int64_t)3) + 64 * itp);
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(ub), (short)0, nrec, 0x00020000);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          b[j] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 64 * j, 0));
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
-      }
+      for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
     };
     f4v buf[PF + 1][4];
 #pragma unroll
@@ -3525,9 +3395,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       produce();
     }
     const double *kt = table(s);
-    int ksh = tshift(s);
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    double acc4[2][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     bool fin = false;
     while (!fin) {
 #pragma unroll
@@ -3548,17 +3416,10 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
             const int v = (int)(s & 3);
             mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
           }
-          if (M4) {
-            const double *const kt4[3] = {kl4[0] + ksh + (4 * it) * kstride, kl4[1] + ksh + (4 * it) * kstride,
-                                          kl4[2] + ksh + (4 * it) * kstride};
-            mf_iter4(kt4, kstride, buf[u], acc4);
-          } else {
-            mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
-          }
+          mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
         }
         if (++it == nit) {
-          const d4v a = M4 ? d4v{acc4[0][0] + acc4[1][0], acc4[0][1] + acc4[1][1], acc4[0][2] + acc4[1][2], 0.0}
-                           : acc0 + acc1;
+          const d4v a = acc0 + acc1;
           if (MODE == 4) {
             Y0[(cg * g.nb + k) * 16 + col] = a[q & 3];
           } else {
@@ -3566,8 +3427,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
           }
           acc0 = d4v{0.0, 0.0, 0.0, 0.0};
           acc1 = d4v{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int m = 0; m < 3; ++m) acc4[0][m] = acc4[1][m] = 0.0;
           it = 0;
           ++k;
           s += L;
@@ -3576,15 +3435,11 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
             break;
           }
           kt = table(s);
-          ksh = tshift(s);
         }
       }
     }
   }
   for (int64_t k = kb; k < k1; ++k) guarded_block(k);
-  if constexpr (!PERSIST) break;
-  unit += wave_slots;
-  }  // units
 }
 
 // ---------------------------------------------------------------------------
@@ -3698,7 +3553,7 @@ __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmI
   }
 }
 
-// tm_iter on v_mfma_f64_4x4x4_4b (mf_iter4's lane algebra): tile t's
+// tm_iter on v_mfma_f64_4x4x4_4b (operand layout: tools/check_mfma4x4.hip): tile t's
 // functionals 4m + q accumulate in element m of acc_t (m < 3), i.e. acc_t
 // already holds (e_f[q], e_r0[q], p0) as block_done reads them
 template <bool SWAP>
@@ -4316,160 +4171,43 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   return hipGetLastError();
 }
 
-template <int PF, int MODE, int NT, bool M4 = false, int MINW = 0, bool BUFL = false, bool SEPI = false,
-          bool PERSIST = false, bool LAT = false, bool WGCG = false>
+template <int PF, int MODE, int NT, int MINW = 0, bool LAT = false>
 hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g, const double *taps,
                   const TapGeom &tg, const RunGeom &rg, double *Y0, double *AG, int64_t units, hipStream_t st) {
   constexpr int W = NT / 64;  // waves per workgroup, each with its own run buffer
-  // (MODE 4 diagnostic, SEPI and LAT: no run buffers)
-  const size_t lds = (SEPI || LAT) ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
-                          : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
+  // (MODE 4 diagnostic and LAT: no run buffers)
+  const size_t lds = LAT ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
+                         : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  auto kern = &k_block_runs_mfma<PF, MODE, NT, M4, MINW, BUFL, SEPI, PERSIST, LAT, WGCG>;
-  if constexpr (WGCG) units = ((g.n_ch + 15) / 16) * ((rg.n_groups + W - 1) / W) * W;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  unsigned grid = nblk(units, W);
-  if constexpr (PERSIST) {
-    // one resident workgroup per slot the LDS / registers allow on every CU
-    int dev = 0, n_cu = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess)
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern), NT, lds);
-    if (e != hipSuccess) return e;
-    grid = std::min<unsigned>(grid, (unsigned)std::max(1, n_cu * std::max(1, per_cu)));
-  }
-  kern<<<grid, NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
+  auto kern = &k_block_runs_mfma<PF, MODE, NT, MINW, LAT>;
+  static std::once_flag attr_once;
+  hipError_t ea = hipSuccess;
+  std::call_once(attr_once, [&] {
+    ea = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             TAP_LDS_MAX);
+  });
+  if (ea != hipSuccess) return ea;
+  kern<<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
   return hipGetLastError();
 }
-
-#ifdef LFD_DIAG
-hipError_t launch_block_runs_mfma_ab(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
-                                  const double *taps, const TapGeom &tg, const RunGeom &rg,
-                                  double *Y0, double *AG, hipStream_t st) {
-  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
-  const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
-  // 512-thread workgroups (2 per CU: 16 waves, 2 x 77 KB LDS at cfg3) retire
-  // independently, unlike one 1024-thread group per CU: 12.3-12.7 ms vs
-  // 12.65-13.0 on cfg3 (A/B, tools/ab_env.sh). Prefetch depth 2: 0.6 % faster
-  // than depth 1 in 15 of 15 in-process pairs on two boxes (tools/probe_k1cfg.py)
-  // Registers for 4 waves per SIMD (MINW 4: 16 waves per CU, as many as two
-  // workgroups' LDS allow) at prefetch depth 1: 12.77 ms vs 13.09-13.12 for
-  // depth 2 at the compiler's 144 VGPRs (3 waves per SIMD), in-process A/B on
-  // one allocation, 2 processes x 20 launches (tools/ab_plan.py); depth 2
-  // under the cap spills 18 VGPRs and is slower (13.25)
-  int mode = 0, pf = 1, nt = 512;
-  {
-    static int band_set = 0;
-    const char *v = knob("LFD_K1_BAND");
-    const int band = v ? std::max(0, std::atoi(v)) : 0;
-    if (band != band_set) {
-      hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_k1_band), &band, sizeof(int), 0,
-                                            hipMemcpyHostToDevice, st);
-      if (e != hipSuccess) return e;
-      e = hipStreamSynchronize(st);
-      if (e != hipSuccess) return e;
-      band_set = band;
-    }
-  }
-  if (const char *v = knob("LFD_RUN_MODE")) mode = std::atoi(v);
-  if (const char *v = knob("LFD_RUN_PF")) pf = std::atoi(v);
-  if (const char *v = knob("LFD_RUN_NT")) nt = std::atoi(v);
-  // three v_mfma_f64_4x4x4_4b per step instead of one 16x16x4 (mf_iter4)
-  bool m4 = false;
-  if (const char *v = knob("LFD_RUN_M4")) m4 = std::atoi(v) != 0;
-  int minw = 4;  // LFD_RUN_MINW=0: the compiler's register allocation
-  if (const char *v = knob("LFD_RUN_MINW")) minw = std::atoi(v);
-  bool bufl = false;  // LFD_RUN_BUF=1: buffer loads (A/B knob)
-  if (const char *v = knob("LFD_RUN_BUF")) bufl = std::atoi(v) != 0;
-  if (bufl && 16 * s_ch + 64 < ((int64_t)1 << 29) && mode == 0 && nt == 512 && minw == 4 && !m4) {
-    if (pf == 2) return run_k1<2, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (pf == 1) return run_k1<1, 0, 512, false, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    return hipErrorInvalidValue;
-  }
-  // streaming run epilogue (A/B knob LFD_RUN_SEPI=1): no gain on
-  // channel-major rows (12.59 / 12.52 vs 12.50 ms on cfg3, 1.88 / 1.76 vs 1.76
-  // on a 1,250-channel shard; profiles/r03_ab_cm_sepi.txt), where 16 waves
-  // per CU already hide the run-end sweep
-  bool sepi = false;
-  if (const char *v = knob("LFD_RUN_SEPI")) sepi = std::atoi(v) != 0;
-  if (sepi && mode == 0 && nt == 512 && !m4 && !bufl) {
-    if (minw == 4 && pf == 1) return run_k1<1, 0, 512, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (minw == 4 && pf == 2) return run_k1<2, 0, 512, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (minw == 0 && pf == 2) return run_k1<2, 0, 512, false, 0, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    return hipErrorInvalidValue;
-  }
-  if (minw == 4 && mode == 0 && nt == 512) {
-    if (m4 && pf == 2) return run_k1<2, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (m4 && pf == 1) return run_k1<1, 0, 512, true, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (!m4 && pf == 2) return run_k1<2, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (!m4 && pf == 1) {
-      // LFD_K1_PERSIST=1: persistent waves walking units w, w + W, ... —
-      // measured slower at every width (1,250 ch 1.98 vs 1.65 ms, 10,000 ch
-      // 14.8 vs 13.6 ms; profiles/r04_ab_k1_persist_*.txt): the unit loop
-      // spills 30 VGPRs under the 128-register cap into the sample loop
-      if (knob_flag("LFD_K1_WGCG"))
-        return run_k1<1, 0, 512, false, 4, false, false, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG,
-                                                                             units, st);
-      const char *pv = knob("LFD_K1_PERSIST");
-      if (pv && std::atoi(pv) != 0)
-        return run_k1<1, 0, 512, false, 4, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-      // LFD_K1_WG=256: 256-thread groups with the streaming epilogue (taps +
-      // constants only in LDS: 4 groups / 16 waves per CU); =2561: the same
-      // with the LDS run buffers (57 KB: 2 groups / 8 waves per CU)
-      if (const char *wv = knob("LFD_K1_WG")) {
-        if (std::atoi(wv) == 256)
-          return run_k1<1, 0, 256, false, 4, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-        if (std::atoi(wv) == 2561)
-          return run_k1<1, 0, 256, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-      }
-      return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    }
-    return hipErrorInvalidValue;
-  }
-  if (m4 && mode == 0) {
-    if (pf == 2 && nt == 512) return run_k1<2, 0, 512, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (pf == 1 && nt == 512) return run_k1<1, 0, 512, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    if (pf == 3 && nt == 512) return run_k1<3, 0, 512, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-    return hipErrorInvalidValue;
-  }
-  if (mode == 1) return run_k1<1, 1, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (mode == 4 && nt == 320) return run_k1<1, 4, 320>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (mode == 4 && nt == 512) return run_k1<1, 4, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (mode == 4) return run_k1<1, 4, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 3 && nt == 512) return run_k1<3, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 4 && nt == 512) return run_k1<4, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 2 && nt == 768) return run_k1<2, 0, 768>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 2 && nt == 384) return run_k1<2, 0, 384>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 2 && nt == 512) return run_k1<2, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 1 && nt == 1024) return run_k1<1, 0, 1024>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  if (pf == 1 && nt == 512) return run_k1<1, 0, 512>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
-  // an A/B knob combination without an instantiation: refuse rather than run
-  // (and let a record label) a configuration that never ran
-  return hipErrorInvalidValue;
-}
-#endif  // LFD_DIAG
 
 hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
                                   const double *taps, const TapGeom &tg, const RunGeom &rg,
                                   double *Y0, double *AG, hipStream_t st) {
-#ifdef LFD_DIAG
-  return launch_block_runs_mfma_ab(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, st);
-#else
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || rg.n_groups < 1) return hipErrorInvalidValue;
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
   // 512-thread workgroups (2 per CU: 16 waves), prefetch depth 1, registers
   // capped for 4 waves per SIMD: 12.77 ms vs 13.09-13.12 for depth 2 at the
-  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt).
-  // One unit per wave: persistent waves measured slower (diag LFD_K1_PERSIST)
-  return run_k1<1, 0, 512, false, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt)
+#ifdef LFD_DIAG
+  // timing-only modes (results invalid): LFD_RUN_MODE=1 loads only, =4 no run epilogue
+  if (const char *v = knob("LFD_RUN_MODE")) {
+    const int mode = std::atoi(v);
+    if (mode == 1) return run_k1<1, 1, 512, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+    if (mode == 4) return run_k1<1, 4, 512, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  }
 #endif
+  return run_k1<1, 0, 512, 4>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 }
 
 hipError_t launch_block_runs_mfma_lat(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
@@ -4478,7 +4216,7 @@ hipError_t launch_block_runs_mfma_lat(const float *x, int64_t s_ch, int64_t n_t,
   if (tg.nc <= 2 * RUN_N || tg.nc > 2 * RUN_N + LAT_MAX_OFF || tg.Lp % 64 != 0 || rg.n_groups < 1)
     return hipErrorInvalidValue;
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
-  return run_k1<1, 0, 512, false, 4, false, false, false, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
+  return run_k1<1, 0, 512, 4, true>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG, units, st);
 }
 
 // ---------------------------------------------------------------------------

@@ -47,7 +47,9 @@ def to_device_ct(patch: Patch, device=None, dtype=None):
         if a.ndim != 2:
             raise ValueError("lfdas patches are 2-D (distance, time)")
         npdt = np.float32 if dtype == torch.float32 else np.float64
-        t = torch.from_numpy(np.ascontiguousarray(a, dtype=npdt)).to(dev)
+        from .arena import device_samples
+        t = device_samples(a.shape, dtype=dtype, device=dev)  # (translation-friendly placement, lfdas.arena)
+        t.copy_(torch.from_numpy(np.ascontiguousarray(a, dtype=npdt)))
     return t.permute(*perm)
 
 
