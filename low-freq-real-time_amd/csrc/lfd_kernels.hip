@@ -2720,7 +2720,10 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
 template <int NPF>
 __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch,
                                                      int W, int S, int g, float *__restrict__ y, int64_t ys_ch,
-                                                     int64_t ys_t, int seg_out, int ring_mask) {
+                                                     int64_t ys_t, int seg_out, int ring_mask, int diag = 0) {
+  // (diag, LFD_ROLL_SEG_DIAG, timings only: 1 = loads + lane sums only, 2 = no
+  // output pass)
+  diag = LFD_DG(diag);
   extern __shared__ double rg_ring_all[];
   const int R = ring_mask + 1;
   double *spr = rg_ring_all + (size_t)(threadIdx.x >> 6) * 2 * R;   // SP(j) at slot j & ring_mask
@@ -2789,6 +2792,10 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
         tot += d;
         part += e <= eb ? d : 0.0;
       }
+      if (diag & 1) {
+        if (tot + part == 1234.5 && !bad) yo[0] = 0.f;
+        return;
+      }
       const double incl = wave_incl_scan_dpp(tot);
       if (has) spr[bq & ring_mask] = carry + (incl - tot) + part;
       carry += readlane_d(incl, 63);
@@ -2811,7 +2818,7 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // outputs whose window ends in this tile (kS <= its last position)
       const int kmax = min(k1 - 1, (tb + RG_P - 1) / S);
-      for (int k = kn + lane; k <= kmax; k += 64) {
+      for (int k = kn + lane; k <= kmax && !(diag & 2); k += 64) {
         const int j = k * Q;
         const double sum = spr[j & ring_mask] - spr[(j - M) & ring_mask];
         const int64_t code = cdr[j & ring_mask] - cdr[(j - M) & ring_mask];
@@ -5481,8 +5488,10 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
         }
       }
 #endif
+      int sdiag = 0;
+      if (const char *v = knob("LFD_ROLL_SEG_DIAG")) sdiag = std::atoi(v);
       k_rolling_seg<2><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y, ys_ch,
-                                                           ys_t, (int)seg_out, ring - 1);
+                                                           ys_t, (int)seg_out, ring - 1, sdiag);
       return hipGetLastError();
     }
   }

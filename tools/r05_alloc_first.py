@@ -42,6 +42,50 @@ if method in ("contig", "plain"):
         hip.hipMalloc(ctypes.byref(p), nbytes)
     assert rc == 0, rc
     x = torch.as_tensor(_Arr(p.value, (ch, n)), device=dev)
+elif method.startswith("vmm"):  # vmm<G>: G GiB physical chunks mapped into a G-GiB-aligned VA range; vmmone: one chunk
+    c_sz = ctypes.c_size_t
+    hip = ctypes.CDLL("libamdhip64.so.7")  # torch's runtime (already loaded)
+
+    class Loc(ctypes.Structure):
+        _fields_ = [("type", ctypes.c_int), ("id", ctypes.c_int)]
+
+    class Flg(ctypes.Structure):
+        _fields_ = [("ct", ctypes.c_ubyte), ("rdma", ctypes.c_ubyte), ("usage", ctypes.c_ushort)]
+
+    class Prop(ctypes.Structure):
+        _fields_ = [("type", ctypes.c_int), ("handle", ctypes.c_int), ("location", Loc), ("win32", ctypes.c_void_p),
+                    ("flags", Flg)]
+
+    class Acc(ctypes.Structure):
+        _fields_ = [("location", Loc), ("flags", ctypes.c_int)]
+
+    prop = Prop(1, 0, Loc(1, 0), None, Flg(0, 0, 0))
+    gran = c_sz()
+    assert hip.hipMemGetAllocationGranularity(ctypes.byref(gran), ctypes.byref(prop), 1) == 0
+    G = (nbytes + gran.value - 1) // gran.value * gran.value if method == "vmmone" else int(method[3:] or 1) << 30
+    size = (nbytes + G - 1) // G * G
+    va = ctypes.c_void_p()
+    hip.hipMemAddressReserve.argtypes = [ctypes.POINTER(ctypes.c_void_p), c_sz, c_sz, ctypes.c_void_p,
+                                         ctypes.c_ulonglong]
+    hip.hipMemCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p), c_sz, ctypes.POINTER(Prop), ctypes.c_ulonglong]
+    hip.hipMemMap.argtypes = [ctypes.c_void_p, c_sz, c_sz, ctypes.c_void_p, ctypes.c_ulonglong]
+    hip.hipMemSetAccess.argtypes = [ctypes.c_void_p, c_sz, ctypes.POINTER(Acc), c_sz]
+    align = min(G, 1 << 30)
+    assert hip.hipMemAddressReserve(ctypes.byref(va), size, align, None, 0) == 0
+    for i in range(size // G):
+        h = ctypes.c_void_p()
+        rc = hip.hipMemCreate(ctypes.byref(h), G, ctypes.byref(prop), 0)
+        assert rc == 0, rc
+        assert hip.hipMemMap(va.value + i * G, G, 0, h, 0) == 0
+    acc = Acc(Loc(1, 0), 3)
+    assert hip.hipMemSetAccess(va, size, ctypes.byref(acc), 1) == 0
+    print(f"vmm granularity {gran.value} chunk {G} size {size}", flush=True)
+    x = torch.as_tensor(_Arr(va.value, (ch, n)), device=dev)
+elif method.startswith("pool"):  # pool[<GiB>]: lfdas.arena.device_samples with that pool size
+    from lfdas import arena
+    if method[4:]:
+        arena.POOL_BYTES = int(method[4:]) << 30
+    x = arena.device_samples((ch, n), device=dev)
 elif method.startswith("big"):  # big<k>[last]: k x the rows, the shard at the start / end
     k = int(method[3:].replace("last", "") or 4)
     full = torch.empty((k * ch, n), dtype=torch.float32, device=dev)
