@@ -36,6 +36,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "low-freq-real-time_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+# steps through lfdas.plan.LowpassPipeline (each step's scan beside the next
+# step's block pass; --serial: one execute after the other on one stream)
+PIPELINED = True
 
 
 def _args():
@@ -63,6 +66,9 @@ def _args():
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo collectives "
                         "(the line is marked rehearsal; not a scaling measurement)")
+    p.add_argument("--serial", action="store_true",
+                   help="time the steps one execute after the other on one stream (default: pipelined, "
+                        "lfdas.plan.LowpassPipeline; the serial time is reported beside it either way)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 PMC traffic summary (tools/pmc_summary.py) for roofline.traffic")
     return p.parse_args()
@@ -199,6 +205,29 @@ def time_plan(plan, x, y, wsb, stream, steps, warmup, barrier=None):
     return el, k1, sc
 
 
+def time_plan_pipelined(plan, x, y, steps, warmup, barrier=None):
+    """Wall seconds of ``steps`` batches through ``lfdas.plan.LowpassPipeline``
+    (each batch's scan beside the next batch's block pass, two workspaces),
+    between two barriers; every batch is the full computation of
+    ``plan.execute`` (bit-identical outputs, tests/test_gpu_lowpass.py)."""
+    import torch
+    from lfdas.plan import LowpassPipeline
+    barrier = barrier or (lambda: torch.cuda.synchronize(x.device))
+    pipe = LowpassPipeline(plan, x.device)
+    for _ in range(warmup):
+        pipe.submit(x, y)
+    pipe.wait()
+    barrier()
+    t_a = time.perf_counter()
+    for _ in range(steps):
+        pipe.submit(x, y)
+    pipe.wait()
+    barrier()
+    el = time.perf_counter() - t_a
+    del pipe
+    return el
+
+
 def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_major=False, steps=5,
                        label="", warmup=1):
     """One extra low-pass workload, timed like the headline (inputs in HBM,
@@ -217,10 +246,14 @@ def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_majo
     wsb = plan.alloc_workspace(dev)
     stream = torch.cuda.current_stream(dev)
     el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, steps, warmup)
+    el_s = el
+    if PIPELINED:
+        el = time_plan_pipelined(plan, x, y, steps, warmup)
     R = int(round(fs * dt_out))
     k1 = float(np.mean(k1_ms))
     gbs = n_ch * n * (4.0 + 4.0 / R) / (k1 * 1e-3) / 1e9
     out = {"value": n_ch * n * steps / el, "unit": "channel-samples/s", "ms_per_step": el / steps * 1e3,
+           "ms_per_step_serial": el_s / steps * 1e3, "pipelined": PIPELINED,
            "config": label, "k1": plan.last_kernel(), "block_len": plan.block_len,
            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": gbs / HBM_PEAK_GBS, "kernel": K1_KERNELS.get(plan.last_kernel()),
@@ -741,6 +774,8 @@ def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48, backend="
 
 def main():
     args = _args()
+    global PIPELINED
+    PIPELINED = not args.serial
     rc = launch_or_check(args)
     if rc is not None:
         sys.exit(rc)
@@ -823,7 +858,10 @@ def main():
         torch.distributed.all_reduce(one)
         ranks_seen = int(one.item())
     el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, args.steps, args.warmup, barrier)
-    el = max_over_ranks(el)
+    el_serial = max_over_ranks(el)
+    el = el_serial
+    if PIPELINED:
+        el = max_over_ranks(time_plan_pipelined(plan, x, y, args.steps, args.warmup, barrier))
     k1_kernel = plan.last_kernel()
 
     R = int(round(args.fs * args.dt_out))
@@ -927,6 +965,9 @@ def main():
             r = bench_lowpass_line(dev, c, args.fs, args.seconds, args.dt_out, args.patch_size, args.edge_buff,
                                    steps=20, warmup=3, label=f"{c:,}-channel shard of cfg3 ({n_gpu} GPUs)")
             shards[f"n{n_gpu}"] = {"channels": c, "ms_per_step": r["ms_per_step"],
+                                   "ms_per_step_serial": r["ms_per_step_serial"],
+                                   "projected_efficiency_serial":
+                                       (el_serial / args.steps * 1e3 / n_gpu) / r["ms_per_step_serial"],
                                    "kernel_ms": r["roofline"]["kernel_ms"],
                                    "scan_kernel_ms": r["roofline"]["scan_kernel_ms"],
                                    "roofline_frac": r["roofline"]["frac"],
@@ -956,6 +997,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
+            "ms_per_step_serial": el_serial / args.steps * 1e3,
+            "pipelined": ("each step's chunk scan runs beside the next step's block pass (lfdas.plan."
+                          "LowpassPipeline: two workspaces, one block stream, one scan stream); every step "
+                          "is the full computation" if PIPELINED else False),
             "higher_is_better": True,
             "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,

@@ -114,6 +114,20 @@ int lfd_lowpass_plan_info(const lfd_lowpass_plan *plan, size_t *workspace_bytes,
 int lfd_lowpass_execute(const lfd_lowpass_plan *plan, const float *x,
                         int64_t s_ch, int64_t s_t, float *y, int64_t ys_ch,
                         int64_t ys_t, void *workspace, void *stream);
+/* Two-stream execute for batch pipelines: the block pass (K1) runs on
+ * `block_stream`, the chunk scan and the outputs on `scan_stream` after it
+ * (an event), so y is complete in scan_stream order and the workspace is
+ * free again once scan_stream has passed this call.  Consecutive executes
+ * on two workspaces then overlap one execute's scan and its block pass's
+ * drain with the next block pass (lfdas.plan.LowpassPipeline, bench.py).
+ * Plans with no separate scan launch (lattice / sub-plan grids) run whole
+ * on block_stream and scan_stream waits for them.  Replaces nothing in the
+ * reference (LFProc.process_time_range, lf_das.py:219-290, filters one
+ * range per call); it is the same computation as lfd_lowpass_execute. */
+int lfd_lowpass_execute_split(const lfd_lowpass_plan *plan, const float *x,
+                              int64_t s_ch, int64_t s_t, float *y,
+                              int64_t ys_ch, int64_t ys_t, void *workspace,
+                              void *block_stream, void *scan_stream);
 /* Per-kernel device time of the last execute on `stream` (ms), measured
  * with HIP events when enabled by lfd_set_timing(1). */
 int lfd_lowpass_last_timing(const lfd_lowpass_plan *plan, float *ms_blocks,

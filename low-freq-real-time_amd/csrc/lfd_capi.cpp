@@ -802,6 +802,10 @@ struct lfd_lowpass_plan {
   // lfd_set_timing(n > 1): a ring of n event triples, so n timed executes
   // need no host synchronisation between them (lfd_lowpass_timings)
   mutable std::vector<hipEvent_t> ring;
+  // split executes: the block-pass -> scan-stream events, reused round-robin
+  // (a stream wait binds to the record made before it)
+  mutable std::vector<hipEvent_t> split_ev;
+  mutable size_t split_i = 0;
   mutable int64_t n_exec = 0;
   mutable int last_ring = 0;  // ring size of the last timed execute (0: ev)
   mutable bool timed = false;
@@ -1521,10 +1525,37 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
                         void *workspace, void *stream) {
   return lfd::lowpass_execute_gen(p, x, s_ch, s_t, y, ys_ch, ys_t, workspace, stream, lfd::GridGen{});
 }
+
+int lfd_lowpass_execute_split(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
+                              int64_t ys_ch, int64_t ys_t, void *workspace, void *block_stream, void *scan_stream) {
+  if (!scan_stream) return fail(LFD_EINVAL, "scan_stream is NULL");
+  return lfd::lowpass_execute_gen(p, x, s_ch, s_t, y, ys_ch, ys_t, workspace, block_stream, lfd::GridGen{},
+                                  scan_stream == block_stream ? nullptr : scan_stream);
+}
 }  // extern "C"
 
+namespace {
+// `to` waits for the work enqueued so far on `from` (one of the plan's split
+// events; a stream wait binds to the record made before it, so the event can
+// be recorded again by a later execute)
+hipError_t stream_after(const lfd_lowpass_plan *p, hipStream_t to, hipStream_t from) {
+  constexpr size_t N_SPLIT_EV = 8;
+  if (p->split_ev.size() < N_SPLIT_EV) {
+    hipEvent_t e = nullptr;
+    const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (rc != hipSuccess) return rc;
+    p->split_ev.push_back(e);
+  }
+  hipEvent_t e = p->split_ev[p->split_i++ % p->split_ev.size()];
+  hipError_t rc = hipEventRecord(e, from);
+  if (rc == hipSuccess) rc = hipStreamWaitEvent(to, e, 0);
+  return rc;
+}
+}  // namespace
+
 int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
-                             int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const lfd::GridGen &gen) {
+                             int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const lfd::GridGen &gen,
+                             void *scan_stream) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
   if (!x || !y || !workspace) return fail(LFD_EINVAL, "x, y and workspace must be device pointers");
   if (s_t == 0 || (p->n_ch > 1 && s_ch == 0)) return fail(LFD_EINVAL, "zero stride");
@@ -1533,6 +1564,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
   LFD_HIP(hipGetDevice(&dev));
   if (dev != p->device) return fail(LFD_EINVAL, "plan was created on another device");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the scan's stream: `st`, or (split execute) scan_stream after the block pass
+  hipStream_t st2 = scan_stream ? reinterpret_cast<hipStream_t>(scan_stream) : st;
   char *ws = static_cast<char *>(workspace);
   double *F = reinterpret_cast<double *>(ws + p->off_F);
   double *SF = reinterpret_cast<double *>(ws + p->off_SF);
@@ -1581,6 +1614,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
       LFD_HIP(lfd::launch_blend_grid_sm(tmp, p->n_ch, p->d_bj, p->d_bi_lat, p->d_bw, p->n_blend, y, ys_ch, ys_t, st,
                                         gen));
       if (timed) LFD_HIP(hipEventRecord(ev[2], st));
+      if (st2 != st) LFD_HIP(stream_after(p, st2, st));
       p->last_k1 = LFD_K1_MFMA_RUNS;
       return LFD_OK;
     }
@@ -1595,6 +1629,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     LFD_HIP(lfd::launch_blend_grid(tmp, p->comp_T, p->n_ch, p->d_bj, p->d_bi, p->d_bw, p->n_blend, y, ys_ch,
                                    ys_t, st, gen));
     if (timed) LFD_HIP(hipEventRecord(ev[2], st));
+    if (st2 != st) LFD_HIP(stream_after(p, st2, st));
     p->last_k1 = p->subs[0]->last_k1.load();
     return LFD_OK;
   }
@@ -1629,13 +1664,14 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
       LFD_HIP(lfd::launch_fold_runs(F, p->bg, rg, Y0, AG, st));
     }
     if (timed) LFD_HIP(hipEventRecord(ev[1], st));
+    if (st2 != st) LFD_HIP(stream_after(p, st2, st));
     LFD_HIP(lfd::launch_chunk_scan_runs(x, s_ch, s_t, p->bg, p->padlen, p->sc, rg, p->d_chunks, p->n_chunks, Y0,
-                                        AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st,
+                                        AG, SR, TP, p->tp_len, y, ys_ch, ys_t, st2,
                                         reinterpret_cast<double *>(ws + p->off_TR),
                                         reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk, p->d_segs,
                                         p->seg_max, reinterpret_cast<double *>(ws + p->off_SC), p->d_segs_fu,
                                         p->nw_fu));
-    if (timed) LFD_HIP(hipEventRecord(ev[2], st));
+    if (timed) LFD_HIP(hipEventRecord(ev[2], st2));
     return LFD_OK;
   }
   if (mfma)
@@ -1643,9 +1679,10 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
   else
     LFD_HIP(lfd::launch_block_functionals(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->kc, F, st));
   if (timed) LFD_HIP(hipEventRecord(ev[1], st));
+  if (st2 != st) LFD_HIP(stream_after(p, st2, st));
   LFD_HIP(lfd::launch_chunk_scan(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
-                                 p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st));
-  if (timed) LFD_HIP(hipEventRecord(ev[2], st));
+                                 p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st2));
+  if (timed) LFD_HIP(hipEventRecord(ev[2], st2));
   return LFD_OK;
 }
 
@@ -1758,6 +1795,8 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
                   (void *)p->d_slot_chunk})
     if (d) (void)hipFree(d);
   for (auto &e : p->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &e : p->split_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto &e : p->ring)
     if (e) (void)hipEventDestroy(e);

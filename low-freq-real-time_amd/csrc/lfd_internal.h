@@ -376,8 +376,11 @@ hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const in
                              const GridGen &gen = GridGen{});
 // lfd_lowpass_execute with a generated grid (a lattice plan's weights from
 // `gen`; the stream caches lattice plans by structure).  Other plans ignore it.
+// scan_stream (lfd_lowpass_execute_split): the scan and outputs there after
+// the block pass (an event); nullptr = everything on `stream`.
 int lowpass_execute_gen(const ::lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
-                        int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const GridGen &gen);
+                        int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const GridGen &gen,
+                        void *scan_stream = nullptr);
 // dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.
 hipError_t launch_transpose(const float *src, int64_t n_rows, int64_t n_cols, int64_t sp, float *dst,
                             int64_t dp, hipStream_t st);

@@ -135,6 +135,7 @@ def load():
                                      vp, i64], i32),
         "lfd_lowpass_plan_info": ([vp, P(sz), P(i64), P(i64)], i32),
         "lfd_lowpass_execute": ([vp, vp, i64, i64, vp, i64, i64, vp, vp], i32),
+        "lfd_lowpass_execute_split": ([vp, vp, i64, i64, vp, i64, i64, vp, vp, vp], i32),
         "lfd_lowpass_last_timing": ([vp, P(ctypes.c_float), P(ctypes.c_float)], i32),
         "lfd_lowpass_timings": ([vp, vp, vp, i64], i32),
         "lfd_lowpass_plan_destroy": ([vp], None),
@@ -186,7 +187,7 @@ def load():
 
 EXPORTED = (
     "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing", "lfd_set_option", "lfd_get_option",
-    "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute",
+    "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute", "lfd_lowpass_execute_split",
     "lfd_lowpass_last_timing", "lfd_lowpass_timings", "lfd_lowpass_plan_destroy",
     "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_debug_runs",
     "lfd_sos_filtfilt_resample_f32",

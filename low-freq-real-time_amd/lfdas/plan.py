@@ -122,6 +122,27 @@ class LowpassPlan:
             self._h, _ptr(x), x.stride(0), x.stride(1), _ptr(y), y.stride(0), y.stride(1),
             _ptr(workspace), _stream_ptr(stream)))
 
+    def execute_split(self, x, y, workspace, block_stream, scan_stream):
+        """``execute`` with the block pass (K1) on ``block_stream`` and the
+        chunk scan + outputs on ``scan_stream`` after it
+        (``lfd_lowpass_execute_split``): y is complete in scan_stream order,
+        and the workspace is free once scan_stream has passed this call."""
+        import torch
+        _require_cuda(x, "x", torch.float32)
+        _require_cuda(y, "y", torch.float32)
+        if tuple(x.shape) != (self.n_ch, self.n_t):
+            raise ValueError(f"x shape {tuple(x.shape)} != plan {(self.n_ch, self.n_t)}")
+        if tuple(y.shape) != (self.n_ch, self.n_grid):
+            raise ValueError(f"y shape {tuple(y.shape)} != {(self.n_ch, self.n_grid)}")
+        if workspace.numel() * workspace.element_size() < self.workspace_bytes:
+            raise ValueError("workspace too small")
+        if block_stream is None or scan_stream is None:
+            raise ValueError("execute_split needs both streams")
+        _count()
+        check(self._lib.lfd_lowpass_execute_split(
+            self._h, _ptr(x), x.stride(0), x.stride(1), _ptr(y), y.stride(0), y.stride(1),
+            _ptr(workspace), _stream_ptr(block_stream), _stream_ptr(scan_stream)))
+
     def last_timing_ms(self):
         a = ctypes.c_float()
         b = ctypes.c_float()
@@ -201,6 +222,59 @@ class LowpassPlan:
             self._h, bc.ctypes.data, bc.nbytes, sc.ctypes.data, sc.nbytes, cg.ctypes.data, cg.nbytes))
         return bc[0], sc[0], cg
 
+
+
+class LowpassPipeline:
+    """Back-to-back executes of one plan over a sequence of same-shape batches
+    (consecutive time ranges, many records), overlapped on the device.  Every
+    batch's block pass (K1) runs on one block stream, its chunk scan and
+    outputs on a scan stream after it (``LowpassPlan.execute_split``), with
+    the workspaces alternating: batch i's scan — latency-bound, a few hundred
+    workgroups — runs beside batch i + 1's HBM-bound block pass instead of
+    after it, and a workspace is handed to a new block pass only after the
+    scan that read it (an event).  The block passes stay serialised (their
+    HIP-event / rocprof durations are those of ``execute``).  Results are bit
+    for bit those of ``plan.execute``.  The caller keeps ``x`` / ``y`` alive
+    until ``synchronize()`` (or ``wait(stream)``) — they are used on the
+    pipeline's streams."""
+
+    def __init__(self, plan, device=None, depth: int = 2):
+        import torch
+        if depth < 1:
+            raise ValueError("depth must be >= 1")
+        self.plan = plan
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.ws = [plan.alloc_workspace(self.device) for _ in range(depth)]
+        self.block = torch.cuda.Stream(self.device)
+        self.scan = torch.cuda.Stream(self.device)
+        self._done = [None] * depth
+        self._i = 0
+
+    def submit(self, x, y):
+        """Queue one batch: ``y`` <- the plan's outputs of ``x``."""
+        import torch
+        j = self._i % len(self.ws)
+        cur = torch.cuda.current_stream(self.device)
+        self.block.wait_stream(cur)  # x written on the caller's stream
+        self.scan.wait_stream(cur)   # y (and its earlier readers)
+        if self._done[j] is not None:
+            self.block.wait_event(self._done[j])  # the scan that last read ws[j]
+        self.plan.execute_split(x, y, self.ws[j], self.block, self.scan)
+        ev = torch.cuda.Event()
+        ev.record(self.scan)
+        self._done[j] = ev
+        self._i += 1
+
+    def wait(self, stream=None):
+        """``stream`` (default: the current stream) waits for every queued batch."""
+        import torch
+        s = stream or torch.cuda.current_stream(self.device)
+        s.wait_stream(self.block)
+        s.wait_stream(self.scan)
+
+    def synchronize(self):
+        self.block.synchronize()
+        self.scan.synchronize()
 
 def set_timing(enable: bool, ring: int = 1):
     """HIP-event timing of executes; ``ring`` > 1 keeps the last ``ring``

@@ -629,3 +629,51 @@ def test_offsample_head_skip_nulls(which):
         assert np.array_equal(np.isnan(yy), np.isnan(r)), (which, a, b)
         m = ~np.isnan(r)
         assert _relrms(yy[m], r[m]) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [
+    (500.0, 1.0, 600, 7, 40, 1500.0, "tc"),   # cfg3 parameters, narrow: the fused scan
+    (250.0, 0.2, 40, 6, 37, 24.0, "cc"),      # cfg1 geometry, (time, channel) rows
+    (3000.0, 1.0, 120, 7, 6, 300.0, "tc"),    # lattice grid (one-pass K1 + scan + blend)
+])
+def test_pipeline_matches_execute(cfg):
+    """lfdas.plan.LowpassPipeline (lfd_lowpass_execute_split: each batch's
+    scan on a scan stream beside the next batch's block pass, two
+    workspaces) gives every batch exactly plan.execute's outputs, for
+    batches submitted back to back without host synchronisation."""
+    import torch
+    from lfdas.plan import LowpassPipeline, LowpassPlan
+    fs, dt_out, P, B, n_ch, dur, layout = cfg
+    n = int(dur * fs)
+    dt_ns = int(round(1e9 / fs))
+    tg = S.time_grid(T0, T0 + n * dt_ns, dt_out)
+    sched = S.lfproc_chunks(len(tg), P, B)
+    lo, w = S.grid_positions(T0, dt_ns, tg)
+    chunks = [(*S.select_range(T0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
+    sos = oracle.butter_sos(4, (1 / dt_out / 2 * 0.9) / (fs / 2))
+    plan = LowpassPlan(sos, n_ch, n, lo, w, chunks)
+    rng = np.random.default_rng(23)
+    xs = []
+    for i in range(5):
+        x = (rng.standard_normal((n_ch, n)) + 10.0 * i).astype(np.float32)
+        if i == 2:
+            x[1, n // 3] = np.nan
+        xd = torch.from_numpy(x).cuda() if layout == "tc" else torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()
+        xs.append(xd)
+    ws = plan.alloc_workspace()
+    ref = []
+    for xd in xs:
+        y = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float32, device="cuda")
+        plan.execute(xd, y, ws)
+        ref.append(y)
+    torch.cuda.synchronize()
+    pipe = LowpassPipeline(plan)
+    ys = [torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float32, device="cuda") for _ in xs]
+    for xd, y in zip(xs, ys):
+        pipe.submit(xd, y)
+    pipe.wait()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, ys):
+        assert torch.equal(torch.nan_to_num(a, 7.0), torch.nan_to_num(b, 7.0))
+    assert np.isnan(ys[2].cpu().numpy()[1]).any() and not np.isnan(ys[1].cpu().numpy()[1, 50:-50]).any()
+    plan.close()
