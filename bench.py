@@ -36,9 +36,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "low-freq-real-time_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
-# steps through lfdas.plan.LowpassPipeline (each step's scan beside the next
-# step's block pass; --serial: one execute after the other on one stream)
-PIPELINED = True
+# --pipelined: steps through lfdas.plan.LowpassPipeline (each step's scan
+# beside the next step's block pass).  Measured r05t: no gain (cfg3 12.996
+# vs 12.986 ms serial; 1,250 ch 1.723 vs 1.745, 2,500 ch 3.366 vs 3.307), so
+# the default is serial: one execute after the other on one stream
+PIPELINED = False
 
 
 def _args():
@@ -66,9 +68,10 @@ def _args():
     p.add_argument("--one-device", action="store_true",
                    help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo collectives "
                         "(the line is marked rehearsal; not a scaling measurement)")
-    p.add_argument("--serial", action="store_true",
-                   help="time the steps one execute after the other on one stream (default: pipelined, "
-                        "lfdas.plan.LowpassPipeline; the serial time is reported beside it either way)")
+    p.add_argument("--pipelined", action="store_true",
+                   help="also time the steps through lfdas.plan.LowpassPipeline (each step's scan beside the "
+                        "next step's block pass) and report that as the value; the serial time is reported "
+                        "beside it")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 PMC traffic summary (tools/pmc_summary.py) for roofline.traffic")
     return p.parse_args()
@@ -775,7 +778,7 @@ def cpu_baseline_parallel(args, sos, sched, t0, dt_ns, tg, n_c_per=48, backend="
 def main():
     args = _args()
     global PIPELINED
-    PIPELINED = not args.serial
+    PIPELINED = args.pipelined
     rc = launch_or_check(args)
     if rc is not None:
         sys.exit(rc)

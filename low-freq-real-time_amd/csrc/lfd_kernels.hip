@@ -2720,7 +2720,8 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
 template <int NPF>
 __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch,
                                                      int W, int S, int g, float *__restrict__ y, int64_t ys_ch,
-                                                     int64_t ys_t, int seg_out, int ring_mask, int diag = 0) {
+                                                     int64_t ys_t, int seg_out, int ring_mask, int ebatch,
+                                                     int diag = 0) {
   // (diag, LFD_ROLL_SEG_DIAG, timings only: 1 = loads + lane sums only, 2 = no
   // output pass)
   diag = LFD_DG(diag);
@@ -2813,22 +2814,25 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
       } else if (has) {
         cdr[bq & ring_mask] = ccarry;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // outputs whose window ends in this tile (kS <= its last position)
+      // outputs whose window ends by this tile (kS <= its last position)
+      // leave ebatch (<= 64, a power of 2) at a time — one coalesced store
+      // per 64 outputs instead of a few lanes' per tile; the ring holds every
+      // prefix they need (launcher) — the rest after the unit's last tile
       const int kmax = min(k1 - 1, (tb + RG_P - 1) / S);
-      for (int k = kn + lane; k <= kmax && !(diag & 2); k += 64) {
-        const int j = k * Q;
-        const double sum = spr[j & ring_mask] - spr[(j - M) & ring_mask];
-        const int64_t code = cdr[j & ring_mask] - cdr[(j - M) & ring_mask];
-        const float mean = (float)(sum * inv_w);
-        yo[(int64_t)k * ys_t] = code ? null_mean(code, mean) : mean;
+      if ((kmax - kn + 1 >= ebatch || kmax == k1 - 1) && !(diag & 2)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int kend = kmax == k1 - 1 ? kmax + 1 : kn + ((kmax - kn + 1) & ~(ebatch - 1));
+        for (int k = kn + lane; k < kend; k += 64) {
+          const int j = k * Q;
+          const double sum = spr[j & ring_mask] - spr[(j - M) & ring_mask];
+          const int64_t code = cdr[j & ring_mask] - cdr[(j - M) & ring_mask];
+          const float mean = (float)(sum * inv_w);
+          yo[(int64_t)k * ys_t] = code ? null_mean(code, mean) : mean;
+        }
+        kn = kend;
       }
-      kn = max(kn, kmax + 1);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     Tile Tr[NPF + 1];
     int tb = pos0 & ~3;
@@ -5447,17 +5451,36 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
       gb = t;
     }
     const int64_t g = ga;
-    int ring = 16;
-    while (ring < W / g + RG_P / g + 3) ring *= 2;
+    // prefix ring: the boundaries of up to ebatch + (one tile's outputs)
+    // pending outputs' windows plus one tile's new boundaries (k_rolling_seg
+    // emits its outputs ebatch at a time: 64, fewer when the ring would not
+    // fit 1,024 entries).  Measured r05t on cfg2, W = 1000, S = 250: the
+    // per-tile output pass cost 2.45 vs 2.15 ms without it
+    // (profiles/r05_roll_seg_diag.txt)
+    auto ring_for = [&](int64_t eb) {
+      int64_t r = 16;
+      while (r < W / g + (eb + RG_P / S + 1) * (S / g) + RG_P / g + 3) r *= 2;
+      return r;
+    };
+    int ebatch = 64;
+    while (ebatch > 1 && ring_for(ebatch) > 1024) ebatch /= 2;
+    const int64_t ring = ring_for(ebatch);
     // (rows of any stride: 4-B aligned 16-B pieces, f4u)
     bool seg = s_t == 1 && S > 1 && S < W && g >= 16 && ring <= 1024 && n_t < (int64_t)INT32_MAX - 2 * RG_P &&
                (reinterpret_cast<uintptr_t>(x) & 3) == 0;
     if (const char *v = knob("LFD_ROLL_SEGSUM")) seg = seg && std::atoi(v) != 0;
     if (seg) {
-      int64_t span = std::max<int64_t>(32768, 8 * W);
-      if (const char *v = knob("LFD_ROLL_SEG")) span = std::max<int64_t>(4 * W, std::atoll(v));
-      while (span > std::max<int64_t>(4096, 4 * W) && n_ch * ((n_t + span - 1) / span) < 16384) span /= 2;
-      const int64_t seg_out = std::max<int64_t>(1, span / S);
+      // units: each channel cut into the fewest equal pieces that give >= 3
+      // rounds of the resident waves (16 per CU) — a unit's first loads wait
+      // a full memory latency, so long units stream better: cfg2 at S = 250
+      // 32,768-position units (23 rounds) 2.36 ms, 65,536 2.29, 200,000 (3
+      // per channel) 2.25 (profiles/r05_roll_seg_diag.txt) — and >= 4W
+      // positions each (the halo re-read)
+      const int64_t resident = 16 * (int64_t)cu_count();
+      const int64_t pieces = std::max<int64_t>(1, (3 * resident + n_ch - 1) / n_ch);
+      int64_t seg_out = std::max<int64_t>((n_out + pieces - 1) / pieces, (4 * W + S - 1) / S);
+      if (const char *v = knob("LFD_ROLL_SEG")) seg_out = std::max<int64_t>(4 * W, std::atoll(v)) / S;
+      seg_out = std::max<int64_t>(1, seg_out);
       const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
       int64_t blocks = (units + 3) / 4;
       if (blocks > cap_unit) blocks = cap_unit;
@@ -5480,10 +5503,10 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
           if (e != hipSuccess) return e;
           if (pf == 1)
             k_rolling_seg<1><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y,
-                                                                 ys_ch, ys_t, (int)seg_out, ring - 1);
+                                                                 ys_ch, ys_t, (int)seg_out, (int)ring - 1, ebatch);
           else
             k_rolling_seg<3><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y,
-                                                                 ys_ch, ys_t, (int)seg_out, ring - 1);
+                                                                 ys_ch, ys_t, (int)seg_out, (int)ring - 1, ebatch);
           return hipGetLastError();
         }
       }
@@ -5491,7 +5514,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
       int sdiag = 0;
       if (const char *v = knob("LFD_ROLL_SEG_DIAG")) sdiag = std::atoi(v);
       k_rolling_seg<2><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y, ys_ch,
-                                                           ys_t, (int)seg_out, ring - 1, sdiag);
+                                                           ys_t, (int)seg_out, (int)ring - 1, ebatch, sdiag);
       return hipGetLastError();
     }
   }
