@@ -5727,7 +5727,13 @@ template <int Q, bool DB = false>
 constexpr size_t fdm_lds_bytes() {
   return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32) * (DB ? 2 : 1);
 }
-template <int Q, bool DB = false>
+// SB: a scheduling barrier after SB of a phase's DM Toeplitz steps
+// (production SB = DM: at the phase's end).  Without it the compiler hoisted
+// the next phase's f32 -> f64 conversions — and so the wait for that phase's
+// LDS reads, issued at this phase's start — in between this phase's first
+// MFMAs: 2,000 x 600,000 at q = 10 1.648 -> 1.565 ms (SB = 0 / 3 / 4 / 5 / 6:
+// 1.648 / 1.653 / 1.623 / 1.593 / 1.565, profiles/r05_fir_sched.txt)
+template <int Q, bool DB = false, int SB = 0>
 __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
                                                           int64_t s_ch, const double *__restrict__ h, int n_taps,
                                                           int64_t delay, int64_t n_out, int64_t tiles_o, int strip,
@@ -5870,6 +5876,7 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(ac[d], bd[4 * t + DM - 1 - d], acc[t], 0, 0, 0);
+          if (SB > 0 && d == DM - SB) __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
@@ -5915,33 +5922,44 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     const bool db = knob_flag("LFD_FIR_DB");  // double-buffered staging (measured, not kept)
     bool launched = false;
     hipError_t e = hipSuccess;
-#define LFD_FDM1(QV, DBV)                                                                                    \
+#define LFD_FDM1(QV, DBV, SBV)                                                                               \
   {                                                                                                          \
     static bool attr = false;                                                                                \
     if (!attr) {                                                                                             \
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV, DBV>),                 \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV, DBV, SBV>),            \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV, DBV>());    \
       if (e != hipSuccess) return e;                                                                         \
       attr = true;                                                                                           \
     }                                                                                                        \
-    k_fir_decimate_mfma<QV, DBV><<<(unsigned)grid, 256, fdm_lds_bytes<QV, DBV>(), st>>>(                    \
+    k_fir_decimate_mfma<QV, DBV, SBV><<<(unsigned)grid, 256, fdm_lds_bytes<QV, DBV>(), st>>>(               \
         x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, diag);                  \
   }
 #ifdef LFD_DIAG
-#define LFD_FDM(QV)          \
-  case QV: {                 \
-    if (db)                  \
-      LFD_FDM1(QV, true)     \
-    else                     \
-      LFD_FDM1(QV, false)    \
-    launched = true;         \
-    break;                   \
+    // LFD_FIR_SB (q = 10): the phase barrier after 0 (none: the compiler
+    // hoists the next phase's conversions into the phase's first MFMAs), 3 or
+    // 4 of the 6 Toeplitz steps (production: 6)
+    int sb = FDM_DM;
+    if (const char *v = knob("LFD_FIR_SB")) sb = std::atoi(v);
+#define LFD_FDM(QV)                          \
+  case QV: {                                 \
+    if (QV == 10 && sb == 0)                 \
+      LFD_FDM1(10, false, 0)                 \
+    else if (QV == 10 && sb == 3)            \
+      LFD_FDM1(10, false, 3)                 \
+    else if (QV == 10 && sb == 4)            \
+      LFD_FDM1(10, false, 4)                 \
+    else if (db)                             \
+      LFD_FDM1(QV, true, FDM_DM)             \
+    else                                     \
+      LFD_FDM1(QV, false, FDM_DM)            \
+    launched = true;                         \
+    break;                                   \
   }
 #else
 #define LFD_FDM(QV)          \
   case QV: {                 \
     (void)db;                \
-    LFD_FDM1(QV, false)      \
+    LFD_FDM1(QV, false, FDM_DM) \
     launched = true;         \
     break;                   \
   }
