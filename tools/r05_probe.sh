@@ -1,9 +1,7 @@
-# round-5: full GPU suite + default bench
+# round-5: rolling S = 1 (k_rolling_scan_tc) span / cap A/B
 set -o pipefail
-O=gpurun_out/r05y
+O=gpurun_out/r05z3
 mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
-echo "pytest exit $?"; tail -3 $O/pytest_gpu.log
-timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
-echo "bench exit $?"
-python tools/bench_summary.py $O/bench.json
+export LFDAS_LIB="$PWD/low-freq-real-time_amd/lfdas/liblfdas_diag.so"
+timeout -k 10 400 python tools/roll_ab.py 1000 1 "" "LFD_ROLL_SEG=16384" "LFD_ROLL_SEG=8192" "LFD_ROLL_CAP=4096" "LFD_ROLL_CAP=16384" "LFD_ROLL_MINW=4" > $O/roll_ab1.txt 2>&1
+echo "exit $?"; grep -E "W=|bit" $O/roll_ab1.txt
