@@ -1060,6 +1060,23 @@ typedef double fr_d4v __attribute__((ext_vector_type(4)));
 // LFD_FR_STAGE_OLD=1 (A/B knob): the big block's loads in groups of 8 dwords
 #ifdef LFD_DIAG
 __constant__ int g_fr_stage_old = 0;
+// LFD_FR_STAGGER (diag A/B): the output pass's first 4,096 waves sleep
+// 0-3 x this many 2,048-cycle units (a hashed slot), so the waves sharing a
+// SIMD do not run their load / scan / MFMA phases in lock step
+__constant__ int g_fr_stagger = 0;
+// LFD_FR_TIMES (diag): phase stamps of the output pass's first 16,384 waves
+__device__ uint64_t g_fr_times[16384 * 8];
+#define FR_STAMP(i)                                                                                   \
+  do {                                                                                                \
+    if (blockIdx.x < 16384) {                                                                         \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                           \
+      if (threadIdx.x == 0) g_fr_times[(size_t)blockIdx.x * 8 + (i)] = t_;                            \
+    }                                                                                                 \
+  } while (0)
+#else
+#define FR_STAMP(i) \
+  do {              \
+  } while (0)
 #endif
 #ifndef FRS_Q
 // k_fullrate_scan: big blocks per load batch (8: 0.83 ms vs 0.91 at 4 on the
@@ -1139,6 +1156,7 @@ __device__ __forceinline__ void fr_out_mfma(int lane, const FRConst *__restrict_
     }
     __syncthreads();
   }
+  FR_STAMP(5);
 }
 
 // One DPP lane move of a double inside 16-lane rows (both 32-bit halves;
@@ -1441,6 +1459,13 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
   // reads 9.55 -> 5.08 GB per launch at 2,000 x 600,000 (x 4.8 GB + SF / ST
   // 0.3 GB algorithmic; channel-major re-fetched each 128-B line of states
   // once per channel), 3.89 -> 3.84 ms (profiles/r04au_fr_ab_block_order.txt)
+  FR_STAMP(0);
+#ifdef LFD_DIAG
+  if (g_fr_stagger && blockIdx.x < 4096) {
+    const int slot = (int)(((uint32_t)blockIdx.x * 2654435761u) >> 30);
+    for (int i = 0; i < slot * g_fr_stagger; ++i) __builtin_amdgcn_s_sleep(32);
+  }
+#endif
   int64_t bid = blockIdx.x;
   if (ord == 2 && (gridDim.x & 7) == 0) bid = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
   const int64_t ch = ord ? bid % n_ch : bid / nb, k = ord ? bid / n_ch : bid % nb;
@@ -1489,6 +1514,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     }
   }
   __syncthreads();
+  FR_STAMP(1);
   const float *tb = tile + TS * col + q;  // B[k = q][j = col] of tile nt, k-step ks: tb[TS*16*nt + 4*ks]
   // ---- 1. sub-block exits on the matrix cores
   double A[N], Z[N];
@@ -1523,6 +1549,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       Z[n] = f[(N + n) / 4][(N + n) % 4];
     }
   }
+  FR_STAMP(2);
   auto matvec_add = [&](const double *P, const double (&o)[N], double (&v)[N], bool tri) {
 #pragma unroll
     for (int r = 0; r < N; ++r) {
@@ -1588,6 +1615,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       W[N + n] = jr == 15 ? Tin[n] : u;
     }
   }
+  FR_STAMP(3);
   // ---- 3. y = Kr x + Q w on the matrix cores
   // state product first (W dies as it is consumed), then Kr x from the tile.
   // B operand of the state product: k-step ks, tile nt at row q =
@@ -1616,6 +1644,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       mfma_k4<M4>(fc->KRA[mt][ks][lane], bx, yacc[mt]);
     }
   }
+  FR_STAMP(4);
   double *yr = y + ch * ys_ch + a * ys_t;
   const int nsb = nvs / LS;
   if constexpr (DIRECT) {
@@ -5261,6 +5290,8 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
   if (stage_old < 0) {
     stage_old = knob_flag("LFD_FR_STAGE_OLD") ? 1 : 0;
     if (stage_old) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stage_old), &stage_old, sizeof(int));
+    const int stagger = knob("LFD_FR_STAGGER") ? std::atoi(knob("LFD_FR_STAGGER")) : 0;
+    if (stagger) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stagger), &stagger, sizeof(int));
   }
 #endif
 #define LFD_FR(NS, OUT) \
@@ -5272,9 +5303,6 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
   static const int fr_pre = knob("LFD_FR_PRE") ? std::atoi(knob("LFD_FR_PRE")) : -1;
   static const int fr_ord = knob("LFD_FR_ORDER") ? std::atoi(knob("LFD_FR_ORDER")) : 2;
 #else
-  constexpr bool fr_direct = false;
-  constexpr int fr_lay = 1;
-  constexpr bool fr_m4 = false;
   constexpr int fr_ord = 2;
 #endif
 #ifdef LFD_DIAG
@@ -5292,17 +5320,27 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
 #else
 #define LFD_FR_PRE_AB(NS)
 #endif
+#ifdef LFD_DIAG
+#define LFD_FR_LAY_AB(NS)                                                                                        \
+  if (out && mb && fr_m4)                                                                                        \
+    k_fullrate_out_mb<NS, false, 1, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y,  \
+                                                                         ys_ch, ys_t);                           \
+  else if (out && mb && fr_direct)                                                                               \
+    k_fullrate_out_mb<NS, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
+  else if (out && mb && fr_lay == 0)                                                                             \
+    k_fullrate_out_mb<NS, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch,  \
+                                                                   ys_t);                                        \
+  else if (out && mb && fr_lay == 2)                                                                             \
+    k_fullrate_out_mb<NS, false, 2><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch,  \
+                                                                   ys_t);                                        \
+  else
+#else
+#define LFD_FR_LAY_AB(NS)
+#endif
 #define LFD_FR2(NS)   \
   LFD_FR_PRE_AB(NS) \
-  if (out && mb && fr_m4)      \
-    k_fullrate_out_mb<NS, false, 1, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
-  else if (out && mb && fr_direct)      \
-    k_fullrate_out_mb<NS, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
-  else if (out && mb && fr_lay == 0)      \
-    k_fullrate_out_mb<NS, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
-  else if (out && mb && fr_lay == 2)      \
-    k_fullrate_out_mb<NS, false, 2><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
-  else if (out && mb)      \
+  LFD_FR_LAY_AB(NS) \
+  if (out && mb)      \
     k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t, fr_ord); \
   else if (out)       \
     LFD_FR(NS, true); \
@@ -5316,7 +5354,31 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
     default: return hipErrorInvalidValue;
   }
 #undef LFD_FR2
+#undef LFD_FR_LAY_AB
+#undef LFD_FR_PRE_AB
 #undef LFD_FR
+#ifdef LFD_DIAG
+  if (out && mb && knob_flag("LFD_FR_TIMES")) {
+    // phase durations (us, mean over the first waves): 0-1 tile load, 1-2
+    // KAZ products + transposes, 2-3 row scans, 3-4 Q / Kr products, 4-5 stage
+    // + stores; and the first start -> last end of those waves
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    const size_t nw = (size_t)std::min<int64_t>(n_wg, 16384);
+    std::vector<uint64_t> t(nw * 8);
+    e = hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_fr_times), t.size() * sizeof(uint64_t));
+    if (e != hipSuccess) return e;
+    double d[5] = {0, 0, 0, 0, 0};
+    uint64_t t0 = ~0ull, t1 = 0;
+    for (size_t b = 0; b < nw; ++b) {
+      for (int i = 0; i < 5; ++i) d[i] += 0.01 * (double)(t[b * 8 + i + 1] - t[b * 8 + i]);
+      t0 = std::min(t0, t[b * 8]);
+      t1 = std::max(t1, t[b * 8 + 5]);
+    }
+    fprintf(stderr, "k_fullrate_out_mb us/wave: load %.2f kaz %.2f scans %.2f qkr %.2f store %.2f; %zu waves span %.1f us\n",
+            d[0] / nw, d[1] / nw, d[2] / nw, d[3] / nw, d[4] / nw, nw, 0.01 * (double)(t1 - t0));
+  }
+#endif
   return hipGetLastError();
 }
 
