@@ -1358,47 +1358,12 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
   swap16_d(v2, v3);
 }
 
-// One 16x16x4 fp64 MFMA step as four v_mfma_f64_4x4x4_4b (M4): the same
-// 1,024 MACs at 4 x 18.5 instead of ~109 cycles per SIMD with dense A
-// operands (tools/ubench_mfma64b.hip, profiles/r02_ubench_mfma64b.txt).  The
-// 4x4x4_4b lane layout (A[i][k] at lane 16k + 4b + i, B[k][j] at 16k + 4b + j,
-// D[i][j] at 16i + 4b + j; tools/check_mfma4x4.hip) makes B the 16x16x4 B
-// register unchanged and D[r] the 16x16x4 accumulator's row q + 4r when A is
-// the 16x16x4 A register with quad r of every 16-lane row broadcast to its
-// four quads: ds_swizzle bit-mask mode (and 0x13, or 4r: lane bits 0, 1, 4
-// kept, bits 2, 3 = r), a lane crossbar with no memory access.
-// quad r of every 16-lane row broadcast to the row's four quads (ds_swizzle
-// bit-mask mode: and 0x13, or 4r — lane bits 0, 1, 4 kept, bits 2, 3 = r):
-// the 4x4x4_4b A operand of functional group r from a 16x16x4 A register
-// (mfma_k4, mf_iter_s)
-template <int FG>
-__device__ __forceinline__ double quad_bcast(double v) {
-  constexpr int pat = 0x13 | ((FG << 2) << 5);
-  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
-  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
-  return __hiloint2double(hi, lo);
-}
 // one k-step of A (this lane's 16x16x4 A value) against four column tiles
-// (one broadcast variant live at a time)
-template <bool M4>
+// (the 4x4x4_4b form of the same products measured slower,
+// profiles/r02_ubench_mfma64b.txt)
 __device__ __forceinline__ void mfma_k4(double av, const double (&b)[4], fr_d4v (&acc)[4]) {
-  if constexpr (M4) {
-    const double a0 = quad_bcast<0>(av);
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, b[nt], acc[nt][0], 0, 0, 0);
-    const double a1 = quad_bcast<1>(av);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, b[nt], acc[nt][1], 0, 0, 0);
-    const double a2 = quad_bcast<2>(av);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, b[nt], acc[nt][2], 0, 0, 0);
-    const double a3 = quad_bcast<3>(av);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt][3] = __builtin_amdgcn_mfma_f64_4x4x4f64(a3, b[nt], acc[nt][3], 0, 0, 0);
-  } else {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[nt], acc[nt], 0, 0, 0);
-  }
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[nt], acc[nt], 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1415,37 +1380,25 @@ __device__ __forceinline__ void mfma_k4(double av, const double (&b)[4], fr_d4v 
 //      staged through the tile's LDS into rows and stored as 16-B pieces.
 // The round-3 output pass ran the zero-state responses as TDF-II recurrences
 // (40 fp64 FMAs per sample on the VALU: the pass was fp64-issue bound).
-// DIRECT (diag A/B): y stored straight from the MFMA layout (32-B pieces per
-// lane quad, 4 instructions per 128-B line) instead of through the LDS stage
-// LAY: 1 (production) = tile rows 36 floats apart written as 16-B pieces,
-// row reads pairing rows r and r + 1; 0 (diag A/B) = the bank-conflict-free
-// layout below (tile rows 34 floats apart, 8-B staging writes, r / r + 8 row
-// reads): 2.5x fewer SQ_LDS_BANK_CONFLICT cycles (1.9e8 -> 7.5e7 per call)
-// but 1 % slower on the same box (4.19 vs 4.14 ms; the pass is matrix-core
-// bound, profiles/r04h_fr_ab_lds_layout.txt); 2 (diag) = the 36-float tile
-// with the r / r + 8 row reads (4.17 ms)
-// M4: every product as 4x4x4_4b steps (mfma16x4)
-// PRE: the entering states SF (PRE >= 1) and ST (PRE = 2, production) are
-// loaded at the kernel start with the tile, so their latency hides behind
-// the tile's and the KAZ products instead of stalling the row scans: 3.92
-// vs 3.98 ms (PRE 0) and 4.00 (PRE 1) at 2,000 x 600,000
-// (profiles/r04ao_fr_ab_early_states.txt; diag knob LFD_FR_PRE=0 / 1)
-template <int NS, bool DIRECT = false, int LAY = 1, bool M4 = false, int PRE = 2>
+// The tile's sub-block rows are 36 floats apart, written as 16-B pieces; the
+// entering states SF / ST load at the kernel start with the tile, so their
+// latency hides behind the tile's and the KAZ products (3.92 vs 3.98 ms
+// loading them at the scans, profiles/r04ao_fr_ab_early_states.txt).
+// (Measured and removed, records in profiles/: stores straight from the MFMA
+// layout, the bank-conflict-free 34-float layout — 2.5x fewer LDS conflicts,
+// 1 % slower, profiles/r04h_fr_ab_lds_layout.txt — 4x4x4_4b products, the KAZ
+// column preloaded.)
+template <int NS>
 __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     const float *__restrict__ x, int64_t s_ch, int64_t n_ch, int64_t nb, int64_t n_mb,
     const FRConst *__restrict__ fc, const double *__restrict__ SF, const double *__restrict__ ST,
     double *__restrict__ y, int64_t ys_ch, int64_t ys_t, int ord = 0) {
   constexpr int N = 2 * NS, LS = FR_LS, L = FR_L, K = 2 * N, KS = K / 4, OSTR = 18;
   static_assert(N % 2 == 0 && K % 4 == 0, "state components in groups of 4");
-  // LDS banks (gfx950: 32 banks for 4-B accesses, 64 for 8 / 16 B): the
-  // tile's sub-block rows are TS = 34 floats apart, so the MFMA B reads (lane
-  // (q, col) reads row col + q: 2 col + q mod 32) are conflict-free, and
-  // each 8-B staging write pairs rows i and i + 16 (34 x 16 = 32 mod 64);
-  // the output stage's rows are OSTR = 18 doubles apart (MFMA-layout 8-B
-  // writes: 36 col + 2 q distinct mod 64 per half wave) and each 16-B row
-  // read pairs rows r and r + 8 (36 x 8 = 32 mod 64)
-  constexpr bool T36 = LAY != 0;
-  constexpr int TS = T36 ? 36 : 34;
+  // LDS: the tile's sub-block rows TS = 36 floats apart (float4 staging
+  // writes); the output stage's rows OSTR = 18 doubles apart (MFMA-layout
+  // 8-B writes: 36 col + 2 q distinct mod 64 per half wave)
+  constexpr int TS = 36;
   constexpr int TLDS = 64 * TS;
   constexpr int NLDS = 64 * OSTR > TLDS / 2 ? 64 * OSTR : TLDS / 2;
   __shared__ __attribute__((aligned(16))) double lds[NLDS];
@@ -1473,26 +1426,18 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
   const int nvs = (int)(n_mb - 4 * k < 4 ? (n_mb - 4 * k) * FR_LB : L);
   const int64_t m_row = 4 * k + (lane >> 4);
   const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
-  double SinE[PRE >= 1 ? N : 1], TinE[PRE >= 2 ? N : 1];
-  if constexpr (PRE >= 1) {
+  double SinE[N], TinE[N];
 #pragma unroll
-    for (int n = 0; n < N; ++n) SinE[n] = SF[(m * N + n) * n_ch + ch];
-  }
-  if constexpr (PRE >= 2) {
-#pragma unroll
-    for (int n = 0; n < N; ++n) TinE[n] = ST[((m + 1) * N + n) * n_ch + ch];
-  }
-  double kazE[PRE >= 3 ? LS / 4 : 1];  // (PRE 3, diag: the KAZ column too)
-  if constexpr (PRE >= 3) {
-#pragma unroll
-    for (int ks = 0; ks < LS / 4; ++ks) kazE[ks] = fc->KAZ[ks][lane];
+  for (int n = 0; n < N; ++n) {
+    SinE[n] = SF[(m * N + n) * n_ch + ch];
+    TinE[n] = ST[((m + 1) * N + n) * n_ch + ch];
   }
   {
     const float *row = x + ch * s_ch + a;
     if (nvs < L) {
 #pragma unroll 8
       for (int u = lane; u < L; u += 64) tile[(u >> 5) * TS + (u & 31)] = u < nvs ? row[u] : 0.0f;
-    } else if constexpr (T36) {
+    } else {
       // (rows need not be 16-B aligned: f4u pieces)
       f4v v[L / 256];
 #pragma unroll
@@ -1502,15 +1447,6 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
         const int u = 4 * lane + 256 * i;
         *reinterpret_cast<f4v *>(tile + u + 4 * (u >> 5)) = v[i];
       }
-    } else {
-      // instruction i: lane quarter g = lane >> 4 reads sub-block 16 g + i
-      // (4 x 128-B pieces), 2 samples per lane
-      const int g = lane >> 4, e2 = 2 * (lane & 15);
-      f2u v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const f2u *>(row + (16 * g + i) * LS + e2);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) *reinterpret_cast<f2u *>(tile + (16 * g + i) * TS + e2) = v[i];
     }
   }
   __syncthreads();
@@ -1524,11 +1460,11 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     for (int nt = 0; nt < 4; ++nt) acc[nt] = fr_d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int ks = 0; ks < LS / 4; ++ks) {
-      const double av = PRE >= 3 ? kazE[ks] : fc->KAZ[ks][lane];
+      const double av = fc->KAZ[ks][lane];
       double bk[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) bk[nt] = (double)tb[TS * 16 * nt + 4 * ks];
-      mfma_k4<M4>(av, bk, acc);
+      mfma_k4(av, bk, acc);
     }
     // acc[nt][r] at row q = functional q + 4r of sub-block 16 nt + col: per r,
     // transpose (row q <-> register nt) -> at row R, register q' = functional
@@ -1566,7 +1502,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     double Sin[N], vf[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      Sin[n] = PRE >= 1 ? SinE[n] : SF[(m * N + n) * n_ch + ch];
+      Sin[n] = SinE[n];
       vf[n] = A[n];
     }
     if (jr == 0) matvec_add(fc->PhiP[0], Sin, vf, true);
@@ -1595,7 +1531,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     matvec_add(fc->M32, Sj, vb, false);
     double Tin[N];
 #pragma unroll
-    for (int n = 0; n < N; ++n) Tin[n] = PRE >= 2 ? TinE[n] : ST[((m + 1) * N + n) * n_ch + ch];
+    for (int n = 0; n < N; ++n) Tin[n] = TinE[n];
     if (jr == 15) matvec_add(fc->PhiP[0], Tin, vb, true);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1631,7 +1567,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     rows_transpose4(bop[0], bop[1], bop[2], bop[3]);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      mfma_k4<M4>(fc->QA[mt][ks][lane], bop, yacc[mt]);
+      mfma_k4(fc->QA[mt][ks][lane], bop, yacc[mt]);
     }
   }
 #pragma unroll
@@ -1641,26 +1577,12 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     for (int nt = 0; nt < 4; ++nt) bx[nt] = (double)tb[TS * 16 * nt + 4 * ks];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      mfma_k4<M4>(fc->KRA[mt][ks][lane], bx, yacc[mt]);
+      mfma_k4(fc->KRA[mt][ks][lane], bx, yacc[mt]);
     }
   }
   FR_STAMP(4);
   double *yr = y + ch * ys_ch + a * ys_t;
   const int nsb = nvs / LS;
-  if constexpr (DIRECT) {
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int sb = 16 * nt + col;
-        if (sb < nsb) {
-          double *o = yr + (int64_t)(sb * LS + 16 * mt + q) * ys_t;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[4 * r * ys_t] = yacc[mt][nt][r];
-        }
-      }
-    return;
-  }
   __syncthreads();  // the tile's reads are done: its LDS becomes the output stage
   double *ob = lds;
 #pragma unroll
@@ -1678,7 +1600,7 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
     if (ys_t == 1) {  // 16-B pieces, 8-B aligned on rows of odd length (d2u)
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
-        const int r = LAY == 1 ? it * 8 + (lane >> 3) : it + 8 * (lane >> 3), c2 = 2 * (lane & 7);
+        const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
         if (r < nsb)
           *reinterpret_cast<d2u *>(yr + r * LS + 16 * mt + c2) = *reinterpret_cast<const d2u *>(ob + r * OSTR + c2);
       }
@@ -2422,10 +2344,10 @@ __device__ __forceinline__ float null_mean(int64_t code, float mean) {
   return mean;
 }
 
-// STAGE (A/B knob LFD_ROLL_STAGE): bit 0 = loads are coalesced float4 (lane
-// 4l + 256j) staged through a wave-private LDS tile into lane-consecutive
-// order; bit 1 = S == 1 outputs leave through LDS the same way (coalesced
-// float4 stores); else lanes load / store their 8 positions directly.
+// STAGE: 2 = S == 1 outputs leave through a wave-private LDS tile as
+// coalesced float4 stores (lane 4l + 256j); 0 = lanes store their 8
+// positions directly (unaligned rows).  Loads: lanes read their 8
+// consecutive positions directly.
 constexpr int RS_ROW = RS_E + 4;    // padded LDS row (floats): conflict-free ds_read_b128
 // RING: the samples leaving the window, x[t - W], come from a wave-private
 // LDS ring of the last ring_mask + 1 >= W + 512 samples (each step writes
@@ -2437,13 +2359,11 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch, int W, int S,
     float *__restrict__ y, int64_t ys_ch, int64_t ys_t, int seg_out, bool vec_out, int ring_mask, bool scan_dpp) {
   // positions are row-relative int32 (the launcher checks n_t < 2^31 - 1024)
-  __shared__ __attribute__((aligned(16))) float lds_all[(STAGE & 3) ? 4 : 1][(STAGE & 1) ? 2 : 1]
-                                                       [(STAGE & 3) ? 64 * RS_ROW : 4];
+  __shared__ __attribute__((aligned(16))) float lds_all[(STAGE & 2) ? 4 : 1][(STAGE & 2) ? 64 * RS_ROW : 4];
   extern __shared__ __attribute__((aligned(16))) float rs_ring_all[];
   float *ring = rs_ring_all + (RING ? (threadIdx.x >> 6) * (ring_mask + 1) : 0);
   const int lane = threadIdx.x & 63;
-  float *lx = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][0];
-  float *lo_ = lds_all[(STAGE & 3) ? threadIdx.x >> 6 : 0][(STAGE & 1) ? 1 : 0];
+  float *lx = lds_all[(STAGE & 2) ? threadIdx.x >> 6 : 0];
   const int n_out = (n_t + S - 1) / S;
   const int n_seg = (n_out + seg_out - 1) / seg_out;
   const int64_t n_units = (int64_t)n_seg * n_ch;
@@ -2501,25 +2421,7 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         }
         return;
       }
-      if ((STAGE & 1) && VEC && full) {
-        // coalesced: float4 j of lane l = positions 4l + 256j (unstaged here;
-        // process() moves them to lane-consecutive order through LDS)
-#pragma unroll
-        for (int h = 0; h < RS_E / 4; ++h) {
-          const int tc = tb + 4 * lane + 256 * h;
-          const f4v a = *reinterpret_cast<const f4u *>(row + tc);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
-          if ((W & 3) == 0) {
-            const f4v b = *reinterpret_cast<const f4u *>(row + tc - W);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = b[e];
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) T.xo[4 * h + e] = row[tc + e - W];
-          }
-        }
-      } else if (VEC && full) {
+      if (VEC && full) {
 #pragma unroll
         for (int h = 0; h < RS_E / 4; ++h) {
           const f4v a = *reinterpret_cast<const f4u *>(row + t + 4 * h);
@@ -2566,32 +2468,6 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
         } else {
 #pragma unroll
           for (int e = 0; e < RS_E; ++e) T.xo[e] = ring[(t + e - W) & ring_mask];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      if (!RING && (STAGE & 1) && VEC && tb + RS_P <= n_t && tb - W >= 0) {
-        // coalesced -> lane-consecutive through LDS (padded rows of 12 floats)
-#pragma unroll
-        for (int h = 0; h < RS_E / 4; ++h) {
-          const int pos = 4 * lane + 256 * h;
-          const int off = (pos / RS_E) * RS_ROW + (pos % RS_E);
-          *reinterpret_cast<f4v *>(lx + off) = f4v{Tin.xi[4 * h], Tin.xi[4 * h + 1], Tin.xi[4 * h + 2], Tin.xi[4 * h + 3]};
-          *reinterpret_cast<f4v *>(lo_ + off) = f4v{Tin.xo[4 * h], Tin.xo[4 * h + 1], Tin.xo[4 * h + 2], Tin.xo[4 * h + 3]};
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int h = 0; h < RS_E / 4; ++h) {
-          const f4v a = *reinterpret_cast<const f4v *>(lx + lane * RS_ROW + 4 * h);
-          const f4v b = *reinterpret_cast<const f4v *>(lo_ + lane * RS_ROW + 4 * h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            T.xi[4 * h + e] = a[e];
-            T.xo[4 * h + e] = b[e];
-          }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -2933,31 +2809,6 @@ __device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o0, int lo, i
 }
 
 
-// (M4S) the same 16 MFMA steps as 4 x 4 v_mfma_f64_4x4x4_4b with A from the
-// lane's 16x16x4 taps through quad_bcast: the D layout stays acc0/acc1's
-template <bool M4S>
-__device__ __forceinline__ void mf_iter_s(const double *kt, int kstride, const f4v (&cur)[4], d4v &acc0, d4v &acc1) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double2 b01 = *reinterpret_cast<const double2 *>(kt + j * kstride);
-    const double2 b23 = *reinterpret_cast<const double2 *>(kt + j * kstride + 2);
-    const double a[4] = {b01.x, b01.y, b23.x, b23.y};
-    const double bv[4] = {(double)cur[j].x, (double)cur[j].y, (double)cur[j].z, (double)cur[j].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      d4v &acc = (e & 1) ? acc1 : acc0;
-      if constexpr (M4S) {
-        acc[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<0>(a[e]), bv[e], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<1>(a[e]), bv[e], acc[1], 0, 0, 0);
-        acc[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<2>(a[e]), bv[e], acc[2], 0, 0, 0);
-        acc[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(quad_bcast<3>(a[e]), bv[e], acc[3], 0, 0, 0);
-      } else {
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], bv[e], acc, 0, 0, 0);
-      }
-    }
-  }
-}
-
 // 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur.
 // Lanes of A rows c >= nc read a copy of row nc-1 instead of zeros: MFMA rows
 // are independent (D[c][:] depends on A[c][:] only) and rows >= nc of D are
@@ -2998,7 +2849,7 @@ __device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<c
 // invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
 // ceiling of the x stream + F stores; 3 = no MFMA and no F stores = the
 // x-stream ceiling alone.
-template <int PF, int MODE, bool M4S = false>
+template <int PF, int MODE>
 __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs,
@@ -3103,10 +2954,7 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
           const int v = (int)(s & 3);
           mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
         }
-        if constexpr (M4S)
-          mf_iter_s<true>(kt + (4 * it) * kstride, kstride, buf[u], acc0, acc1);
-        else
-          mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
+        mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
       }
       if (++it == nit) {
         if (MODE == 6) {  // diagnostic: same stores into a 64 KB L2-resident window
@@ -3486,32 +3334,25 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
 // k_block_runs_mfma_tm — run-mode K1 for (time, channel) storage (the real
 // files' layout, low_pass_dascore.ipynb cell 14 data[:, ch]: s_ch = 1, rows
 // of s_t floats).  A wave owns 32 channels = one 128-B line of every sample
-// row, i.e. two MFMA column tiles (channels 0-15, 16-31).  Per MFMA step
-// (16-sample group j, step e) the four samples 16j + e + {0, 4, 8, 12} of
-// the block row are loaded with two dword loads, P (rows +0, +4) and Q (+8,
-// +12): lane l reads channel l & 31 of row 4 (l >> 5), so every load
-// instruction reads two whole lines.  v_permlane32_swap + v_permlane16_swap
-// then leave lane 16k + c holding row k of channel c (P: tile 0) and of
-// channel 16 + c (Q: tile 1) — the B operand layout of
-// v_mfma_f64_16x16x4_f64 with the channel-major kernel's sample order, so
-// the same tap table (row shift 0) and the same run epilogue apply, once per
-// tile.  512-thread workgroups: taps + 8 waves x 2 run buffers in LDS.
+// row, i.e. two MFMA column tiles.  Lane (q, col) loads row +4q of its
+// channels (X2: the channel pair 2 col, 2 col + 1 with one 8-B load, tile 0
+// = even channels, tile 1 = odd, so every load instruction reads 4 whole
+// 128-B lines; else col and 16 + col with two dword loads), i.e. the B
+// operand layout of v_mfma_f64_16x16x4_f64 with the channel-major kernel's
+// sample order: the same tap table (row shift 0) and the same run algebra
+// apply, once per tile.  (Measured and removed, records in profiles/ and
+// CHANGELOG.md: permlane-swapped row loads, one tile per wave, 4x4x4 steps,
+// 768-thread groups, prefetch depth 3, 128-thread groups.)
 // ---------------------------------------------------------------------------
 
 struct TmIter {
   float p[4][4], q[4][4];  // [16-sample group j][step e]
 };
 
-// SWAP: lane l reads channel l & 31 of rows +4 (l >> 5) (P) and +8 + 4 (l >> 5)
-// (Q); else lane (q, col) reads channel col (P) and 16 + col (Q) of row +4q
-// (two half lines of the same rows back to back; A/B knob LFD_TM_SWAP=0).
 // Interior loads: the row pointer is wave-uniform (SGPR base) and the lane's
 // part a 32-bit element offset, so a load needs no per-lane 64-bit address
 // arithmetic (global_load ... saddr).
-// X2: lane (q, col) reads channels 2 col, 2 col + 1 of row +4q with one
-// 8-B load (tile 0 = even channels, tile 1 = odd): every load instruction
-// reads 4 whole 128-B lines, half as many instructions as two dword loads
-template <bool SWAP, int NTILE = 2, bool X2 = false>
+template <bool X2>
 __device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c0, int64_t s_t, int64_t row0,
                                           uint32_t offp, uint32_t offq, TmIter &b) {
 #pragma unroll
@@ -3520,44 +3361,34 @@ __device__ __forceinline__ void tm_load_u(const float *__restrict__ x, int64_t c
     for (int e = 0; e < 4; ++e) {
       const int64_t ro = uniform64(c0 + (row0 + 16 * j + e) * s_t);  // element offset of the row
       const char *rp = reinterpret_cast<const char *>(x + ro);
-      const char *rq = SWAP ? reinterpret_cast<const char *>(x + ro + 8 * s_t) : rp;
       if (X2) {
         const float2 v = *reinterpret_cast<const float2 *>(rp + offp);
         b.p[j][e] = v.x;
         b.q[j][e] = v.y;
       } else {
         b.p[j][e] = *reinterpret_cast<const float *>(rp + offp);
-        if (NTILE == 2) b.q[j][e] = *reinterpret_cast<const float *>(rq + offq);
+        b.q[j][e] = *reinterpret_cast<const float *>(rp + offq);
       }
     }
 }
 
-template <bool GUARD, bool SWAP, int NTILE = 2>
-__device__ __forceinline__ void tm_load(const float *__restrict__ xc, const float *__restrict__ xq, int64_t s_t,
-                                        int64_t n_t, int64_t row0, TmIter &b) {
+// the edge blocks' loads: rows outside [0, n_t) read 0
+__device__ __forceinline__ void tm_load_guarded(const float *__restrict__ xc, const float *__restrict__ xq,
+                                                int64_t s_t, int64_t n_t, int64_t row0, TmIter &b) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int64_t rp = row0 + 16 * j + e, rq = SWAP ? rp + 8 : rp;
-      if (GUARD) {
-        const int64_t cp = rp < 0 ? 0 : (rp >= n_t ? n_t - 1 : rp);
-        const int64_t cq = rq < 0 ? 0 : (rq >= n_t ? n_t - 1 : rq);
-        const float vp = xc[cp * s_t], vq = NTILE == 2 ? xq[cq * s_t] : 0.0f;
-        b.p[j][e] = (rp >= 0 && rp < n_t) ? vp : 0.0f;
-        b.q[j][e] = (rq >= 0 && rq < n_t) ? vq : 0.0f;
-      } else {
-        b.p[j][e] = xc[rp * s_t];
-        if (NTILE == 2) b.q[j][e] = xq[rq * s_t];
-      }
+      const int64_t rp = row0 + 16 * j + e;
+      const int64_t cp = rp < 0 ? 0 : (rp >= n_t ? n_t - 1 : rp);
+      const float vp = xc[cp * s_t], vq = xq[cp * s_t];
+      b.p[j][e] = (rp >= 0 && rp < n_t) ? vp : 0.0f;
+      b.q[j][e] = (rp >= 0 && rp < n_t) ? vq : 0.0f;
     }
 }
 
 // 2 x 16 MFMAs of one 64-sample iteration (offset o0 = 64 it); out-of-block
 // samples (row offsets outside [lo, hi)) finite-masked when `mask`
-// NTILE == 2: acc0 / acc1 are tiles 0 / 1; NTILE == 1: two chains of tile 0
-// (even / odd steps), summed at the block end
-template <bool SWAP, int NTILE = 2>
 __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmIter &b, int o0, int q, bool mask,
                                         int lo, int hi, d4v &acc0, d4v &acc1) {
 #pragma unroll
@@ -3568,12 +3399,6 @@ __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmI
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float v0 = b.p[j][e], v1 = b.q[j][e];
-      if (SWAP) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
-        const auto s2 = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
-        v0 = __uint_as_float(s2[0]);
-        v1 = __uint_as_float(s2[1]);
-      }
       if (mask) {
         const int o = o0 + 16 * j + 4 * q + e;
         if (o < lo || o >= hi) {
@@ -3581,57 +3406,8 @@ __device__ __forceinline__ void tm_iter(const double *kt, int kstride, const TmI
           v1 = finite_or_zero(v1);
         }
       }
-      if (NTILE == 2) {
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v1, acc1, 0, 0, 0);
-      } else if (e & 1) {
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc1, 0, 0, 0);
-      } else {
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
-      }
-    }
-  }
-}
-
-// tm_iter on v_mfma_f64_4x4x4_4b (operand layout: tools/check_mfma4x4.hip): tile t's
-// functionals 4m + q accumulate in element m of acc_t (m < 3), i.e. acc_t
-// already holds (e_f[q], e_r0[q], p0) as block_done reads them
-template <bool SWAP>
-__device__ __forceinline__ void tm_iter4(const double *const (&kt)[3], int off, int kstride, const TmIter &b, int o0,
-                                         int q, bool mask, int lo, int hi, d4v &acc0, d4v &acc1) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    double a[3][4];
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const double2 b01 = *reinterpret_cast<const double2 *>(kt[m] + off + j * kstride);
-      const double2 b23 = *reinterpret_cast<const double2 *>(kt[m] + off + j * kstride + 2);
-      a[m][0] = b01.x;
-      a[m][1] = b01.y;
-      a[m][2] = b23.x;
-      a[m][3] = b23.y;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float v0 = b.p[j][e], v1 = b.q[j][e];
-      if (SWAP) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
-        const auto s2 = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
-        v0 = __uint_as_float(s2[0]);
-        v1 = __uint_as_float(s2[1]);
-      }
-      if (mask) {
-        const int o = o0 + 16 * j + 4 * q + e;
-        if (o < lo || o >= hi) {
-          v0 = finite_or_zero(v0);
-          v1 = finite_or_zero(v1);
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        acc0[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[m][e], (double)v0, acc0[m], 0, 0, 0);
-        acc1[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[m][e], (double)v1, acc1[m], 0, 0, 0);
-      }
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e], (double)v1, acc1, 0, 0, 0);
     }
   }
 }
@@ -3653,22 +3429,20 @@ __device__ __forceinline__ void tm_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t 
     }
 }
 
-// MODE 0: production.  Diagnostics (timing only, results invalid;
-// LFD_TM_MODE, X2 + BUF instantiations): 3 = loads only (a VALU sum of the
-// samples, no MFMA, no run epilogue, no stores) = the floor of this access
-// shape; 4 = loads + MFMAs, the run epilogue reduced to nothing.
 // SEPI: streaming run epilogue (run_block_stream): the LDS holds only the
 // taps and RUN_CST_S constants; no backward sweep at run ends, during which
-// a wave issued no loads.  Registers allow 2 waves per SIMD (8 per CU: the
-// occupancy at which this access shape streams fastest,
-// profiles/r03_ubench_tm.txt).
-// TMW (diag A/B): minimum waves per SIMD for the register allocation (0: 4
-// for one tile, 2 with SEPI, else 1)
-template <int TM_PF, int NT, bool SWAP, int NTILE = 2, bool X2 = false, bool M4 = false, bool BUF = false,
-          int MODE = 0, bool SEPI = false, int TMW = 0>
-__global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1))) void k_block_runs_mfma_tm(
+// a wave issued no loads.  MINW: waves per SIMD the registers are capped for
+// (production: 256-thread groups, 2 per SIMD: 8 waves per CU, the occupancy
+// at which this access shape streams fastest, profiles/r03_ubench_tm.txt).
+// MODE 0: production.  Diagnostics (timing only, results invalid;
+// LFD_TM_MODE): 3 = loads only (a VALU sum of the samples, no MFMA, no run
+// epilogue, no stores) = the floor of this access shape; 4 = loads + MFMAs,
+// the run epilogue reduced to nothing.
+template <int TM_PF, int NT, bool X2, bool BUF, bool SEPI, int MINW, int MODE = 0>
+__global__ __launch_bounds__(NT, MINW) void k_block_runs_mfma_tm(
     const float *__restrict__ x, int64_t s_t, int64_t n_t, BlockGeom g, const double *__restrict__ taps,
     TapGeom tg, RunGeom rg, double *__restrict__ Y0, double *__restrict__ AG) {
+  static_assert(!BUF || X2, "buffer loads read channel pairs");
   extern __shared__ double Ks[];
   const int tab = tg.Lp * tg.nc;  // one table: row shift 0
   for (int i = 2 * threadIdx.x; i < tab; i += 2 * blockDim.x)
@@ -3681,10 +3455,9 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  double *wbase = Ks + tab + RUN_CST + wave * NTILE * RUN_WB;  // tile t's buffer: wbase + t * RUN_WB
+  double *wbase = Ks + tab + RUN_CST + wave * 2 * RUN_WB;  // tile t's buffer: wbase + t * RUN_WB
   (void)wbase;
-  constexpr int CW = 16 * NTILE;  // channels per wave
-  const int64_t n_c32 = (g.n_ch + CW - 1) / CW;
+  const int64_t n_c32 = (g.n_ch + 31) / 32;
   const int64_t unit = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   if (unit >= n_c32 * rg.n_groups) return;
   const int64_t c32 = unit % n_c32, grp = unit / n_c32;
@@ -3702,29 +3475,24 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
   const int64_t k0 = run_ks_of(r);
   const int64_t k1 = run_ks_of(r_end - 1) + run_len_of(r_end - 1);
   const int col = lane & 15, q = lane >> 4;
-  const bool tile1 = NTILE == 2 && c32 * 32 + 16 < g.n_ch;  // tile 1 holds a real channel (else its stores would
-                                               // leave the 16-channel padding of Y0 / AG)
-  // this lane's load channel and row offset
-  // (X2: channel pairs 2 col, 2 col + 1; n_ch is even, a pair past n_ch
-  // reads the last pair)
-  const int lc = SWAP ? (lane & 31) : (X2 ? 2 * col : col);
-  const int64_t lch = X2 ? min(c32 * CW + lc, g.n_ch - 2) : min(c32 * CW + lc, g.n_ch - 1);
+  const bool tile1 = c32 * 32 + 16 < g.n_ch;  // tile 1 holds a real channel (else its stores would
+                                              // leave the 16-channel padding of Y0 / AG)
+  // this lane's load channel and row offset (X2: channel pairs 2 col,
+  // 2 col + 1; n_ch is even, a pair past n_ch reads the last pair; else
+  // channels past n_ch, in a ragged last group, read channel n_ch - 1)
+  const int lc = X2 ? 2 * col : col;
+  const int64_t lch = X2 ? min(c32 * 32 + lc, g.n_ch - 2) : min(c32 * 32 + lc, g.n_ch - 1);
   const float *xc = x + lch;
-  const int rsel = SWAP ? 4 * (lane >> 5) : 4 * q;
-  // (channels past n_ch, in a ragged last group, read channel n_ch - 1)
-  // Q loads: the same lane channel (SWAP) or tile 1's (16 + col), clamped
-  // like P so no load leaves the array
-  const int64_t lchq = SWAP ? lch : (X2 ? lch + 1 : min(c32 * CW + 16 + col, g.n_ch - 1));
+  const int rsel = 4 * q;
+  // Q loads: tile 1's channel (16 + col), clamped like P so no load leaves the array
+  const int64_t lchq = X2 ? lch + 1 : min(c32 * 32 + 16 + col, g.n_ch - 1);
   const float *xq = x + lchq;
-  const int64_t c0 = uniform64(c32 * CW);  // interior loads: uniform row base + lane offset
-  const uint32_t offp = (uint32_t)(4 * (lch - c32 * CW + rsel * s_t)),  // bytes
-      offq = (uint32_t)(4 * (lchq - c32 * CW + rsel * s_t));
+  const int64_t c0 = uniform64(c32 * 32);  // interior loads: uniform row base + lane offset
+  const uint32_t offp = (uint32_t)(4 * (lch - c32 * 32 + rsel * s_t)),  // bytes
+      offq = (uint32_t)(4 * (lchq - c32 * 32 + rsel * s_t));
 
   const bool colv = col < tg.nc;
   const double *kl = Ks + (q * tg.nc + (colv ? col : tg.nc - 1)) * 4;
-  const double *kl4[3];  // (M4) tap columns of functionals 4m + (lane & 3)
-#pragma unroll
-  for (int m = 0; m < 3; ++m) kl4[m] = Ks + (q * tg.nc + min(4 * m + (lane & 3), tg.nc - 1)) * 4;
   const int nit = tg.Lp / 64;
   const int kstride = 16 * tg.nc;
   const int64_t s0 = g.base - tg.J;
@@ -3760,7 +3528,7 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
       if (!X2 && t == 1 && !tile1) break;
       const double *wb = wbase + t * RUN_WB;
       // tile t, lane col: channel 16 (2 c32 + t) + col, or (X2) 32 c32 + 2 col + t
-      const int64_t chn = X2 ? c32 * 32 + 2 * col + t : (NTILE * c32 + t) * 16 + col;
+      const int64_t chn = X2 ? c32 * 32 + 2 * col + t : (2 * c32 + t) * 16 + col;
       const int64_t cg = chn >> 4;
       const int cc = (int)(chn & 15);
       const bool st_ok = !X2 || cg * 16 < g.n_ch;  // (X2) inside the 16-channel padding
@@ -3802,7 +3570,7 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (!X2 && t == 1 && !tile1) break;
-      const int64_t chn = X2 ? c32 * 32 + 2 * col + t : (NTILE * c32 + t) * 16 + col;
+      const int64_t chn = X2 ? c32 * 32 + 2 * col + t : (2 * c32 + t) * 16 + col;
       const int64_t cg = chn >> 4;
       const int cc = (int)(chn & 15);
       if (X2 && cg * 16 >= g.n_ch) continue;
@@ -3824,20 +3592,14 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
     if constexpr (SEPI) {
       const int p = (int)(k - rks);
       const double a0[3] = {acc0[0], acc0[1], acc0[2]};
+      const double a1[3] = {acc1[0], acc1[1], acc1[2]};
       run_block_stream(cst, q, p, a0, ra[0]);
-      if (NTILE == 2) {
-        const double a1[3] = {acc1[0], acc1[1], acc1[2]};
-        run_block_stream(cst, q, p, a1, ra[1]);
-      }
+      run_block_stream(cst, q, p, a1, ra[1]);
       if (p + 1 == rlen) run_end_stream();
       return;
     }
-    if (NTILE == 2) {
-      block_done(acc0, 0, k);
-      block_done(acc1, 1, k);
-    } else {
-      block_done(acc0 + acc1, 0, k);
-    }
+    block_done(acc0, 0, k);
+    block_done(acc1, 1, k);
     if (k - rks + 1 == rlen) run_done();
   };
   auto guarded_block = [&](int64_t k) {
@@ -3845,12 +3607,8 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     for (int it = 0; it < nit; ++it) {
       TmIter b;
-      tm_load<true, SWAP, NTILE>(xc, xq, s_t, n_t, s + 64 * it + rsel, b);
-      if (M4)
-        tm_iter4<SWAP>(kl4, (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0, acc1);
-      else
-        tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0,
-                             acc1);
+      tm_load_guarded(xc, xq, s_t, n_t, s + 64 * it + rsel, b);
+      tm_iter(kl + (4 * it) * kstride, kstride, b, 64 * it, q, it == 0 || it == nit - 1, lo, hi, acc0, acc1);
     }
     if (MODE == 0) finish_block(acc0, acc1, k);  // (diagnostics: no LDS run buffers)
   };
@@ -3887,7 +3645,7 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(rowp), (short)0, nrec, 0x00020000);
         tm_load_buf(rs, offp, soff, b);
       } else {
-        tm_load_u<SWAP, NTILE, X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, b);
+        tm_load_u<X2>(x, c0, s_t, uniform64(sp + 64 * itp), offp, offq, b);
       }
     };
 #pragma unroll
@@ -3912,10 +3670,8 @@ __global__ __launch_bounds__(NT, TMW > 0 ? TMW : (NTILE == 1 ? 4 : (SEPI ? 2 : 1
           for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc0[e] += (double)(buf[u].p[j][e] + buf[u].q[j][e]);
-        } else if (M4) {
-          tm_iter4<SWAP>(kl4, (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
         } else {
-          tm_iter<SWAP, NTILE>(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
+          tm_iter(kl + (4 * it) * kstride, kstride, buf[u], 64 * it, q, mask, lo, hi, acc0, acc1);
         }
         if (++it == nit) {
           if (MODE == 0) {
@@ -3960,116 +3716,9 @@ hipError_t block_functionals_ns(const float *x, int64_t s_ch, int64_t s_t, const
 
 }  // namespace
 
-#ifdef LFD_DIAG
-hipError_t launch_block_runs_mfma_tm_ab(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
-                                     const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
-                                     double *AG, hipStream_t st) {
-  if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || tg.nvar != 1 || tg.v0 != 0 || rg.n_groups < 1)
-    return hipErrorInvalidValue;
-  const size_t tab = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST);
-  // measured on cfg3 stored time-major (tools/tm_bench.py): no-swap loads at
-  // 512 threads / depth 2 14.28 ms, 768 / 1 14.46; permlane loads 14.74-14.89
-  int nt = 512, pf = 2;
-  if (const char *v = knob("LFD_TM_NT")) nt = std::atoi(v);
-  if (const char *v = knob("LFD_TM_PF")) pf = std::atoi(v);
-  int ntile = 2;
-  if (const char *v = knob("LFD_TM_NTILE")) ntile = std::atoi(v) == 1 ? 1 : 2;
-  size_t lds = tab + sizeof(double) * (size_t)(nt / 64) * ntile * RUN_WB;
-  if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  auto go = [&](auto kern, int NT) -> hipError_t {
-    static bool attr[2] = {false, false};  // per instantiation below
-    (void)attr;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       TAP_LDS_MAX);
-    if (e != hipSuccess) return e;
-    const int W = NT / 64;
-    const int64_t units = ((g.n_ch + 16 * ntile - 1) / (16 * ntile)) * rg.n_groups;
-    kern<<<(unsigned)((units + W - 1) / W), NT, lds, st>>>(x, s_t, n_t, g, taps, tg, rg, Y0, AG);
-    return hipGetLastError();
-  };
-  bool swap = false;
-  if (const char *v = knob("LFD_TM_SWAP")) swap = std::atoi(v) != 0;
-  // channel-pair loads: need 8-B aligned pairs (even n_ch and row stride)
-  const bool x2_ok = g.n_ch % 2 == 0 && s_t % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
-  bool x2 = x2_ok && !option(LFD_OPT_TM_NO_PAIRS);
-  if (const char *v = knob("LFD_TM_X2")) x2 = x2_ok && std::atoi(v) != 0;
-  bool m4 = false;
-  if (const char *v = knob("LFD_TM_M4")) m4 = std::atoi(v) != 0;
-  if (m4 && x2 && !swap && ntile == 2 && (knob("LFD_TM_PF") || knob("LFD_TM_NT"))) {
-    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, true>, 512);
-    if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true>, 512);
-    return hipErrorInvalidValue;
-  }
-  // buffer loads at prefetch depth 1: 14.01 vs 14.18 ms on cfg3 stored
-  // time-major (in-process A/B, tools/ab_plan.py --tm; bit-identical)
-  bool buf = !knob("LFD_TM_PF") && !knob("LFD_TM_NT");
-  if (const char *v = knob("LFD_TM_BUF")) buf = std::atoi(v) != 0;
-  if (buf && x2 && !swap && ntile == 2 && s_t < (int64_t)1 << 22) {
-    const int pfb = knob("LFD_TM_PF") ? pf : 1;
-    int mode = 0;
-    if (const char *v = knob("LFD_TM_MODE")) mode = std::atoi(v);
-    // (LFD_TM_DIAG_LDS=1: the diagnostics allocate only the tap table, so
-    // their occupancy is set by registers, not by the run buffers)
-    if (mode >= 3 && knob_flag("LFD_TM_DIAG_LDS")) lds = tab;
-    if (mode == 3 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 3>, 512);
-    if (mode == 3) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 3>, 512);
-    if (mode == 4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 4>, 512);
-    // streaming run epilogue: taps + constants only in LDS: 13.85 vs 14.35 ms
-    // on cfg3 stored time-major (in-process A/B on one allocation,
-    // profiles/r03_ab_tm_sepi.txt; A/B knob LFD_TM_SEPI=0)
-    bool sepi = true;
-    if (const char *v = knob("LFD_TM_SEPI")) sepi = std::atoi(v) != 0;
-    if (sepi && nt == 512) {
-      lds = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
-      // (LFD_TM_M4=1: v_mfma_f64_4x4x4 steps, a third less matrix-core issue time)
-      if (m4) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, true, true, 0, true>, 512);
-      // production: 256-thread groups, registers for 2 waves per SIMD;
-      // LFD_TM_W=512: the 512-thread groups of round 3; =3: 256 threads,
-      // registers for 3 waves per SIMD (spills); =21: 128-thread groups
-      // (profiles/r04q_ab_tm_w.txt)
-      if (const char *wv = knob("LFD_TM_W")) {
-        if (std::atoi(wv) == 3) return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 3>, 256);
-        if (std::atoi(wv) == 21) return go(&k_block_runs_mfma_tm<1, 128, false, 2, true, false, true, 0, true, 2>, 128);
-        if (std::atoi(wv) == 22) return go(&k_block_runs_mfma_tm<2, 256, false, 2, true, false, true, 0, true, 2>, 256);
-        if (std::atoi(wv) == 512) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
-      }
-      if (pfb == 1) return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 2>, 256);
-      if (pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true, 0, true>, 512);
-      return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true, 0, true>, 512);
-    }
-    if (nt == 512 && pfb == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true, false, true>, 512);
-    if (nt == 512 && pfb == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true, false, true>, 512);
-    return hipErrorInvalidValue;
-  }
-  if (x2 && !swap && ntile == 2) {
-    if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, false, 2, true>, 768);
-    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, 512);
-    if (nt == 512 && pf == 3) return go(&k_block_runs_mfma_tm<3, 512, false, 2, true>, 512);
-    if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, false, 2, true>, 512);
-    return hipErrorInvalidValue;
-  }
-  if (ntile == 1) {  // one 16-channel tile per wave: half-line loads, 16 waves/CU
-    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false, 1>, 512);
-    return hipErrorInvalidValue;
-  }
-  if (swap) {
-    if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, true>, 768);
-    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, true>, 512);
-    if (nt == 512 && pf == 1) return go(&k_block_runs_mfma_tm<1, 512, true>, 512);
-  } else {
-    if (nt == 768 && pf == 1) return go(&k_block_runs_mfma_tm<1, 768, false>, 768);
-    if (nt == 512 && pf == 2) return go(&k_block_runs_mfma_tm<2, 512, false>, 512);
-  }
-  return hipErrorInvalidValue;  // no instantiation for this A/B knob combination
-}
-#endif  // LFD_DIAG
-
 hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, const BlockGeom &g,
                                      const double *taps, const TapGeom &tg, const RunGeom &rg, double *Y0,
                                      double *AG, hipStream_t st) {
-#ifdef LFD_DIAG
-  return launch_block_runs_mfma_tm_ab(x, s_t, n_t, g, taps, tg, rg, Y0, AG, st);
-#else
   if (tg.nc != 2 * RUN_N + 1 || tg.Lp % 64 != 0 || tg.nvar != 1 || tg.v0 != 0 || rg.n_groups < 1)
     return hipErrorInvalidValue;
   const size_t tab = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST);
@@ -4086,19 +3735,26 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   // channel-pair loads need 8-B aligned pairs (even n_ch and row stride)
   const bool x2 = g.n_ch % 2 == 0 && s_t % 2 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
                   !option(LFD_OPT_TM_NO_PAIRS);
-  if (x2 && s_t < (int64_t)1 << 22)
+  if (x2 && s_t < (int64_t)1 << 22) {
     // buffer loads at prefetch depth 1 (14.01 vs 14.18 ms) with the streaming
     // run epilogue, taps + constants only in LDS (13.85 vs 14.35 ms) on cfg3
     // stored time-major (profiles/r03_ab_tm_sepi.txt); 256-thread groups (4
     // per CU, registers for 2 waves per SIMD as before): 13.06 vs 13.50 ms
     // median against 512-thread groups, bit-identical; 128-thread groups 15.03
     // (profiles/r04q_ab_tm_w.txt)
-    return go(&k_block_runs_mfma_tm<1, 256, false, 2, true, false, true, 0, true, 2>,
-              sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S), 256);
-  const size_t lds = tab + sizeof(double) * 8 * 2 * RUN_WB;  // + 8 waves x 2 tiles of run buffers
-  if (x2) return go(&k_block_runs_mfma_tm<2, 512, false, 2, true>, lds, 512);
-  return go(&k_block_runs_mfma_tm<2, 512, false>, lds, 512);
+    const size_t lds_s = sizeof(double) * ((size_t)tg.Lp * tg.nc + RUN_CST_S);
+#ifdef LFD_DIAG
+    // timing-only modes (results invalid): LFD_TM_MODE=3 loads only, =4 no run epilogue
+    if (const char *v = knob("LFD_TM_MODE")) {
+      if (std::atoi(v) == 3) return go(&k_block_runs_mfma_tm<1, 256, true, true, true, 2, 3>, lds_s, 256);
+      if (std::atoi(v) == 4) return go(&k_block_runs_mfma_tm<1, 256, true, true, true, 2, 4>, lds_s, 256);
+    }
 #endif
+    return go(&k_block_runs_mfma_tm<1, 256, true, true, true, 2>, lds_s, 256);
+  }
+  const size_t lds = tab + sizeof(double) * 8 * 2 * RUN_WB;  // + 8 waves x 2 tiles of run buffers
+  if (x2) return go(&k_block_runs_mfma_tm<2, 512, true, false, false, 1>, lds, 512);
+  return go(&k_block_runs_mfma_tm<2, 512, false, false, false, 1>, lds, 512);
 }
 
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
@@ -4129,7 +3785,6 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   if (!attr) {
     for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
 #ifdef LFD_DIAG
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<1, 0>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>),
                            reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6>),
@@ -4183,23 +3838,15 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
                                                                    n_runs, bpw)
 #ifdef LFD_DIAG
-  if (knob_flag("LFD_MF_M4S")) {
-    static bool attr_s = false;
-    if (!attr_s) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0, true>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
-      if (e != hipSuccess) return e;
-      attr_s = true;
-    }
-    k_block_functionals_mfma<2, 0, true><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, n_runs, bpw);
-  } else if (mode == 1)
+  // timing-only modes (results invalid, LFD_MF_MODE): 1 loads only, 3 no
+  // stores, 6 stores into an L2-resident window
+  (void)pf;
+  if (mode == 1)
     LFD_MF(2, 1);
   else if (mode == 3)
     LFD_MF(2, 3);
   else if (mode == 6)
     LFD_MF(2, 6);
-  else if (pf == 1)
-    LFD_MF(1, 0);
   else
     LFD_MF(2, 0);
 #else
@@ -5297,49 +4944,12 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
 #define LFD_FR(NS, OUT) \
   k_fullrate_wave<NS, OUT><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, s_t, n_ch, nb, fc, SF, ST, F, y, ys_ch, ys_t)
 #ifdef LFD_DIAG
-  static const bool fr_direct = knob_flag("LFD_FR_OUT_DIRECT");
-  static const int fr_lay = knob("LFD_FR_LAYOUT") ? std::atoi(knob("LFD_FR_LAYOUT")) : 1;
-  static const bool fr_m4 = knob_flag("LFD_FR_M4");
-  static const int fr_pre = knob("LFD_FR_PRE") ? std::atoi(knob("LFD_FR_PRE")) : -1;
+  // (LFD_FR_ORDER: the workgroup order A/B, 0 / 1 / 2 below)
   static const int fr_ord = knob("LFD_FR_ORDER") ? std::atoi(knob("LFD_FR_ORDER")) : 2;
 #else
   constexpr int fr_ord = 2;
 #endif
-#ifdef LFD_DIAG
-#define LFD_FR_PRE_AB(NS)                                                                                           \
-  if (out && mb && fr_pre == 1)                                                                                    \
-    k_fullrate_out_mb<NS, false, 1, false, 1><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
-                                                                            ys_ch, ys_t);                          \
-  else if (out && mb && fr_pre == 3)                                                                               \
-    k_fullrate_out_mb<NS, false, 1, false, 3><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
-                                                                            ys_ch, ys_t);                          \
-  else if (out && mb && fr_pre == 0)                                                                               \
-    k_fullrate_out_mb<NS, false, 1, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, \
-                                                                            ys_ch, ys_t);                          \
-  else
-#else
-#define LFD_FR_PRE_AB(NS)
-#endif
-#ifdef LFD_DIAG
-#define LFD_FR_LAY_AB(NS)                                                                                        \
-  if (out && mb && fr_m4)                                                                                        \
-    k_fullrate_out_mb<NS, false, 1, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y,  \
-                                                                         ys_ch, ys_t);                           \
-  else if (out && mb && fr_direct)                                                                               \
-    k_fullrate_out_mb<NS, true><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t); \
-  else if (out && mb && fr_lay == 0)                                                                             \
-    k_fullrate_out_mb<NS, false, 0><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch,  \
-                                                                   ys_t);                                        \
-  else if (out && mb && fr_lay == 2)                                                                             \
-    k_fullrate_out_mb<NS, false, 2><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch,  \
-                                                                   ys_t);                                        \
-  else
-#else
-#define LFD_FR_LAY_AB(NS)
-#endif
 #define LFD_FR2(NS)   \
-  LFD_FR_PRE_AB(NS) \
-  LFD_FR_LAY_AB(NS) \
   if (out && mb)      \
     k_fullrate_out_mb<NS><<<(unsigned)n_wg, 64, 0, st>>>(x, s_ch, n_ch, nb, n_mb, fc, SF, ST, y, ys_ch, ys_t, fr_ord); \
   else if (out)       \
@@ -5354,8 +4964,6 @@ hipError_t launch_fullrate_blocks(int n_sec, bool out, const float *x, int64_t s
     default: return hipErrorInvalidValue;
   }
 #undef LFD_FR2
-#undef LFD_FR_LAY_AB
-#undef LFD_FR_PRE_AB
 #undef LFD_FR
 #ifdef LFD_DIAG
   if (out && mb && knob_flag("LFD_FR_TIMES")) {
@@ -5554,25 +5162,6 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
         if (e != hipSuccess) return e;
         attr = true;
       }
-#ifdef LFD_DIAG
-      // (diag A/B: tiles in flight per wave)
-      if (const char *v = knob("LFD_ROLL_SEG_PF")) {
-        const int pf = std::atoi(v);
-        if (pf == 1 || pf == 3) {
-          const void *fn = pf == 1 ? reinterpret_cast<const void *>(&k_rolling_seg<1>)
-                                   : reinterpret_cast<const void *>(&k_rolling_seg<3>);
-          hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-          if (e != hipSuccess) return e;
-          if (pf == 1)
-            k_rolling_seg<1><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y,
-                                                                 ys_ch, ys_t, (int)seg_out, (int)ring - 1, ebatch);
-          else
-            k_rolling_seg<3><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y,
-                                                                 ys_ch, ys_t, (int)seg_out, (int)ring - 1, ebatch);
-          return hipGetLastError();
-        }
-      }
-#endif
       int sdiag = 0;
       if (const char *v = knob("LFD_ROLL_SEG_DIAG")) sdiag = std::atoi(v);
       k_rolling_seg<2><<<(unsigned)blocks, 256, lds, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, (int)g, y, ys_ch,
@@ -5601,21 +5190,17 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     if (blocks > cap) blocks = cap;
     const bool vec = (reinterpret_cast<uintptr_t>(x) & 3) == 0;  // (any row stride: f4u loads)
     const bool vec_out = vec && ys_t == 1 && ys_ch % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-    // stage 2 (lanes load their 8 positions directly, outputs leave through
-    // LDS as coalesced float4 stores) measured best on cfg2 at S = 1: 4.77 ms
-    // vs 5.93 (0), 5.99 (1), 5.54 (3)
-    int stage = 2;
-    if (const char *v = knob("LFD_ROLL_STAGE")) stage = std::atoi(v) & 3;
-    int npf = 1, minw = 3;
-    if (const char *v = knob("LFD_ROLL_PF")) npf = std::atoi(v);
-    if (const char *v = knob("LFD_ROLL_MINW")) minw = std::atoi(v);
+    // lanes load their 8 positions directly, outputs leave through LDS as
+    // coalesced float4 stores (cfg2 at S = 1: 4.77 ms vs 5.93 with the loads
+    // staged through LDS too; deeper prefetch and 4 waves per SIMD measured
+    // slower: profiles/r02_ab_roll_*.txt, r05_roll_scan_ab.txt)
     // the per-step wave scan on DPP lane moves (A/B knob LFD_ROLL_DPP=0: shuffles)
     bool dpp = true;
     if (const char *v = knob("LFD_ROLL_DPP")) dpp = std::atoi(v) != 0;
     // LDS ring for x[t - W] (vector rows, W + 512 <= 4096): A/B knob LFD_ROLL_RING
     int ring = 0;
     while (ring < W + RS_P) ring = ring ? 2 * ring : 1024;
-    bool use_ring = vec && ring <= 4096 && stage == 2 && npf == 1 && minw == 3;
+    bool use_ring = vec && ring <= 4096;
     if (const char *v = knob("LFD_ROLL_RING")) use_ring = use_ring && std::atoi(v) != 0;
     if (use_ring) {
       static bool attr = false;
@@ -5634,24 +5219,6 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                                              ys_t, (int)seg_out, V && vec_out, 0, dpp)
     if (!vec)
       LFD_ROLL(false, 0, 1);
-#ifdef LFD_DIAG
-    else if (stage == 2 && npf == 1 && minw == 4)
-      k_rolling_scan_tc<true, 2, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
-                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0, dpp);
-    else if (stage == 2 && npf == 2 && minw == 4)
-      k_rolling_scan_tc<true, 2, 2, 4><<<(unsigned)blocks, 256, 0, st>>>(x, n_ch, (int)n_t, s_ch, (int)W, (int)S, y,
-                                                                      ys_ch, ys_t, (int)seg_out, vec_out, 0, dpp);
-    else if (stage == 2 && npf == 2)
-      LFD_ROLL(true, 2, 2);
-    else if (stage == 2 && npf == 3)
-      LFD_ROLL(true, 2, 3);
-    else if (stage == 0)
-      LFD_ROLL(true, 0, 1);
-    else if (stage == 1)
-      LFD_ROLL(true, 1, 1);
-    else if (stage == 3)
-      LFD_ROLL(true, 3, 1);
-#endif
     else
       LFD_ROLL(true, 2, 1);
 #undef LFD_ROLL
@@ -5783,20 +5350,20 @@ constexpr int fdm_rl() {
   const int a = FDM_NN + ((4 - FDM_NN) % 32 + 32) % 32, b = FDM_NN + ((28 - FDM_NN) % 32 + 32) % 32;
   return a < b ? a : b;
 }
-// DB: two X buffers (the next tile's staging lands in the other one, one
-// barrier per tile, 1 workgroup per CU) instead of one (two barriers, 3 per CU)
-template <int Q, bool DB = false>
+// (one X buffer, two barriers per tile, 3 workgroups per CU; a double-buffered
+// X at 1 workgroup per CU measured slower, profiles/r03_ab_fir.txt)
+template <int Q>
 constexpr size_t fdm_lds_bytes() {
-  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32) * (DB ? 2 : 1);
+  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32);
 }
-// SB: a scheduling barrier after SB of a phase's DM Toeplitz steps
-// (production SB = DM: at the phase's end).  Without it the compiler hoisted
+// A scheduling barrier closes every phase: without it the compiler hoisted
 // the next phase's f32 -> f64 conversions — and so the wait for that phase's
 // LDS reads, issued at this phase's start — in between this phase's first
-// MFMAs: 2,000 x 600,000 at q = 10 1.648 -> 1.565 ms (SB = 0 / 3 / 4 / 5 / 6:
-// 1.648 / 1.653 / 1.623 / 1.593 / 1.565, profiles/r05_fir_sched.txt)
-template <int Q, bool DB = false, int SB = 0>
-__global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
+// MFMAs: 2,000 x 600,000 at q = 10 1.648 -> 1.565 ms (barrier after 0 / 3 / 4
+// / 5 / 6 of the 6 Toeplitz steps: 1.648 / 1.653 / 1.623 / 1.593 / 1.565,
+// profiles/r05_fir_sched.txt)
+template <int Q>
+__global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
                                                           int64_t s_ch, const double *__restrict__ h, int n_taps,
                                                           int64_t delay, int64_t n_out, int64_t tiles_o, int strip,
                                                           double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
@@ -5816,8 +5383,7 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
   const int64_t nb = (int64_t)gridDim.x;
   // XCD-aware order: consecutive strips of one channel group on one XCD
   // (their input halos meet in that XCD's L2)
-  // (diag bit 128: dispatch order, no XCD remap)
-  if ((nb & 7) == 0 && !(diag & 128)) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
+  if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
   const int64_t cg = bid / n_strips;
   const int64_t t_begin = (bid % n_strips) * strip;
   const int64_t t_end = t_begin + strip < tiles_o ? t_begin + strip : tiles_o;
@@ -5856,15 +5422,13 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
       }
     }
   };
-  auto commit = [&](int cpar = 0) {
+  auto commit = [&]() {
     int ln = lane;
     asm volatile("" : "+v"(ln));  // recomputed per tile, not hoisted into registers
     const int n_l = ln / Q, r_l = ln - n_l * Q;
-    float *a0 = row_ld + cpar * (4 * JB) + (Q - 1 - r_l) * RL + n_l;
+    float *a0 = row_ld + (Q - 1 - r_l) * RL + n_l;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      constexpr int dummy = 0;
-      (void)dummy;
       const int c = (64 * r) % Q, f = (64 * r) / Q;
       const bool carry = r_l + c >= Q;
       float *dst = a0 + (f - c * RL) + (carry ? Q * RL + 1 : 0);
@@ -5882,27 +5446,14 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
   const float *x21 = Xs + jl * JB + offj(jl) + 64 * w + 4 * ((lane >> 2) & 3);
   // diag (LFD_FIR_DIAG, timing breakdowns only): 1 = staging without the
   // MFMA phase loop, 2 = MFMA phase loop without the staging
-  constexpr int XB = 4 * JB;  // floats per X buffer
   if ((diag & 3) != 2) issue(t_begin * NO);
-  if (DB) {
-    if ((diag & 3) != 2) commit();
-  }
-  if (diag & 16) {  // (A/B: stagger the workgroups sharing a CU by a third of a tile)
-    const int sk = (int)(blockIdx.x % 3);
-    for (int i = 0; i < sk * (1 + ((diag >> 5) & 3)); ++i) __builtin_amdgcn_s_sleep(127);
-  }
   for (int64_t tt = t_begin; tt < t_end; ++tt) {
-    const int par = DB ? (int)((tt - t_begin) & 1) : 0;
-    if (!DB) {
-      __syncthreads();  // the previous tile's reads of X are done
-      if ((diag & 3) != 2) commit();
-    }
+    __syncthreads();  // the previous tile's reads of X are done
+    if ((diag & 3) != 2) commit();
     __syncthreads();
-    // (diag bit 4: the next tile's loads issued half-way through the phases)
+    // the next tile's input loads while this one computes
     const bool pf_next = tt + 1 < t_end && (diag & 3) != 2;
-    if (pf_next && !(diag & 4)) issue((tt + 1) * NO);
-    const float *xbc = xb + par * XB;
-    if (diag & 8) __builtin_amdgcn_s_setprio(2);
+    if (pf_next) issue((tt + 1) * NO);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     if ((diag & 3) != 1) {
       // phase v: acc[t] += sum_d A_{v,d} B(index offset 4 (4t + DM - 1 - d));
@@ -5913,7 +5464,7 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
 #pragma unroll
       for (int d = 0; d < DM; ++d) an[d] = At[d * 16 + lane_a];
 #pragma unroll
-      for (int si = 0; si < NB; ++si) bn[si] = xbc[4 * si];
+      for (int si = 0; si < NB; ++si) bn[si] = xb[4 * si];
 #pragma unroll
       for (int v = 0; v < Q; ++v) {
         double ac[DM], bd[NB];
@@ -5921,16 +5472,11 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
         for (int d = 0; d < DM; ++d) ac[d] = an[d];
 #pragma unroll
         for (int si = 0; si < NB; ++si) bd[si] = (double)bn[si];
-        if (diag & 64) {  // (A/B: every conversion issued before the phase's first MFMA)
-#pragma unroll
-          for (int si = 0; si < NB; ++si) asm volatile("" : "+v"(bd[si]));
-        }
-        if (v == Q / 2 && pf_next && (diag & 4)) issue((tt + 1) * NO);
         if (v + 1 < Q) {
 #pragma unroll
           for (int d = 0; d < DM; ++d) an[d] = At[((v + 1) * DM + d) * 16 + lane_a];
 #pragma unroll
-          for (int si = 0; si < NB; ++si) bn[si] = xbc[(v + 1) * RL + 4 * si];
+          for (int si = 0; si < NB; ++si) bn[si] = xb[(v + 1) * RL + 4 * si];
         }
         // the four tiles' accumulators alternate: dependent MFMAs sit 4 apart
 #pragma unroll
@@ -5938,17 +5484,16 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(ac[d], bd[4 * t + DM - 1 - d], acc[t], 0, 0, 0);
-          if (SB > 0 && d == DM - SB) __builtin_amdgcn_sched_barrier(0);
         }
+        __builtin_amdgcn_sched_barrier(0);  // (the phase's end: see above)
       }
     }
-    if (diag & 8) __builtin_amdgcn_s_setprio(0);
     const int64_t O = tt * NO;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int64_t o = O + 64 * w + 16 * t + 4 * bo + io;
       if (ch >= n_ch || o >= n_out) continue;
-      double val = fma(h21, (double)x21[par * XB + 16 * t], acc[t]);
+      double val = fma(h21, (double)x21[16 * t], acc[t]);
       if (!isfinite(val)) {
         // direct sum (rare: a non-finite sample within reach of this output)
         const float *xr = x + ch * s_ch;
@@ -5961,7 +5506,6 @@ __global__ __launch_bounds__(256, DB ? 1 : 3) void k_fir_decimate_mfma(const flo
       }
       y[ch * ys_ch + o * ys_t] = val;
     }
-    if (DB && pf_next) commit(par ^ 1);  // next tile into the other buffer
   }
 }
 
@@ -5979,53 +5523,24 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     if (const char *sv = knob("LFD_FIR_STRIP")) strip = std::max(1, std::atoi(sv));
     if (strip > tiles_o) strip = (int)tiles_o;
     const int64_t grid = (n_ch + 3) / 4 * ((tiles_o + strip - 1) / strip);
-    int diag = 0;
+    int diag = 0;  // (diag build: LFD_FIR_DIAG timing breakdowns)
     if (const char *dv = knob("LFD_FIR_DIAG")) diag = std::atoi(dv);
-    const bool db = knob_flag("LFD_FIR_DB");  // double-buffered staging (measured, not kept)
     bool launched = false;
     hipError_t e = hipSuccess;
-#define LFD_FDM1(QV, DBV, SBV)                                                                               \
-  {                                                                                                          \
+#define LFD_FDM(QV)                                                                                          \
+  case QV: {                                                                                                 \
     static bool attr = false;                                                                                \
     if (!attr) {                                                                                             \
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV, DBV, SBV>),            \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV, DBV>());    \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV>());         \
       if (e != hipSuccess) return e;                                                                         \
       attr = true;                                                                                           \
     }                                                                                                        \
-    k_fir_decimate_mfma<QV, DBV, SBV><<<(unsigned)grid, 256, fdm_lds_bytes<QV, DBV>(), st>>>(               \
+    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdm_lds_bytes<QV>(), st>>>(                              \
         x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, diag);                  \
+    launched = true;                                                                                         \
+    break;                                                                                                   \
   }
-#ifdef LFD_DIAG
-    // LFD_FIR_SB (q = 10): the phase barrier after 0 (none: the compiler
-    // hoists the next phase's conversions into the phase's first MFMAs), 3 or
-    // 4 of the 6 Toeplitz steps (production: 6)
-    int sb = FDM_DM;
-    if (const char *v = knob("LFD_FIR_SB")) sb = std::atoi(v);
-#define LFD_FDM(QV)                          \
-  case QV: {                                 \
-    if (QV == 10 && sb == 0)                 \
-      LFD_FDM1(10, false, 0)                 \
-    else if (QV == 10 && sb == 3)            \
-      LFD_FDM1(10, false, 3)                 \
-    else if (QV == 10 && sb == 4)            \
-      LFD_FDM1(10, false, 4)                 \
-    else if (db)                             \
-      LFD_FDM1(QV, true, FDM_DM)             \
-    else                                     \
-      LFD_FDM1(QV, false, FDM_DM)            \
-    launched = true;                         \
-    break;                                   \
-  }
-#else
-#define LFD_FDM(QV)          \
-  case QV: {                 \
-    (void)db;                \
-    LFD_FDM1(QV, false, FDM_DM) \
-    launched = true;         \
-    break;                   \
-  }
-#endif
     if (grid <= (int64_t)INT32_MAX) {
       switch (q) {
         LFD_FDM(4)
@@ -6037,7 +5552,6 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
       }
     }
 #undef LFD_FDM
-#undef LFD_FDM1
     if (launched) {
       if (kernel_used) *kernel_used = 1;
       return hipGetLastError();

@@ -7,6 +7,14 @@
 # In-process A/Bs compare knobs on ONE input allocation (tools/ab_plan.py),
 # because K1's speed depends on the physical placement of a fresh 72 GB
 # tensor, and NaN-fill the output before every compared execute.
+# Round 5 deleted the kernel variants those records rejected (K1 4x4x4 /
+# buffer-load / streaming-epilogue / persistent / band orders; time-major
+# swap / one-tile / 4x4x4 / 768-thread / depth-3; full-rate direct stores,
+# 34-float layout, 4x4x4, early-KAZ; FIR double buffer; rolling staged loads,
+# depth 2-3, 4 waves per SIMD; functionals 4x4x4 and depth 1): their knobs in
+# the recipes below are now no-ops and the records in profiles/ are the
+# history.  The timing-only modes (LFD_RUN_MODE, LFD_TM_MODE, LFD_MF_MODE,
+# LFD_FIR_DIAG 1 / 2, LFD_SCAN_DIAG, LFD_FU_*, LFD_FR_TIMES) remain.
 set -o pipefail
 mkdir -p gpurun_out
 export LFDAS_LIB="$PWD/low-freq-real-time_amd/lfdas/liblfdas_diag.so"
