@@ -1,8 +1,7 @@
-# round-5: GPU suite after removing the rejected kernel variants; FIR / full-rate / tm timings
+# round-5: K1 timing modes on cfg3 (what a producer/consumer split could win)
 set -o pipefail
-O=gpurun_out/r05c
+O=gpurun_out/r05k1
 mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
-echo "pytest exit $?"; tail -3 $O/pytest_gpu.log
-timeout -k 10 300 python tools/fir_ab.py 10 "" > $O/fir.txt 2>&1; grep "q=" $O/fir.txt
-timeout -k 10 300 python tools/fr_bench.py 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['ms'],3), {k.split(' ')[0]: round(v,3) for k,v in d['kernels_ms'].items()})"
+export LFDAS_LIB="$PWD/low-freq-real-time_amd/lfdas/liblfdas_diag.so"
+timeout -k 10 600 python tools/ab_plan.py --ch 10000 --reps 3 --steps 5 "" "LFD_RUN_MODE=4" "LFD_RUN_MODE=1" > $O/modes.txt 2>&1
+echo "exit $?"; grep -E "K1|bit" $O/modes.txt
