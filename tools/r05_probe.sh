@@ -1,7 +1,10 @@
-# round-5: K1 timing modes on cfg3 (what a producer/consumer split could win)
+# round-5: non-temporal output stores A/B (FIR, rolling S = 1, full-rate)
 set -o pipefail
-O=gpurun_out/r05k1
+O=gpurun_out/r05nt
 mkdir -p $O
 export LFDAS_LIB="$PWD/low-freq-real-time_amd/lfdas/liblfdas_diag.so"
-timeout -k 10 600 python tools/ab_plan.py --ch 10000 --reps 3 --steps 5 "" "LFD_RUN_MODE=4" "LFD_RUN_MODE=1" > $O/modes.txt 2>&1
-echo "exit $?"; grep -E "K1|bit" $O/modes.txt
+timeout -k 10 300 python tools/fir_ab.py 10 "" "LFD_NT_STORES=1" "" "LFD_NT_STORES=1" > $O/fir.txt 2>&1; grep -E "q=|bit" $O/fir.txt
+timeout -k 10 300 python tools/roll_ab.py 1000 1 "" "LFD_NT_STORES=1" > $O/roll.txt 2>&1; grep -E "W=|bit" $O/roll.txt
+for v in 0 1 0 1; do
+  LFD_NT_STORES=$v timeout -k 10 200 python tools/fr_bench.py 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('NT=$v', round(d['ms'],3), {k.split(' ')[0]: round(v,3) for k,v in d['kernels_ms'].items()}, d['relrms_vs_oracle_3ch'])" || exit 1
+done
