@@ -261,6 +261,32 @@ def test_rolling_mean_window_step(W, S_):
         assert _relrms(y[m], ref[m]) < 1e-6, layout
 
 
+@pytest.mark.parametrize("W,S_,n", [
+    (320, 16, 12_345),     # 80 outputs per unit: a batch of 64 leaves mid-unit, the rest at its end
+    (2032, 1008, 50_000),  # Q = 63: the prefix ring only fits batches of 8 (9 outputs per unit)
+    (4096, 64, 40_000),    # batches of 64 inside 256-output units
+])
+def test_rolling_seg_output_batches(W, S_, n):
+    """k_rolling_seg emits its outputs in batches (64, or fewer when the
+    prefix ring of 1,024 entries would not hold a batch's windows): batch
+    boundaries inside a unit and the ring bound give the oracle's means, with
+    nulls spread across batches."""
+    import torch
+    from lfdas.plan import rolling_mean_device
+    rng = np.random.default_rng(W + S_ + n)
+    n_ch = 3
+    x = (rng.standard_normal((n_ch, n)) + 3.0).astype(np.float32)
+    x[1, n // 3] = np.nan
+    x[2, n // 2] = np.inf
+    ref = oracle.rolling_mean(x, W, S_)
+    y = rolling_mean_device(torch.from_numpy(x).cuda(), W, S_).cpu().numpy()
+    assert y.shape == ref.shape
+    np.testing.assert_array_equal(np.isnan(y), np.isnan(ref))
+    np.testing.assert_array_equal(np.isposinf(y), np.isposinf(ref))
+    m = np.isfinite(ref)
+    assert _relrms(y[m], ref[m]) < 1e-6
+
+
 @pytest.mark.parametrize("S_", [1, 250, 200])
 def test_rolling_mean_overlapping_nulls(S_):
     """step < window: a NaN / inf sample turns exactly the windows holding it
