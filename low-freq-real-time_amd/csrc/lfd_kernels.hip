@@ -5362,6 +5362,10 @@ constexpr size_t fdm_lds_bytes() {
 // MFMAs: 2,000 x 600,000 at q = 10 1.648 -> 1.565 ms (barrier after 0 / 3 / 4
 // / 5 / 6 of the 6 Toeplitz steps: 1.648 / 1.653 / 1.623 / 1.593 / 1.565,
 // profiles/r05_fir_sched.txt)
+// The staging loads are 16-B pieces (lane 4l + 256r + e): 11 load
+// instructions per lane and tile at q = 10 instead of 44 dword loads (lane
+// l + 64r): 1.630 -> 1.539 ms at q = 10, 1.853 -> 1.763 at q = 4, bit-identical
+// (profiles/r05_fir_f4.txt)
 template <int Q>
 __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
                                                           int64_t s_ch, const double *__restrict__ h, int n_taps,
@@ -5371,7 +5375,6 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
   constexpr int DM = FDM_DM, NO = FDM_NO, NN = FDM_NN, RL = fdm_rl();
   diag = LFD_DG(diag);                     // production: 0, the diagnostics compile out
   constexpr int SPAN = NN * Q;             // samples per channel and tile
-  constexpr int NR = (SPAN + 63) / 64;     // staging loads per lane
   constexpr int JB = Q * RL + 32;          // j-block stride (floats)
   extern __shared__ double fdm_lds[];
   double *At = fdm_lds;                                          // [v][d][16]
@@ -5399,40 +5402,52 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
     At[e] = (u >= 0 && ti < n_taps) ? h[ti] : 0.0;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // staging: wave w loads channel w of the group, sample m = lane + 64 r of
-  // the tile's span, polyphase row v = Q - 1 - m % Q, index m / Q
+  // staging: wave w loads channel w of the group, samples m = 4 lane + e +
+  // 256 r of the tile's span (16-B pieces), polyphase row v = Q - 1 - m % Q,
+  // index m / Q
   const int64_t ch_ld = cg * 4 + w;
   const bool live = ch_ld < n_ch;
   const float *xr_ld = x + (live ? ch_ld : 0) * s_ch;
   float *row_ld = Xs + w * JB + offj(w);
-  float pf[NR];
+  constexpr int NR4 = (SPAN + 255) / 256;  // 16-B pieces per lane
+  float pf4[4 * NR4];
   auto issue = [&](int64_t Ot) {
     const int64_t s0 = (Ot - 4 * (DM - 1) - 1) * Q + delay - (Q - 1);
-    if (live && s0 >= 0 && s0 + 64 * NR <= n_t) {
-      const float *p = xr_ld + s0 + lane;
+    if (live && s0 >= 0 && s0 + 256 * NR4 <= n_t) {
+      const float *p = xr_ld + s0 + 4 * lane;  // (any alignment: 4-B aligned 16-B pieces)
 #pragma unroll
-      for (int r = 0; r < NR; ++r) pf[r] = p[64 * r];
+      for (int r = 0; r < NR4; ++r) {
+        const f4v v = *reinterpret_cast<const f4u *>(p + 256 * r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pf4[4 * r + e] = v[e];
+      }
     } else {  // record edges / channels past n_ch: clamped loads, zeros outside
 #pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int64_t t = s0 + lane + 64 * r;
-        const int64_t tc = t < 0 ? 0 : (t >= n_t ? n_t - 1 : t);
-        const float v = xr_ld[tc];
-        pf[r] = (live && t >= 0 && t < n_t) ? v : 0.0f;
-      }
+      for (int r = 0; r < NR4; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t t = s0 + 4 * lane + e + 256 * r;
+          const int64_t tc = t < 0 ? 0 : (t >= n_t ? n_t - 1 : t);
+          const float v = xr_ld[tc];
+          pf4[4 * r + e] = (live && t >= 0 && t < n_t) ? v : 0.0f;
+        }
     }
   };
   auto commit = [&]() {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));  // recomputed per tile, not hoisted into registers
-    const int n_l = ln / Q, r_l = ln - n_l * Q;
-    float *a0 = row_ld + (Q - 1 - r_l) * RL + n_l;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const int c = (64 * r) % Q, f = (64 * r) / Q;
-      const bool carry = r_l + c >= Q;
-      float *dst = a0 + (f - c * RL) + (carry ? Q * RL + 1 : 0);
-      if (64 * (r + 1) <= SPAN || ln + 64 * r < SPAN) *dst = pf[r];
+    for (int e = 0; e < 4; ++e) {
+      int ln = 4 * lane + e;
+      asm volatile("" : "+v"(ln));  // recomputed per tile, not hoisted into registers
+      const int n_l = ln / Q, r_l = ln - n_l * Q;
+      float *a0 = row_ld + (Q - 1 - r_l) * RL + n_l;
+#pragma unroll
+      for (int r = 0; r < NR4; ++r) {
+        // 256 r = f Q + c: the sample's row and index relative to the lane's
+        const int c = (256 * r) % Q, f = (256 * r) / Q;
+        const bool carry = r_l + c >= Q;
+        float *dst = a0 + (f - c * RL) + (carry ? Q * RL + 1 : 0);
+        if (256 * r + 255 < SPAN || ln + 256 * r < SPAN) *dst = pf4[4 * r + e];
+      }
     }
   };
   const int jl = lane & 3;                                  // B / D channel
@@ -5527,19 +5542,23 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     if (const char *dv = knob("LFD_FIR_DIAG")) diag = std::atoi(dv);
     bool launched = false;
     hipError_t e = hipSuccess;
-#define LFD_FDM(QV)                                                                                          \
-  case QV: {                                                                                                 \
+#define LFD_FDM1(QV)                                                                                    \
+  {                                                                                                          \
     static bool attr = false;                                                                                \
     if (!attr) {                                                                                             \
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                      \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                 \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV>());         \
       if (e != hipSuccess) return e;                                                                         \
       attr = true;                                                                                           \
     }                                                                                                        \
-    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdm_lds_bytes<QV>(), st>>>(                              \
+    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdm_lds_bytes<QV>(), st>>>(                         \
         x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, diag);                  \
-    launched = true;                                                                                         \
-    break;                                                                                                   \
+  }
+#define LFD_FDM(QV)            \
+  case QV: {                   \
+    LFD_FDM1(QV)               \
+    launched = true;           \
+    break;                     \
   }
     if (grid <= (int64_t)INT32_MAX) {
       switch (q) {
@@ -5552,6 +5571,7 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
       }
     }
 #undef LFD_FDM
+#undef LFD_FDM1
     if (launched) {
       if (kernel_used) *kernel_used = 1;
       return hipGetLastError();
