@@ -1,11 +1,6 @@
-# round-5 final: GPU suite, smoke, default bench
+# round-5: PMC passes on the full-rate kernels and the FIR decimation (after this round's changes)
 set -o pipefail
-O=gpurun_out/r05final
-mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
-echo "pytest exit $?"; tail -2 $O/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-echo "smoke exit $?"; tail -3 $O/smoke.log
-timeout -k 10 1000 python bench.py > $O/bench.json 2> $O/bench.err
-echo "bench exit $?"
-python tools/bench_summary.py $O/bench.json
+bash tools/pmc_fullrate.sh r05fr > /dev/null 2>&1 && echo fr-ok
+bash tools/pmc_kernel.sh r05fir k_fir_decimate tools/fir_one.py > /dev/null 2>&1 && echo fir-ok
+cat gpurun_out/pmc_r05fr/summary.txt | grep -E "k_fullrate_out_mb" | head -30
+cat gpurun_out/pmc_r05fir/summary.txt | head -30
