@@ -1165,8 +1165,8 @@ __device__ __forceinline__ void fr_out_mfma(int lane, const FRConst *__restrict_
 template <int CTRL>
 __device__ __forceinline__ double dpp_row_d(double v) {
   const int lo = __double2loint(v), hi = __double2hiint(v);
-  const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
-  const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+  const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, true);
+  const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, true);
   return __hiloint2double(h2, l2);
 }
 
