@@ -1597,7 +1597,13 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
       o[12] = yacc[mt][nt][3];
     }
     __syncthreads();
-    if (ys_t == 1) {  // 16-B pieces, 8-B aligned on rows of odd length (d2u)
+    if (ys_t == 1 && nsb == 64) {  // whole big block: no per-piece bounds, one base per lane
+      double *yp = yr + (lane >> 3) * LS + 16 * mt + 2 * (lane & 7);
+      const double *op = ob + (lane >> 3) * OSTR + 2 * (lane & 7);
+#pragma unroll
+      for (int it = 0; it < 8; ++it)
+        *reinterpret_cast<d2u *>(yp + it * 8 * LS) = *reinterpret_cast<const d2u *>(op + it * 8 * OSTR);
+    } else if (ys_t == 1) {  // 16-B pieces, 8-B aligned on rows of odd length (d2u)
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int r = it * 8 + (lane >> 3), c2 = 2 * (lane & 7);
