@@ -1427,10 +1427,16 @@ __global__ __launch_bounds__(64, FR_WAVES) void k_fullrate_out_mb(
   const int64_t m_row = 4 * k + (lane >> 4);
   const int64_t m = m_row < n_mb ? m_row : n_mb - 1;  // rows past the last medium block: any valid state
   double SinE[N], TinE[N];
+  {
+    // wave-uniform bases (medium block 4k) + one 32-bit per-lane byte offset
+    // (the row's m - 4k < 4): scalar-base loads, no 64-bit address per load
+    const double *sfb = SF + 4 * k * N * n_ch + ch, *stb = ST + (4 * k + 1) * N * n_ch + ch;
+    const uint32_t vo = (uint32_t)(m - 4 * k) * (uint32_t)(N * n_ch) * 8u;
 #pragma unroll
-  for (int n = 0; n < N; ++n) {
-    SinE[n] = SF[(m * N + n) * n_ch + ch];
-    TinE[n] = ST[((m + 1) * N + n) * n_ch + ch];
+    for (int n = 0; n < N; ++n) {
+      SinE[n] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(sfb + n * n_ch) + vo);
+      TinE[n] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(stb + n * n_ch) + vo);
+    }
   }
   {
     const float *row = x + ch * s_ch + a;
