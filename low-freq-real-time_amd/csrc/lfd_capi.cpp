@@ -1190,6 +1190,61 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
       for (const auto &G : p->chunks) nr_max = std::max<int64_t>(nr_max, G.r1 - G.r0);
       p->nw_fu = nr_max <= (int64_t)lfd::FU_SEG_HOST * lfd::FU_SEGR_HOST ? lfd::FU_SEG_HOST : 0;
       if (p->nw_fu) build_segs(lfd::FU_SEG_HOST, 1, p->segs_fu);
+      // the fused scan's right-edge maps: scan_tail (lfd_kernels.hip) on zero
+      // samples from S = e_k, in extended precision — the tail's forward walk
+      // over its samples and the odd-extension pad, the reverse from the
+      // steady state of the last forward output, the tail output (interp1d
+      // between two reverse outputs); the device adds its S = 0 walk
+      bool tmap_on = p->nw_fu != 0;
+      if (const char *v = lfd::knob("LFD_FU_TAILMAP")) tmap_on = tmap_on && std::atoi(v) != 0;
+      RModel tm_m;
+      if (tmap_on && make_rmodel(c, tm_m) != LFD_OK) tmap_on = false;
+      if (tmap_on && tm_m.ns != 2) tmap_on = false;  // (run mode is 4th order)
+      for (int64_t ci = 0; tmap_on && ci < n_chunks; ++ci) {
+        const auto &G = p->chunks[ci];
+        const int J = tm_m.J;
+        const int64_t ntp = G.s1 + 1 - G.tail_begin + padlen;
+        R TM[4][4] = {}, tmv[4] = {};
+        std::vector<R> tp((size_t)ntp);
+        for (int k = 0; k < 4; ++k) {
+          R S[4] = {0, 0, 0, 0};
+          S[k] = 1;
+          R ylast = 0;
+          for (int64_t i = 0; i < ntp; ++i) tp[(size_t)i] = ylast = tm_m.G * r_allpole(tm_m, S, 0);
+          R T[4], v = ylast;
+          for (int sct = 0; sct < 2; ++sct) {
+            v *= 1.0L / ((1.0L + tm_m.a1[sct]) + tm_m.a2[sct]);
+            T[2 * sct] = T[2 * sct + 1] = v;
+          }
+          R qw[lfd::MAX_J];
+          for (int j = 0; j < J; ++j) qw[j] = v;
+          R y_next = 0, y_out = 0;
+          for (int64_t i = ntp - 1; i >= 0; --i) {
+            const R q = r_allpole(tm_m, T, tp[(size_t)i]);
+            if (G.tail_out_j >= 0 && (G.tail_begin + i == G.tail_out_pos || G.tail_begin + i == G.tail_out_pos + 1)) {
+              R acc = q;
+              for (int j = 1; j <= J; ++j) acc += tm_m.c[j] * qw[j - 1];
+              acc *= tm_m.G;
+              if (G.tail_begin + i == G.tail_out_pos + 1)
+                y_next = acc;
+              else
+                y_out = acc + (R)p->ow * (y_next - acc);
+            }
+            for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
+            qw[0] = q;
+          }
+          for (int i = 0; i < 4; ++i) TM[i][k] = T[i];
+          tmv[k] = y_out;
+        }
+        for (int sgi = 0; sgi < lfd::FU_SEG_HOST; ++sgi) {
+          lfd::SegGeom &sgm = p->segs_fu[(size_t)(ci * lfd::FU_SEG_HOST + sgi)];
+          sgm.tmap = 1;
+          for (int i = 0; i < 4; ++i) {
+            sgm.tm[i] = (double)tmv[i];
+            for (int k = 0; k < 4; ++k) sgm.TM[i * 4 + k] = (double)TM[i][k];
+          }
+        }
+      }
     }
     if (n_off > 0) {
       // per offset d: the output's responses to the states (G0_d, H0_d) and

@@ -198,6 +198,12 @@ constexpr int SC_N_HOST = 24;  // doubles per (chunk, channel) of the segmented 
 struct SegGeom {
   int64_t ra, rb, last;
   double P[16], Q[16];
+  // fused scan (k_scan_fused) only: the chunk's right edge is affine in the
+  // forward state S entering it, T_end = T_end(S = 0) + TM S and the tail
+  // output = its S = 0 value + tm . S (host-simulated, every entry of the
+  // chunk; tmap = 0: walk the edge after the forward states instead)
+  int64_t tmap;
+  double TM[16], tm[4];
 };
 constexpr int HSKIP_MAX = 32;
 struct RunGeom {

@@ -635,7 +635,7 @@ __device__ __forceinline__ void scan_tail(const float *__restrict__ xc, int64_t 
                                           const SeqR<NS> &R, const ScanConst &sc, double (&S)[2 * NS],
                                           double *__restrict__ tp, int64_t tp_stride, float *__restrict__ y,
                                           int64_t ch, int64_t ys_ch, int64_t ys_t, double (&T)[2 * NS],
-                                          bool store = true) {
+                                          bool store = true, double *yret = nullptr) {
   constexpr int J = 2 * NS;
   constexpr int SB = 8;
   double h[J];
@@ -686,10 +686,15 @@ __device__ __forceinline__ void scan_tail(const float *__restrict__ xc, int64_t 
 #pragma unroll
       for (int j = 1; j <= J; ++j) acc = fma(sc.r.c64[j], qw[j - 1], acc);
       acc *= sc.r.G;
-      if (G.tail_begin + i == G.tail_out_pos + 1)
+      if (G.tail_begin + i == G.tail_out_pos + 1) {
         y_next = acc;
-      else if (store)  // interp1d between the two samples (w = sc.ow)
-        y[ch * ys_ch + G.tail_out_j * ys_t] = (float)fma(sc.ow, y_next - acc, acc);
+      } else {  // interp1d between the two samples (w = sc.ow)
+        const double yv = fma(sc.ow, y_next - acc, acc);
+        if (yret)
+          *yret = yv;  // (k_scan_fused's zero-state edge: the caller adds the state part)
+        else if (store)
+          y[ch * ys_ch + G.tail_out_j * ys_t] = (float)yv;
+      }
     }
 #pragma unroll
     for (int j = J - 1; j > 0; --j) qw[j] = qw[j - 1];
@@ -4338,7 +4343,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
   FU_STAMP();
   __shared__ RunConst rcs;
   __shared__ double Ps[FU_SEG][16], Qs[FU_SEG][16];
-  __shared__ double aggf[FU_SEG][N][16], aggb[FU_SEG][N][16], hS[N][16], tT[N][16], corr[NF][16];
+  __shared__ double aggf[FU_SEG][N][16], aggb[FU_SEG][N][16], hS[N][16], tT[N][16], corr[NF][16], tY[16];
   __shared__ float otile[4][64][RUN_R + 1];  // output staging per wave
   __shared__ int64_t omk[4][64];             // its run's first block
   __shared__ int oml[4][64];                 // its run's length (0: nothing to store)
@@ -4415,6 +4420,19 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
     for (int i = 0; i < N; ++i) hS[i][col] = S[i];
 #pragma unroll
     for (int i = 0; i < NF; ++i) corr[i][col] = cr[i];
+  }
+  // right edge, state-free part: the edge is affine in the S entering it
+  // (SegGeom::TM / tm, host-simulated), so its lanes walk it from S = 0 now
+  // — beside the left edge, while the forward chain is not known yet — and
+  // add TM S after the forward walk (step 3)
+  const bool tmap = sgc[tail_seg].tmap != 0;
+  if (tmap && sg == tail_seg) {
+    double Sz[N] = {0.0, 0.0, 0.0, 0.0}, Tz[N], yz = 0.0;
+    scan_tail<2>(xc, s_t, G, padlen, R, sc, Sz, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t, Tz,
+                 false, &yz);
+#pragma unroll
+    for (int i = 0; i < N; ++i) tT[i][col] = Tz[i];
+    tY[col] = yz;
   }
   // (segment 0's lanes wrote corr themselves: a wave reads its own LDS writes
   // in order; the other segments never reach run r0)
@@ -4498,8 +4516,25 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
       yv[u][pp] = (u >= nrun || pp >= len[u] || (LFD_DG(g_fu_diag) & 2)) ? 0.0 : y0b[(ksv[u] + pp) * 16];
   if (sg == tail_seg) {
     double T[N];
-    scan_tail<2>(xc, s_t, G, padlen, R, sc, S, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t, T,
-                 valid);
+    if (tmap) {
+      const double *TM = sgc[tail_seg].TM, *tm = sgc[tail_seg].tm;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double acc = tT[i][col];
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc = fma(TM[i * 4 + j], S[j], acc);
+        T[i] = acc;
+      }
+      if (G.tail_out_j >= 0 && valid) {
+        double yv = tY[col];
+#pragma unroll
+        for (int j = 0; j < N; ++j) yv = fma(tm[j], S[j], yv);
+        y[ch * ys_ch + G.tail_out_j * ys_t] = (float)yv;
+      }
+    } else {
+      scan_tail<2>(xc, s_t, G, padlen, R, sc, S, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t, T,
+                   valid);
+    }
 #pragma unroll
     for (int i = 0; i < N; ++i) tT[i][col] = T[i];
   }
