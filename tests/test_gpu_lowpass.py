@@ -596,6 +596,7 @@ def test_scan_segmented_chains_match_deferred(cfg):
 @pytest.mark.parametrize("cfg", [
     (500.0, 1.0, 60, 7, 70, 400.0, 0, False, "tc"),          # short chains (~8 runs per chunk), ragged 64-groups
     (500.0, 1.0, 600, 7, 130, 1500.0, 123_457, False, "tc"),  # off-sample grid, head skip, 3 x 64-groups
+    (500.0, 1.0, 600, 7, 19, 1500.0, 123_457, True, "tc"),    # the same with a null (the right edge's map)
     (1000.0, 10.0, 30, 6, 20, 3000.0, 0, True, "tc"),        # dt = 10 s: long chains (sub-blocks), a null
     (500.0, 1.0, 600, 7, 64, 1200.0, 0, True, "cc"),         # (time, channel) storage, one full 64-group
     (250.0, 0.2, 40, 6, 24, 24.0, 0, False, "tc"),           # cfg1 geometry: 1-run chunks
