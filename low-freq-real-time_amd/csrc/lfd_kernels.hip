@@ -4317,6 +4317,9 @@ __constant__ int g_fu_diag = 0;
 // k_scan_fused phase stamps (LFD_FU_TIMES): [wg < 8192][wave < 4][8]
 __device__ uint64_t g_fu_times[8192 * 4 * 8];
 #endif
+// (registers for 3 workgroups per CU — one round of the 1,250-channel
+// shard's 553 workgroups — spill 34 dwords: scan 0.073 -> 0.080 ms,
+// profiles/r05_scan_tailmap.txt)
 __global__ __launch_bounds__(256, 2) void k_scan_fused(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen, const ScanConst sc,
     const ChunkGeom *__restrict__ cgs, int64_t n_chunks, RunGeom rg, const SegGeom *__restrict__ sgs,
@@ -4502,18 +4505,21 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
     for (int i = 0; i < N; ++i) sin[u][i] = S[i];
     if (u < nrun) fstep(S, ef[u], len[u], ra + u);
   }
-  // the segment's y0 (the E_f registers are free now): in flight behind the
-  // right edge, the backward aggregates and the reverse combine
+  // the segment's y0: the last run's in flight behind the right edge, the
+  // backward aggregates and the reverse combine; each earlier run's loads one
+  // run ahead in the T walk (holding all of them took 80 VGPRs: 2 workgroups
+  // per CU instead of 3)
   const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
-  double yv[SR_][RUN_R];
   int64_t ksv[SR_];
 #pragma unroll
   for (int u = 0; u < SR_; ++u) ksv[u] = u < nrun ? rg.run_ks[ra + u] : 0;
-#pragma unroll
-  for (int u = 0; u < SR_; ++u)
+  auto y0run = [&](int u, double (&yr)[RUN_R]) {
 #pragma unroll
     for (int pp = 0; pp < RUN_R; ++pp)
-      yv[u][pp] = (u >= nrun || pp >= len[u] || (LFD_DG(g_fu_diag) & 2)) ? 0.0 : y0b[(ksv[u] + pp) * 16];
+      yr[pp] = (u >= nrun || pp >= len[u] || (LFD_DG(g_fu_diag) & 2)) ? 0.0 : y0b[(ksv[u] + pp) * 16];
+  };
+  double ycur[RUN_R];
+  y0run(SR_ - 1, ycur);
   if (sg == tail_seg) {
     double T[N];
     if (tmap) {
@@ -4539,13 +4545,16 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
     for (int i = 0; i < N; ++i) tT[i][col] = T[i];
   }
   // E_r of the segment's runs (after the right edge: fewer live registers there)
-  double er[SR_][N];
-#pragma unroll
-  for (int u = 0; u < SR_; ++u) {
+  // (step 4 holds them all; the T walk re-reads each run's, one run ahead,
+  // from the cache, so they are not live through step 5)
+  auto errun = [&](int u, double (&e)[N]) {
     const int64_t r = u < nrun ? ra + u : G.r0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) er[u][i] = agb[(r * 8 + 4 + i) * 16];
-  }
+    for (int i = 0; i < N; ++i) e[i] = agb[(r * 8 + 4 + i) * 16];
+  };
+  double er[SR_][N];
+#pragma unroll
+  for (int u = 0; u < SR_; ++u) errun(u, er[u]);
   FU_STAMP();
   // ---- 4. backward aggregates
   {
@@ -4590,17 +4599,25 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
   // instead of 64 scattered 4-B lanes
   const int wv = threadIdx.x >> 6, ln64 = threadIdx.x & 63;
   float(*tile)[RUN_R + 1] = otile[wv];
+  double ecur[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) ecur[i] = er[SR_ - 1][i];
 #pragma unroll
   for (int u = SR_ - 1; u >= 0; --u) {
     const bool live = u < nrun;
     const int ln = live ? len[u] : 0;
     const int64_t ks = ksv[u];
+    double ynext[RUN_R], enext[N];
+    if (u > 0) {
+      y0run(u - 1, ynext);
+      errun(u - 1, enext);
+    }
 #pragma unroll
     for (int pp = 0; pp < RUN_R; ++pp) {
       const int64_t k = ks + pp;
       float o = 0.f;
       if (pp < ln && is_out(k)) {
-        double acc = yv[u][pp] + (k == G.kb ? crk : 0.0);
+        double acc = ycur[pp] + (k == G.kb ? crk : 0.0);
         const double *A = rcs.A[ln][pp];
         const double *B = rcs.B[ln - 1 - pp];
 #pragma unroll
@@ -4628,7 +4645,13 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (live) bstep(T, sin[u], er[u], ln, ra + u);
+    if (live) bstep(T, sin[u], ecur, ln, ra + u);
+    if (u > 0) {
+#pragma unroll
+      for (int pp = 0; pp < RUN_R; ++pp) ycur[pp] = ynext[pp];
+#pragma unroll
+      for (int i = 0; i < N; ++i) ecur[i] = enext[i];
+    }
   }
   FU_STAMP();
 #undef FU_STAMP
