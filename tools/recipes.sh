@@ -158,10 +158,24 @@ case "$1" in
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
     timeout -k 10 700 python bench.py > gpurun_out/final_bench.json 2> gpurun_out/final_bench.err || exit 1
     tail -1 gpurun_out/final_bench.json ;;
+  # ---- round 5 (lib_ab: old / new diagnostic libraries alternated in separate
+  # processes; the old one built from the previous commit into tools/ab/old/lib)
+  dp_pipe)  # fp64 MFMA vs VALU issue on one SIMD (profiles/r05_dp_pipe.txt)
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o tools/ubench_dp_pipe tools/ubench_dp_pipe.hip &&
+    timeout -k 10 120 ./tools/ubench_dp_pipe ;;
+  fr_lib_ab) # full-rate output pass, old vs new library (profiles/r05_fr_dpp_boundctrl.txt)
+    ./tools/lib_ab.sh "$PWD/tools/ab/old/lib/liblfdas_diag.so" "$LFDAS_LIB" 3 -- python -u tools/fr_bench.py ;;
+  fu_tailmap) # fused scan right-edge map and register budget (profiles/r05_scan_tailmap.txt)
+    timeout -k 10 300 python -u tools/ab_plan.py --ch 1250 --reps 5 --replan "" "LFD_FU_TAILMAP=0" ;;
+  mf_modes) # full-rate functionals diag modes (profiles/r05_mf_modes.txt)
+    for m in 0 1 3 6; do LFD_MF_MODE=$m timeout -k 10 100 python -u tools/fr_bench.py || exit 1; done ;;
+  copy_ceiling) # read + write ceiling for rolling S = 1 (profiles/r05_copy_ceiling.txt)
+    timeout -k 10 120 python -u tools/copy_ceiling.py ;;
   rehearsal) # N = 2 on one device: strong-scaling headline + sharded cfg5 stream
     unset LFDAS_LIB
     timeout -k 10 400 python bench.py --gpus 2 --one-device --steps 3 --warmup 1 --no-cpu --no-rolling --no-extra ;;
   *) echo "recipes: k1 units scan offgrid tm_r02 rolling_r02 mfma tm tm_ubench narrow longscan rolling fir fir_pmc"
      echo "         fullrate lattice multi persist narrow_units scan_trace fr_mb fr_out fr_pmc lattice_pmc tm_wg"
-     echo "         cm_wg fir_strip final rehearsal seg_scan odd_strides fr_scan_edges fir_xcd"; exit 2 ;;
+     echo "         cm_wg fir_strip final rehearsal seg_scan odd_strides fr_scan_edges fir_xcd"
+     echo "         dp_pipe fr_lib_ab fu_tailmap mf_modes copy_ceiling"; exit 2 ;;
 esac
