@@ -265,7 +265,7 @@ def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_majo
     else:
         x = device_samples((n_ch, n), device=dev)
         synth_fill(x, fs, 77)
-    y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
+    y = torch.empty((n_ch, plan.n_grid), dtype=torch.float64, device=dev)
     wsb = plan.alloc_workspace(dev)
     stream = torch.cuda.current_stream(dev)
     el, k1_ms, scan_ms = time_plan(plan, x, y, wsb, stream, steps, warmup)
@@ -274,14 +274,14 @@ def bench_lowpass_line(dev, n_ch, fs, seconds, dt_out, P, B, off_ns=0, time_majo
         el = time_plan_pipelined(plan, x, y, steps, warmup)
     R = int(round(fs * dt_out))
     k1 = float(np.mean(k1_ms))
-    gbs = n_ch * n * (4.0 + 4.0 / R) / (k1 * 1e-3) / 1e9
+    gbs = n_ch * n * (4.0 + 8.0 / R) / (k1 * 1e-3) / 1e9
     out = {"value": n_ch * n * steps / el, "unit": "channel-samples/s", "ms_per_step": el / steps * 1e3,
            "ms_per_step_serial": el_s / steps * 1e3, "pipelined": PIPELINED,
            "config": label, "k1": plan.last_kernel(), "block_len": plan.block_len,
            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": gbs / HBM_PEAK_GBS, "kernel": K1_KERNELS.get(plan.last_kernel()),
                         "kernel_ms": k1, "scan_kernel_ms": float(np.mean(scan_ms)),
-                        "alg_bytes_per_sample": 4.0 + 4.0 / R}}
+                        "alg_bytes_per_sample": 4.0 + 8.0 / R}}
     n_off, onepass, _ = plan.lattice()
     if n_off or "lattice" in label:
         out["lattice"] = {"offsets": n_off, "onepass": onepass}
@@ -465,7 +465,7 @@ def bench_ooc_cfg5(dev, n_ch=50_000, seconds=3600.0, push_s=60.0):
     rel = (float(np.sqrt(np.sum((got.astype(np.float64) - want) ** 2) / np.sum(want ** 2)))
            if got.shape == want.shape else float("inf"))
     out["check"] = {"rows": CFG5_ROWS, "relrms_vs_oracle": rel, "times_identical": times_ok,
-                    "pass": bool(times_ok and rel < 1e-4),
+                    "pass": bool(times_ok and rel < 1e-9),
                     "checker": "oracle.lfproc_process on the sampled rows (untimed)"}
     if not out["check"]["pass"]:
         print(f"WARNING: cfg5 sampled-channel check failed: {out['check']}", file=sys.stderr)
@@ -558,7 +558,7 @@ def bench_ooc_cfg5_sharded(dev, ws, rank, barrier, max_over_ranks, n_ch=50_000, 
                                            np.concatenate([t for t, _ in ref])))
             if got.shape == want.shape:
                 rel = float(np.sqrt(np.sum((got.astype(np.float64) - want) ** 2) / np.sum(want ** 2)))
-            ok = 1.0 if (times_ok and rel < 1e-4) else 0.0
+            ok = 1.0 if (times_ok and rel < 1e-9) else 0.0
         except Exception as e:
             err = e
     for p in pins:
@@ -858,7 +858,7 @@ def main():
     # placement; the 72 GB single-GPU input is that size already)
     x = device_samples((n_ch, n), device=dev)
     synth_fill(x, args.fs, 1234 + rank)
-    y = torch.empty((n_ch, plan.n_grid), dtype=torch.float32, device=dev)
+    y = torch.empty((n_ch, plan.n_grid), dtype=torch.float64, device=dev)
     wsb = plan.alloc_workspace(dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -890,7 +890,7 @@ def main():
     R = int(round(args.fs * args.dt_out))
     value = n_ch_total * n * args.steps / el
     k1 = float(np.mean(k1_ms))
-    alg_bytes = n_ch * n * (4.0 + 4.0 / R)
+    alg_bytes = n_ch * n * (4.0 + 8.0 / R)
     achieved = alg_bytes / (k1 * 1e-3) / 1e9
     traffic = None
     try:
@@ -919,8 +919,8 @@ def main():
             del full
             gm = max_over_ranks(float(np.median(g_ms)))
             secondary["allgather_outputs"] = {
-                "ms": gm, "bytes_per_rank": int(y.numel() * 4), "frac_of_step": gm / (el / args.steps * 1e3),
-                "note": "RCCL all_gather of every rank's (n_ch, n_grid) float32 outputs; not in the timed step"}
+                "ms": gm, "bytes_per_rank": int(y.numel() * 8), "frac_of_step": gm / (el / args.steps * 1e3),
+                "note": "RCCL all_gather of every rank's (n_ch, n_grid) float64 outputs; not in the timed step"}
         except Exception as e:  # the optional gather never voids the bench line
             secondary["allgather_outputs"] = {"error": repr(e)}
     del x, y, wsb
@@ -936,7 +936,7 @@ def main():
         plan_w, _, _, _, _, _ = build_plan(o1 - o0, n, args.fs, args.dt_out, args.patch_size, args.edge_buff)
         xw = device_samples((o1 - o0, n), device=dev)
         synth_fill(xw, args.fs, 4321 + rank)
-        yw = torch.empty((o1 - o0, plan_w.n_grid), dtype=torch.float32, device=dev)
+        yw = torch.empty((o1 - o0, plan_w.n_grid), dtype=torch.float64, device=dev)
         ww = plan_w.alloc_workspace(dev)
         el_w, k1_w, _ = time_plan(plan_w, xw, yw, ww, stream, args.steps, 1, barrier)
         el_w = max_over_ranks(el_w)
@@ -1051,7 +1051,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": K1_KERNELS.get(k1_kernel), "kernel_ms": k1,
                          "scan_kernel_ms": float(np.mean(scan_ms)),
-                         "alg_bytes_per_sample": 4.0 + 4.0 / R, "samples_per_launch": n_ch * n},
+                         "alg_bytes_per_sample": 4.0 + 8.0 / R, "samples_per_launch": n_ch * n},
             "cpu_baseline": cpu,
             "secondary": secondary,
         }

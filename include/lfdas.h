@@ -25,7 +25,10 @@
  *   - arrays are 2-D (channel, time) addressed through element strides
  *     (s_ch, s_t): DASCore's dims ("distance","time") is s_t == 1, the
  *     real-file layout ("time","distance") is s_ch == 1.
- *   - arithmetic is float64 on device; samples are float32 in, float32 out.
+ *   - arithmetic is float64 on device; samples are float32 in.  Low-pass
+ *     outputs are float64 (SciPy's sosfiltfilt result dtype,
+ *     scipy/signal/_signaltools.py:4684, which lf_das.py:223-232 interpolates
+ *     and writes); rolling means are float32.
  *   - caller owns x / y / workspace; the library owns plans only.
  *   - entry points are re-entrant per (device, stream); execute functions
  *     do no allocation and no synchronisation (hipGraph-capturable).
@@ -110,9 +113,9 @@ int lfd_lowpass_plan_create(lfd_lowpass_plan **plan, const double *sos,
 /* Workspace bytes needed by lfd_lowpass_execute, block geometry. */
 int lfd_lowpass_plan_info(const lfd_lowpass_plan *plan, size_t *workspace_bytes,
                           int64_t *n_blocks, int64_t *block_len);
-/* y[ch*ys_ch + j*ys_t] for j in [0, n_grid) that some chunk produces. */
+/* y[ch*ys_ch + j*ys_t] (float64) for j in [0, n_grid) that some chunk produces. */
 int lfd_lowpass_execute(const lfd_lowpass_plan *plan, const float *x,
-                        int64_t s_ch, int64_t s_t, float *y, int64_t ys_ch,
+                        int64_t s_ch, int64_t s_t, double *y, int64_t ys_ch,
                         int64_t ys_t, void *workspace, void *stream);
 /* Two-stream execute for batch pipelines: the block pass (K1) runs on
  * `block_stream`, the chunk scan and the outputs on `scan_stream` after it
@@ -125,7 +128,7 @@ int lfd_lowpass_execute(const lfd_lowpass_plan *plan, const float *x,
  * reference (LFProc.process_time_range, lf_das.py:219-290, filters one
  * range per call); it is the same computation as lfd_lowpass_execute. */
 int lfd_lowpass_execute_split(const lfd_lowpass_plan *plan, const float *x,
-                              int64_t s_ch, int64_t s_t, float *y,
+                              int64_t s_ch, int64_t s_t, double *y,
                               int64_t ys_ch, int64_t ys_t, void *workspace,
                               void *block_stream, void *scan_stream);
 /* Per-kernel device time of the last execute on `stream` (ms), measured
@@ -157,6 +160,19 @@ int lfd_set_timing(int enable);
  * 32-channel row lines, in-register run folding (4th-order cascades). */
 #define LFD_K1_MFMA_RUNS_TM 6
 int lfd_lowpass_last_kernel(const lfd_lowpass_plan *plan);
+/* Which chunk scan the last execute ran: LFD_SCAN_BLOCKS (per-block scan of
+ * plans without run folding) or, for run-mode plans, the outputs inside the
+ * backward run chain (IN_CHAIN), deferred to a parallel output kernel
+ * (DEFERRED), segmented chains (SEGMENTED) or the one-launch fused segmented
+ * scan (FUSED); -1 before the first execute.  Testing hook for
+ * LFD_OPT_SCAN_DEFER (options 3 / 4 fall back to the default choice when the
+ * plan's segment tables do not fit). */
+#define LFD_SCAN_BLOCKS 0
+#define LFD_SCAN_IN_CHAIN 1
+#define LFD_SCAN_DEFERRED 2
+#define LFD_SCAN_SEGMENTED 3
+#define LFD_SCAN_FUSED 4
+int lfd_lowpass_last_scan(const lfd_lowpass_plan *plan);
 /* Testing hook: the plan's block taps Kx[n_comp][row_len] in natural layout,
  * F_c(k) = sum_p Kx[c][p] x[base + k*L - J + p] (row_len = L + J).  With
  * taps == NULL only the sizes are returned.  LFD_EUNSUPPORTED when the plan
@@ -189,7 +205,7 @@ int lfd_debug_plan_constants(const lfd_lowpass_plan *plan, void *block_const,
 int lfd_sos_filtfilt_resample_f32(const float *x, int64_t n_ch, int64_t n_t,
                                   int64_t s_ch, int64_t s_t, const double *sos,
                                   int n_sec, int padlen, const int64_t *lo,
-                                  const double *w, int64_t n_out, float *y,
+                                  const double *w, int64_t n_out, double *y,
                                   int64_t ys_ch, int64_t ys_t, void *stream);
 
 /* ------------------------------------------------------------------------
@@ -214,7 +230,7 @@ int lfd_sosfiltfilt_last_timing(float *ms_functionals, float *ms_scan,
  * lo[j] + w[j] (DASCore Patch.interpolate → interp1d, _interpolate.py:457). */
 int lfd_interp_linear_f64(const double *x, int64_t n_ch, int64_t n_t,
                           int64_t s_ch, int64_t s_t, const int64_t *lo_dev,
-                          const double *w_dev, int64_t n_out, float *y,
+                          const double *w_dev, int64_t n_out, double *y,
                           int64_t ys_ch, int64_t ys_t, void *stream);
 
 /* ------------------------------------------------------------------------
@@ -335,7 +351,7 @@ typedef struct lfd_stream_output {
   int64_t t_step_ns;    /* spacing (int(dt*1000) ms)                                 */
   int64_t n_chunks;     /* LFProc chunks (reference output files) completed          */
   int64_t n_runs;       /* process_time_range runs executed so far                   */
-  const float *y;       /* device (n_ch, n_out), row stride ys_ch; valid until the
+  const double *y;      /* device (n_ch, n_out), row stride ys_ch; valid until the
                            second-next push                                          */
   int64_t ys_ch;
 } lfd_stream_output;
@@ -345,7 +361,7 @@ int lfd_stream_last_chunks(const lfd_stream *s, int64_t *counts, int64_t max_chu
                            int64_t *n_chunks);
 /* Wait for the last push (its host->HBM copy and its outputs) and copy the
  * outputs to host y[ch*ys_ch + j*ys_t] (nothing to copy when n_out == 0). */
-int lfd_stream_fetch(lfd_stream *s, float *y, int64_t ys_ch, int64_t ys_t);
+int lfd_stream_fetch(lfd_stream *s, double *y, int64_t ys_ch, int64_t ys_t);
 /* Wait until the last push's host buffer has been read (its host->HBM copy
  * is done; the run may still be executing).  A pinned ring of host buffers is
  * refilled after this returns. */

@@ -806,15 +806,17 @@ struct lfd_lowpass_plan {
   // (a stream wait binds to the record made before it)
   mutable std::vector<hipEvent_t> split_ev;
   mutable size_t split_i = 0;
+  mutable std::mutex split_mu;  // (executes of one plan from several host threads)
   mutable int64_t n_exec = 0;
   mutable int last_ring = 0;  // ring size of the last timed execute (0: ev)
   mutable bool timed = false;
   mutable std::atomic<int> last_k1{0};  // (plans may be executed from several host threads)
+  mutable std::atomic<int> last_scan{-1};
   // Composite plan (grids that are not one uniform lattice with one fraction
   // w: 3 kHz data on integer-ns times, jittered archives): one uniform,
   // sample-aligned sub-plan per lattice phase d (positions lo0 + j R + d),
   // each writing its lattice outputs into rows [toff, toff + n) of an
-  // [n_ch][comp_T] float32 scratch, then k_blend_grid forms
+  // [n_ch][comp_T] float64 scratch, then k_blend_grid forms
   // y[j] = (1 - w_j) Y_{d_j}[j] + w_j Y_{d_j + 1}[j] (linear interp1d).
   std::vector<lfd_lowpass_plan *> subs;
   std::vector<int64_t> sub_toff;
@@ -833,7 +835,7 @@ struct lfd_lowpass_plan {
 extern "C" {
 
 const char *lfd_last_error(void) { return g_err.c_str(); }
-int lfd_version(void) { return 100; }
+int lfd_version(void) { return 200; }  // 2.0: float64 low-pass outputs
 
 int lfd_device_count(int *count) {
   if (!count) return fail(LFD_EINVAL, "count is NULL");
@@ -1530,7 +1532,7 @@ static int plan_create_composite(lfd_lowpass_plan **out, const double *sos, int 
     g_err = err_keep;
   }
   p->off_tmp = align256(ws_max);
-  p->ws_bytes = align256(p->off_tmp + sizeof(float) * (size_t)n_ch *
+  p->ws_bytes = align256(p->off_tmp + sizeof(double) * (size_t)n_ch *
                                           (size_t)std::max(p->comp_T, p->lat ? n_off * n : (int64_t)0));
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -1576,12 +1578,12 @@ int lfd_lowpass_plan_info(const lfd_lowpass_plan *p, size_t *ws, int64_t *nb, in
 }
 
 int lfd_lowpass_execute(const lfd_lowpass_plan *p, const float *x, int64_t s_ch,
-                        int64_t s_t, float *y, int64_t ys_ch, int64_t ys_t,
+                        int64_t s_t, double *y, int64_t ys_ch, int64_t ys_t,
                         void *workspace, void *stream) {
   return lfd::lowpass_execute_gen(p, x, s_ch, s_t, y, ys_ch, ys_t, workspace, stream, lfd::GridGen{});
 }
 
-int lfd_lowpass_execute_split(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
+int lfd_lowpass_execute_split(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, double *y,
                               int64_t ys_ch, int64_t ys_t, void *workspace, void *block_stream, void *scan_stream) {
   if (!scan_stream) return fail(LFD_EINVAL, "scan_stream is NULL");
   return lfd::lowpass_execute_gen(p, x, s_ch, s_t, y, ys_ch, ys_t, workspace, block_stream, lfd::GridGen{},
@@ -1595,6 +1597,7 @@ namespace {
 // be recorded again by a later execute)
 hipError_t stream_after(const lfd_lowpass_plan *p, hipStream_t to, hipStream_t from) {
   constexpr size_t N_SPLIT_EV = 8;
+  std::lock_guard<std::mutex> lk(p->split_mu);
   if (p->split_ev.size() < N_SPLIT_EV) {
     hipEvent_t e = nullptr;
     const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -1608,7 +1611,7 @@ hipError_t stream_after(const lfd_lowpass_plan *p, hipStream_t to, hipStream_t f
 }
 }  // namespace
 
-int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
+int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, double *y,
                              int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const lfd::GridGen &gen,
                              void *scan_stream) {
   if (!p) return fail(LFD_EINVAL, "plan is NULL");
@@ -1622,6 +1625,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
   // the scan's stream: `st`, or (split execute) scan_stream after the block pass
   hipStream_t st2 = scan_stream ? reinterpret_cast<hipStream_t>(scan_stream) : st;
   char *ws = static_cast<char *>(workspace);
+  int scan_used = -1;
   double *F = reinterpret_cast<double *>(ws + p->off_F);
   double *SF = reinterpret_cast<double *>(ws + p->off_SF);
   double *TP = reinterpret_cast<double *>(ws + p->off_TP);
@@ -1645,7 +1649,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     LFD_HIP(hipEventRecord(ev[0], st));
   }
   if (!p->subs.empty()) {
-    float *tmp = reinterpret_cast<float *>(ws + p->off_tmp);
+    double *tmp = reinterpret_cast<double *>(ws + p->off_tmp);
     const lfd_lowpass_plan *L = p->lat;
     p->last_onepass = L && s_t == 1 && (reinterpret_cast<uintptr_t>(x) & 3) == 0 &&
                       !lfd::option(LFD_OPT_LATTICE_PHASES);
@@ -1665,7 +1669,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
                                        reinterpret_cast<double *>(ws + L->off_TR),
                                        reinterpret_cast<double *>(ws + L->off_CR), L->d_slot_chunk, L->n_off,
                                        L->d_rc_off, L->d_chunks_off, tmp, L->n_off * n_g, n_g, st, L->d_segs,
-                                       L->seg_max, reinterpret_cast<double *>(ws + L->off_SC)));
+                                       L->seg_max, reinterpret_cast<double *>(ws + L->off_SC), &scan_used));
+      p->last_scan = scan_used;
       LFD_HIP(lfd::launch_blend_grid_sm(tmp, p->n_ch, p->d_bj, p->d_bi_lat, p->d_bw, p->n_blend, y, ys_ch, ys_t, st,
                                         gen));
       if (timed) LFD_HIP(hipEventRecord(ev[2], st));
@@ -1686,6 +1691,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     if (timed) LFD_HIP(hipEventRecord(ev[2], st));
     if (st2 != st) LFD_HIP(stream_after(p, st2, st));
     p->last_k1 = p->subs[0]->last_k1.load();
+    p->last_scan = p->subs[0]->last_scan.load();
     return LFD_OK;
   }
   // K1: fp64-MFMA block taps when the layout allows, else the recurrence
@@ -1725,7 +1731,8 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
                                         reinterpret_cast<double *>(ws + p->off_TR),
                                         reinterpret_cast<double *>(ws + p->off_CR), p->d_slot_chunk, p->d_segs,
                                         p->seg_max, reinterpret_cast<double *>(ws + p->off_SC), p->d_segs_fu,
-                                        p->nw_fu));
+                                        p->nw_fu, &scan_used));
+    p->last_scan = scan_used;
     if (timed) LFD_HIP(hipEventRecord(ev[2], st2));
     return LFD_OK;
   }
@@ -1737,6 +1744,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
   if (st2 != st) LFD_HIP(stream_after(p, st2, st));
   LFD_HIP(lfd::launch_chunk_scan(p->n_sec, p->fir32, x, s_ch, s_t, p->bg, p->padlen, p->sc, p->d_chunks,
                                  p->n_chunks, F, SF, TP, p->tp_len, y, ys_ch, ys_t, st2));
+  p->last_scan = LFD_SCAN_BLOCKS;
   if (timed) LFD_HIP(hipEventRecord(ev[2], st2));
   return LFD_OK;
 }
@@ -1829,6 +1837,11 @@ int lfd_debug_runs(const lfd_lowpass_plan *p, int64_t *run_ks, int *run_len, int
     std::memcpy(run_const, &p->rc, rc_bytes);
   }
   return LFD_OK;
+}
+
+int lfd_lowpass_last_scan(const lfd_lowpass_plan *p) {
+  if (!p) return fail(LFD_EINVAL, "plan is NULL");
+  return p->last_scan;
 }
 
 int lfd_lowpass_last_kernel(const lfd_lowpass_plan *p) {
@@ -2070,7 +2083,7 @@ int lfd_sosfiltfilt_last_timing(float *ms_functionals, float *ms_scan, float *ms
 
 int lfd_interp_linear_f64(const double *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
                           int64_t s_t, const int64_t *lo_dev, const double *w_dev,
-                          int64_t n_out, float *y, int64_t ys_ch, int64_t ys_t,
+                          int64_t n_out, double *y, int64_t ys_ch, int64_t ys_t,
                           void *stream) {
   if (n_ch < 1 || n_out < 0) return fail(LFD_EINVAL, "bad sizes");
   if (n_out == 0) return LFD_OK;
@@ -2081,7 +2094,7 @@ int lfd_interp_linear_f64(const double *x, int64_t n_ch, int64_t n_t, int64_t s_
 
 int lfd_sos_filtfilt_resample_f32(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch,
                                   int64_t s_t, const double *sos, int n_sec, int padlen,
-                                  const int64_t *lo, const double *w, int64_t n_out, float *y,
+                                  const int64_t *lo, const double *w, int64_t n_out, double *y,
                                   int64_t ys_ch, int64_t ys_t, void *stream) {
   if (n_out < 1) return LFD_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -318,8 +318,9 @@ hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const 
                                const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
                                double *TR, double *CR, const int *slot_chunk, int n_off, const RunConst *rc_off,
-                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st,
-                               const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr);
+                               const ChunkGeom *cg_off, double *y, int64_t ys_ch, int64_t y_off, hipStream_t st,
+                               const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr,
+                               int *scan_used = nullptr);
 hipError_t launch_fold_runs(const double *F, const BlockGeom &g, const RunGeom &rg, double *Y0,
                             double *AG, hipStream_t st);
 // Run-mode scan.  With TR / CR / slot_chunk (per run slot: its chunk) the
@@ -331,10 +332,10 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg_dev, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
-                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR = nullptr,
+                                  double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR = nullptr,
                                   double *CR = nullptr, const int *slot_chunk = nullptr,
                                   const SegGeom *seg = nullptr, int seg_max = 0, double *SC = nullptr,
-                                  const SegGeom *seg_fu = nullptr, int nw_fu = 0);
+                                  const SegGeom *seg_fu = nullptr, int nw_fu = 0, int *scan_used = nullptr);
 hipError_t launch_block_functionals(int n_sec, bool fir32, const float *x, int64_t s_ch,
                                     int64_t s_t, const BlockGeom &g,
                                     const BlockConst &kc, double *F,
@@ -343,7 +344,7 @@ hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch
                              int64_t s_t, const BlockGeom &g, int padlen,
                              const ScanConst &sc, const ChunkGeom *cg_dev,
                              int64_t n_chunks, const double *F, double *SF,
-                             double *TP, int64_t tp_len, float *y,
+                             double *TP, int64_t tp_len, double *y,
                              int64_t ys_ch, int64_t ys_t, hipStream_t st);
 hipError_t launch_sosfiltfilt(int n_sec, const float *x, int64_t n_ch,
                               int64_t n_t, int64_t s_ch, int64_t s_t,
@@ -352,7 +353,7 @@ hipError_t launch_sosfiltfilt(int n_sec, const float *x, int64_t n_ch,
                               int64_t ys_t, hipStream_t st);
 hipError_t launch_interp_linear(const double *x, int64_t n_ch, int64_t n_t,
                                 int64_t s_ch, int64_t s_t, const int64_t *lo,
-                                const double *w, int64_t n_out, float *y,
+                                const double *w, int64_t n_out, double *y,
                                 int64_t ys_ch, int64_t ys_t, hipStream_t st);
 hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
                                int64_t s_ch, int64_t s_t, int64_t W, int64_t S,
@@ -374,17 +375,17 @@ struct GridGen {
 };
 // the same blend from a slot-major scratch tmp[slot * n_ch + ch] (one-pass
 // lattice plans), LDS-tiled so that reads and writes are both coalesced
-hipError_t launch_blend_grid_sm(const float *tmp, int64_t n_ch, const int64_t *bj, const int64_t *bi,
-                                const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+hipError_t launch_blend_grid_sm(const double *tmp, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                                const double *bw, int64_t nb, double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
                                 const GridGen &gen);
-hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
-                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+hipError_t launch_blend_grid(const double *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                             const double *bw, int64_t nb, double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
                              const GridGen &gen = GridGen{});
 // lfd_lowpass_execute with a generated grid (a lattice plan's weights from
 // `gen`; the stream caches lattice plans by structure).  Other plans ignore it.
 // scan_stream (lfd_lowpass_execute_split): the scan and outputs there after
 // the block pass (an event); nullptr = everything on `stream`.
-int lowpass_execute_gen(const ::lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, float *y,
+int lowpass_execute_gen(const ::lfd_lowpass_plan *p, const float *x, int64_t s_ch, int64_t s_t, double *y,
                         int64_t ys_ch, int64_t ys_t, void *workspace, void *stream, const GridGen &gen,
                         void *scan_stream = nullptr);
 // dst[c * dp + r] = src[r * sp + c] for r < n_rows, c < n_cols.

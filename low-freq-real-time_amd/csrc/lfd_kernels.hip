@@ -633,7 +633,7 @@ __device__ __forceinline__ void scan_head(const float *__restrict__ xc, int64_t 
 template <int NS>
 __device__ __forceinline__ void scan_tail(const float *__restrict__ xc, int64_t s_t, const ChunkGeom &G, int E,
                                           const SeqR<NS> &R, const ScanConst &sc, double (&S)[2 * NS],
-                                          double *__restrict__ tp, int64_t tp_stride, float *__restrict__ y,
+                                          double *__restrict__ tp, int64_t tp_stride, double *__restrict__ y,
                                           int64_t ch, int64_t ys_ch, int64_t ys_t, double (&T)[2 * NS],
                                           bool store = true, double *yret = nullptr) {
   constexpr int J = 2 * NS;
@@ -693,7 +693,7 @@ __device__ __forceinline__ void scan_tail(const float *__restrict__ xc, int64_t 
         if (yret)
           *yret = yv;  // (k_scan_fused's zero-state edge: the caller adds the state part)
         else if (store)
-          y[ch * ys_ch + G.tail_out_j * ys_t] = (float)yv;
+          y[ch * ys_ch + G.tail_out_j * ys_t] = yv;
       }
     }
 #pragma unroll
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen,
     const ScanConst sc, const ChunkGeom *__restrict__ cgs, int64_t n_chunks,
     const double *__restrict__ F, double *__restrict__ SF, double *__restrict__ TP,
-    int64_t tp_len, float *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
+    int64_t tp_len, double *__restrict__ y, int64_t ys_ch, int64_t ys_t, RunGeom rg,
     const double *__restrict__ Y0, double *__restrict__ TR = nullptr, double *__restrict__ CR = nullptr,
     double *__restrict__ SC = nullptr) {
   constexpr int N = 2 * NS;
@@ -745,7 +745,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
   // run-mode output staging: a wave's 64 channels x one run's <= 8 outputs,
   // written back as 8 rows x 8 consecutive samples per store instruction
   // instead of 64 scattered 4-B stores (0.2 ms of the cfg3 scan)
-  __shared__ float outs[RUNS ? 4 : 1][64][RUN_R + 1];
+  __shared__ double outs[RUNS ? 4 : 1][64][RUN_R + 1];
   if constexpr (RUNS) {
     // the fields this scan reads: PhiFp, PhiRp, C (+ A, B for in-chain
     // outputs) and KfH — not the whole 12 KB RunConst (a 64-thread group of
@@ -956,11 +956,11 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
 #pragma unroll
         for (int i = 0; i < N; ++i) tr[i * SF_ISTRIDE] = T[i];
       }
-      float ov[RUN_R];
+      double ov[RUN_R];
 #pragma unroll
       for (int pp = 0; pp < RUN_R; ++pp) {
         const int64_t k = ks + pp;
-        ov[pp] = 0.f;
+        ov[pp] = 0.0;
         if (DEFER || pp >= len || !is_out(k)) continue;
         double acc = cur.y0[pp] + (k == G.kb ? corr[2 * N] : 0.0);
         const double *A = rc.A[len][pp];
@@ -970,11 +970,11 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
           acc = fma(A[j], sin[j], acc);
           acc = fma(B[j], T[j], acc);
         }
-        ov[pp] = (float)acc;
+        ov[pp] = acc;
         if (!coal) y[ch * ys_ch + out_j(k) * ys_t] = ov[pp];
       }
       if (coal && !DEFER) {
-        float(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
+        double(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
 #pragma unroll
         for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -983,11 +983,11 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         const int e = lane & 7;
         const int64_t k = ks + e;
         const bool ok = e < len && is_out(k);
-        float *yb = y + ch_w * ys_ch + (ok ? out_j(k) : 0) * ys_t;
+        double *yb = y + ch_w * ys_ch + (ok ? out_j(k) : 0) * ys_t;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
           const int row = m * 8 + (lane >> 3);
-          const float v = wl[row][e];
+          const double v = wl[row][e];
           if (ok) yb[row * ys_ch] = v;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1025,7 +1025,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         acc = fma(sc.H0[j], T[j], acc);
         acc = fma(sc.G0[j], sfv[j], acc);
       }
-      y[ch * ys_ch + out_j(k) * ys_t] = (float)acc;
+      y[ch * ys_ch + out_j(k) * ys_t] = acc;
     }
     double nr[N];
 #pragma unroll
@@ -2124,7 +2124,7 @@ __global__ __launch_bounds__(256) void k_sosfiltfilt_full(
 __global__ __launch_bounds__(256) void k_interp_linear(
     const double *__restrict__ x, int64_t n_ch, int64_t n_t, int64_t s_ch,
     int64_t s_t, const int64_t *__restrict__ lo, const double *__restrict__ w,
-    int64_t n_out, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+    int64_t n_out, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_ch * n_out) return;
   const int64_t j = i % n_out, ch = i / n_out;
@@ -2132,7 +2132,7 @@ __global__ __launch_bounds__(256) void k_interp_linear(
   const double a = x[ch * s_ch + l * s_t];
   double v = a;
   if (w[j] != 0.0) v = fma(x[ch * s_ch + (l + 1) * s_t] - a, w[j], a);
-  y[ch * ys_ch + j * ys_t] = (float)v;
+  y[ch * ys_ch + j * ys_t] = v;
   (void)n_t;
 }
 
@@ -3934,12 +3934,12 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
                                                      const int *__restrict__ slot_chunk,
                                                      const double *__restrict__ Y0, const double *__restrict__ SR,
                                                      const double *__restrict__ TR, const double *__restrict__ CR,
-                                                     float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+                                                     double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = RUN_N;
   // only the output constants A[len][p], B[d] (2.5 KB; the whole RunConst
   // is 12 KB, and a 1,250-channel shard launches ~2,200 of these groups)
   __shared__ double sA[RUN_R + 1][RUN_R][4], sB[RUN_R][4];
-  __shared__ float outs[4][64][RUN_R + 1];
+  __shared__ double outs[4][64][RUN_R + 1];
   {
     const double *srcA = &rg.rc->A[0][0][0], *srcB = &rg.rc->B[0][0];
     for (int i = threadIdx.x; i < (RUN_R + 1) * RUN_R * 4; i += blockDim.x) (&sA[0][0][0])[i] = srcA[i];
@@ -3974,11 +3974,11 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
   }
   const double *y0b = Y0 + ((chc >> 4) * g.nb) * 16 + (chc & 15);
   const double cr = CR[c * (n_c64 * 64) + chc];
-  float ov[RUN_R];
+  double ov[RUN_R];
 #pragma unroll
   for (int pp = 0; pp < RUN_R; ++pp) {
     const int64_t k = ks + pp;
-    ov[pp] = 0.f;
+    ov[pp] = 0.0;
     if (pp >= len || !is_out(k)) continue;
     double acc = y0b[k * 16] + (k == G.kb ? cr : 0.0);
     const double *A = sA[len][pp];
@@ -3988,10 +3988,10 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
       acc = fma(A[i], sin[i], acc);
       acc = fma(B[i], tin[i], acc);
     }
-    ov[pp] = (float)acc;
+    ov[pp] = acc;
   }
   if (c64 * 64 + 63 < g.n_ch) {
-    float(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
+    double(*wl)[RUN_R + 1] = outs[(threadIdx.x >> 6) & 3];
 #pragma unroll
     for (int pp = 0; pp < RUN_R; ++pp) wl[lane][pp] = ov[pp];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -4000,11 +4000,11 @@ __global__ __launch_bounds__(256) void k_run_outputs(BlockGeom g, const ChunkGeo
     const int e = lane & 7;
     const int64_t k = ks + e;
     const bool ok = e < len && is_out(k);
-    float *yb = y + (c64 * 64) * ys_ch + (ok ? out_j(k) : 0) * ys_t;
+    double *yb = y + (c64 * 64) * ys_ch + (ok ? out_j(k) : 0) * ys_t;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int row = m * 8 + (lane >> 3);
-      const float v = wl[row][e];
+      const double v = wl[row][e];
       if (ok) yb[row * ys_ch] = v;
     }
   } else if (valid) {
@@ -4324,7 +4324,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
     const float *__restrict__ x, int64_t s_ch, int64_t s_t, BlockGeom g, int padlen, const ScanConst sc,
     const ChunkGeom *__restrict__ cgs, int64_t n_chunks, RunGeom rg, const SegGeom *__restrict__ sgs,
     const double *__restrict__ Y0, const double *__restrict__ AG, double *__restrict__ SR,
-    double *__restrict__ TR, double *__restrict__ TP, float *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
+    double *__restrict__ TR, double *__restrict__ TP, double *__restrict__ y, int64_t ys_ch, int64_t ys_t) {
   constexpr int N = RUN_N, NF = 2 * N + 1, SR_ = FU_SEGR;
 #ifdef LFD_DIAG
   // phase stamps of every wave, 100 MHz s_memrealtime
@@ -4347,7 +4347,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
   __shared__ RunConst rcs;
   __shared__ double Ps[FU_SEG][16], Qs[FU_SEG][16];
   __shared__ double aggf[FU_SEG][N][16], aggb[FU_SEG][N][16], hS[N][16], tT[N][16], corr[NF][16], tY[16];
-  __shared__ float otile[4][64][RUN_R + 1];  // output staging per wave
+  __shared__ double otile[4][64][RUN_R + 1];  // output staging per wave
   __shared__ int64_t omk[4][64];             // its run's first block
   __shared__ int oml[4][64];                 // its run's length (0: nothing to store)
   const int64_t n_cg = (g.n_ch + 15) / 16;
@@ -4535,7 +4535,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
         double yv = tY[col];
 #pragma unroll
         for (int j = 0; j < N; ++j) yv = fma(tm[j], S[j], yv);
-        y[ch * ys_ch + G.tail_out_j * ys_t] = (float)yv;
+        y[ch * ys_ch + G.tail_out_j * ys_t] = yv;
       }
     } else {
       scan_tail<2>(xc, s_t, G, padlen, R, sc, S, TP + c * g.n_ch + chc, n_chunks * g.n_ch, y, ch, ys_ch, ys_t, T,
@@ -4598,7 +4598,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
   // so a store instruction writes 8 row pieces of 32 B (one L2 request each)
   // instead of 64 scattered 4-B lanes
   const int wv = threadIdx.x >> 6, ln64 = threadIdx.x & 63;
-  float(*tile)[RUN_R + 1] = otile[wv];
+  double(*tile)[RUN_R + 1] = otile[wv];
   double ecur[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) ecur[i] = er[SR_ - 1][i];
@@ -4615,7 +4615,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
 #pragma unroll
     for (int pp = 0; pp < RUN_R; ++pp) {
       const int64_t k = ks + pp;
-      float o = 0.f;
+      double o = 0.0;
       if (pp < ln && is_out(k)) {
         double acc = ycur[pp] + (k == G.kb ? crk : 0.0);
         const double *A = rcs.A[ln][pp];
@@ -4625,7 +4625,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
           acc = fma(A[j], sin[u][j], acc);
           acc = fma(B[j], T[j], acc);
         }
-        o = (float)acc;
+        o = acc;
       }
       tile[ln64][pp] = o;
     }
@@ -4661,7 +4661,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_fused(
 hipError_t launch_scan_fused(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
                              const ScanConst &sc, const ChunkGeom *cg, int64_t n_chunks, const RunGeom &rg,
                              const SegGeom *seg_fu, const double *Y0, const double *AG, double *SR, double *TR,
-                             double *TP, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
+                             double *TP, double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st) {
   const unsigned nwg = (unsigned)(n_chunks * ((g.n_ch + 15) / 16));
 #ifdef LFD_DIAG
   {
@@ -4714,7 +4714,7 @@ hipError_t launch_scan_fused(const float *x, int64_t s_ch, int64_t s_t, const Bl
 static hipError_t launch_seg_scan(const float *x, int64_t s_ch, int64_t s_t, const BlockGeom &g, int padlen,
                                   const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                   const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
-                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR, double *CR,
+                                  double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR, double *CR,
                                   const SegGeom *seg, int seg_max, double *SC) {
   const int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
   const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
@@ -4746,9 +4746,11 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
                                   int padlen, const ScanConst &sc, const RunGeom &rg,
                                   const ChunkGeom *cg, int64_t n_chunks, const double *Y0,
                                   const double *AG, double *SR, double *TP, int64_t tp_len,
-                                  float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR,
+                                  double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st, double *TR,
                                   double *CR, const int *slot_chunk, const SegGeom *seg, int seg_max, double *SC,
-                                  const SegGeom *seg_fu, int nw_fu) {
+                                  const SegGeom *seg_fu, int nw_fu, int *scan_used) {
+  int scan_dummy = 0;
+  if (!scan_used) scan_used = &scan_dummy;
   // deferred outputs (k_run_outputs) when the scan has few (chunk, channel)
   // threads and is latency-bound: 1,250 ch x 7 chunks (an 8-GPU shard of
   // cfg3) 0.247 -> 0.152 ms, 2,500 ch 0.263 -> 0.191, 5,000 ch equal, 10,000
@@ -4756,7 +4758,9 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   // run chains (dt = 10 s at 1 kHz: ~300 runs per chunk, 0.79 -> 0.67 ms);
   // option LFD_OPT_SCAN_DEFER = 1 / 2 forces in-chain / deferred outputs
   bool defer = n_chunks * g.n_ch < 40000 || rg.n_sr >= 128 * n_chunks;
-  if (const int64_t o = option(LFD_OPT_SCAN_DEFER)) defer = o == 2;
+  // (option 1 / 2 force in-chain / deferred outputs; 3 / 4 fall back to the
+  // default choice when their segment tables do not fit the plan)
+  if (const int64_t o = option(LFD_OPT_SCAN_DEFER); o == 1 || o == 2) defer = o == 2;
 #ifdef LFD_DIAG
   static int diag = -1, threads_ab = 256;
   if (diag < 0) {
@@ -4779,9 +4783,11 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   // profiles/r05_scan_fused.txt)
   const int64_t o_scan = option(LFD_OPT_SCAN_DEFER);
   const bool fused_fits = n_chunks * ((g.n_ch + 15) / 16) <= 3 * (int64_t)cu_count();
-  if (seg_fu && nw_fu == FU_SEG && TR && (o_scan == 4 || (o_scan == 0 && fused_fits)))
+  if (seg_fu && nw_fu == FU_SEG && TR && (o_scan == 4 || (o_scan == 0 && fused_fits))) {
+    *scan_used = LFD_SCAN_FUSED;
     return launch_scan_fused(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0, AG, SR, TR, TP, y, ys_ch,
                              ys_t, st);
+  }
   // segmented chains (option scan_defer = 3, or automatically for long chains
   // on few threads: >= 128 runs per chunk and < 40,000 (chunk, channel)
   // threads — the 3 kHz lattice line's state scan 0.42 -> 0.31 ms; with
@@ -4789,8 +4795,10 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   // scan is faster, 0.60 vs 0.72 ms)
   const int64_t o_defer = option(LFD_OPT_SCAN_DEFER);
   const bool segm = seg && SC && seg_max >= 1 && TR && CR && slot_chunk &&
-                    (o_defer == 3 || (o_defer == 0 && n_chunks * g.n_ch < 40000 && rg.n_sr >= 128 * n_chunks));
+                    (o_defer == 3 || ((o_defer == 0 || o_defer == 4) && n_chunks * g.n_ch < 40000 &&
+                                      rg.n_sr >= 128 * n_chunks));
   if (segm) {
+    *scan_used = LFD_SCAN_SEGMENTED;
     hipError_t e = launch_seg_scan(x, s_ch, s_t, g, padlen, sc, rg, cg, n_chunks, Y0, AG, SR, TP, tp_len, y, ys_ch,
                                    ys_t, st, TR, CR, seg, seg_max, SC);
     if (e != hipSuccess) return e;
@@ -4799,6 +4807,7 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     return hipGetLastError();
   }
   if (TR && CR && slot_chunk && defer) {
+    *scan_used = LFD_SCAN_DEFERRED;
     // narrow shards: 64-thread workgroups (one wave per CU instead of four
     // sharing one): 1,250 channels 0.150 -> 0.126 ms, bit-identical
     // (profiles/r03_ab_scan_narrow.txt; A/B knob LFD_SCAN_DEFER_THREADS)
@@ -4829,6 +4838,7 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   threads = threads_ab;
 #endif
   const unsigned nb = nblk(n_chunks * g.n_ch, threads);
+  *scan_used = LFD_SCAN_IN_CHAIN;
   k_chunk_scan<2, true><<<nb, threads, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                             tp_len, y, ys_ch, ys_t, rg, Y0);
   return hipGetLastError();
@@ -4846,7 +4856,7 @@ __global__ __launch_bounds__(256) void k_lat_outputs(BlockGeom g, const ChunkGeo
                                                      int n_off, RunGeom rg, const int *__restrict__ slot_chunk,
                                                      const RunConst *__restrict__ rc_off, const double *__restrict__ Y0,
                                                      const double *__restrict__ SR, const double *__restrict__ TR,
-                                                     float *__restrict__ tmp, int64_t n_g) {
+                                                     double *__restrict__ tmp, int64_t n_g) {
   constexpr int N = RUN_N;
   __shared__ double sA[LAT_MAX_OFF][RUN_R + 1][4], sB[LAT_MAX_OFF][RUN_R + 1][4];
   for (int i = threadIdx.x; i < n_off * (RUN_R + 1) * 4; i += blockDim.x) {
@@ -4887,7 +4897,7 @@ __global__ __launch_bounds__(256) void k_lat_outputs(BlockGeom g, const ChunkGeo
       acc = fma(sA[d][len][i], sin[i], acc);
       acc = fma(sB[d][len][i], tin[i], acc);
     }
-    if (valid) tmp[((int64_t)d * n_g + jo) * g.n_ch + ch] = (float)acc;
+    if (valid) tmp[((int64_t)d * n_g + jo) * g.n_ch + ch] = acc;
   }
 }
 
@@ -4896,19 +4906,19 @@ __global__ __launch_bounds__(256) void k_lat_outputs(BlockGeom g, const ChunkGeo
 // workgroup = 64 blend points x 64 channels; reads of tmp rows (64 channels)
 // and writes of y rows (64 points) both coalesced through an LDS tile.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_blend_grid_sm(const float *__restrict__ tmp, int64_t n_ch,
+__global__ __launch_bounds__(256) void k_blend_grid_sm(const double *__restrict__ tmp, int64_t n_ch,
                                                        const int64_t *__restrict__ bj, const int64_t *__restrict__ bi,
-                                                       const double *__restrict__ bw, int64_t nb, float *__restrict__ y,
+                                                       const double *__restrict__ bw, int64_t nb, double *__restrict__ y,
                                                        int64_t ys_ch, int64_t ys_t, GridGen gen) {
-  __shared__ float tile[64][65];
+  __shared__ double tile[64][65];
   const int64_t i0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int ii = ty; ii < 64; ii += 4) {
     const int64_t i = i0 + ii, ch = c0 + tx;
-    float v = 0.f;
+    double v = 0.0;
     if (i < nb && ch < n_ch) {
       const int64_t ia = bi[2 * i], ib = bi[2 * i + 1];
-      double a = (double)tmp[ia * n_ch + ch];
+      double a = tmp[ia * n_ch + ch];
       if (ib >= 0) {
         double wv;
         if (gen.dts > 0) {
@@ -4919,9 +4929,9 @@ __global__ __launch_bounds__(256) void k_blend_grid_sm(const float *__restrict__
         } else {
           wv = bw[i];
         }
-        a = fma(wv, (double)tmp[ib * n_ch + ch] - a, a);
+        a = fma(wv, tmp[ib * n_ch + ch] - a, a);
       }
-      v = (float)a;
+      v = a;
     }
     tile[ii][tx] = v;
   }
@@ -4935,8 +4945,8 @@ __global__ __launch_bounds__(256) void k_blend_grid_sm(const float *__restrict__
   }
 }
 
-hipError_t launch_blend_grid_sm(const float *tmp, int64_t n_ch, const int64_t *bj, const int64_t *bi,
-                                const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+hipError_t launch_blend_grid_sm(const double *tmp, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                                const double *bw, int64_t nb, double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
                                 const GridGen &gen) {
   if (nb <= 0 || n_ch <= 0) return hipSuccess;
   if ((n_ch + 63) / 64 > 65535) return hipErrorInvalidValue;
@@ -4949,18 +4959,19 @@ hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const 
                                const ScanConst &sc, const RunGeom &rg, const ChunkGeom *cg, int64_t n_chunks,
                                const double *Y0, const double *AG, double *SR, double *TP, int64_t tp_len,
                                double *TR, double *CR, const int *slot_chunk, int n_off, const RunConst *rc_off,
-                               const ChunkGeom *cg_off, float *y, int64_t ys_ch, int64_t y_off, hipStream_t st,
-                               const SegGeom *seg, int seg_max, double *SC) {
+                               const ChunkGeom *cg_off, double *y, int64_t ys_ch, int64_t y_off, hipStream_t st,
+                               const SegGeom *seg, int seg_max, double *SC, int *scan_used) {
   if (n_off < 1 || n_off > LAT_MAX_OFF || !TR || !CR || !slot_chunk) return hipErrorInvalidValue;
   const int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
   const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
   const int64_t o_defer = option(LFD_OPT_SCAN_DEFER);
   if (seg && SC && seg_max >= 1 &&
-      (o_defer == 3 || (o_defer == 0 && n_chunks * g.n_ch < 40000 && rg.n_sr >= 128 * n_chunks))) {
+      (o_defer == 3 || (o_defer != 1 && o_defer != 2 && n_chunks * g.n_ch < 40000 && rg.n_sr >= 128 * n_chunks))) {
+    if (scan_used) *scan_used = LFD_SCAN_SEGMENTED;
     const hipError_t e = launch_seg_scan(x, s_ch, s_t, g, padlen, sc, rg, cg, n_chunks, Y0, AG, SR, TP, tp_len, y,
                                          ys_ch, 1, st, TR, CR, seg, seg_max, SC);
     if (e != hipSuccess) return e;
-  } else if (rg.n_sr >= 128 * n_chunks)
+  } else if ((scan_used ? (*scan_used = LFD_SCAN_DEFERRED) : 0), rg.n_sr >= 128 * n_chunks)
     k_chunk_scan<2, true, true, 16, 8><<<nb, dthr, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
                                                             tp_len, y, ys_ch, 1, rg, Y0, TR, CR);
   else
@@ -4978,7 +4989,7 @@ hipError_t launch_lattice_scan(const float *x, int64_t s_ch, int64_t s_t, const 
 hipError_t launch_chunk_scan(int n_sec, bool fir32, const float *x, int64_t s_ch, int64_t s_t,
                              const BlockGeom &g, int padlen, const ScanConst &sc,
                              const ChunkGeom *cg, int64_t n_chunks, const double *F, double *SF,
-                             double *TP, int64_t tp_len, float *y, int64_t ys_ch, int64_t ys_t,
+                             double *TP, int64_t tp_len, double *y, int64_t ys_ch, int64_t ys_t,
                              hipStream_t st) {
   (void)fir32;
   const unsigned nb = nblk(n_chunks * g.n_ch, 256);
@@ -5156,7 +5167,7 @@ hipError_t launch_sosfiltfilt(int n_sec, const float *x, int64_t n_ch,
 
 hipError_t launch_interp_linear(const double *x, int64_t n_ch, int64_t n_t,
                                 int64_t s_ch, int64_t s_t, const int64_t *lo,
-                                const double *w, int64_t n_out, float *y,
+                                const double *w, int64_t n_out, double *y,
                                 int64_t ys_ch, int64_t ys_t, hipStream_t st) {
   k_interp_linear<<<nblk(n_ch * n_out, 256), 256, 0, st>>>(
       x, n_ch, n_t, s_ch, s_t, lo, w, n_out, y, ys_ch, ys_t);
@@ -5677,16 +5688,16 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
 // w = (rel - floor(rel / dts) dts) / dts — the host's formula (lfd_stream.cpp
 // run_chunks), so a stream's lattice plan serves every push whose grid has
 // the same lattice structure, whatever its fractions.
-__global__ __launch_bounds__(256) void k_blend_grid(const float *__restrict__ tmp, int64_t T, int64_t n_ch,
+__global__ __launch_bounds__(256) void k_blend_grid(const double *__restrict__ tmp, int64_t T, int64_t n_ch,
                                                     const int64_t *__restrict__ bj, const int64_t *__restrict__ bi,
-                                                    const double *__restrict__ bw, int64_t nb, float *__restrict__ y,
+                                                    const double *__restrict__ bw, int64_t nb, double *__restrict__ y,
                                                     int64_t ys_ch, int64_t ys_t, GridGen gen) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nb * n_ch) return;
   const int64_t ch = idx / nb, i = idx - ch * nb;
-  const float *row = tmp + ch * T;
+  const double *row = tmp + ch * T;
   const int64_t ia = bi[2 * i], ib = bi[2 * i + 1];
-  double v = (double)row[ia];
+  double v = row[ia];
   if (ib >= 0) {
     double wv;
     if (gen.dts > 0) {
@@ -5697,13 +5708,13 @@ __global__ __launch_bounds__(256) void k_blend_grid(const float *__restrict__ tm
     } else {
       wv = bw[i];
     }
-    v = fma(wv, (double)row[ib] - v, v);
+    v = fma(wv, row[ib] - v, v);
   }
-  y[ch * ys_ch + bj[i] * ys_t] = (float)v;
+  y[ch * ys_ch + bj[i] * ys_t] = v;
 }
 
-hipError_t launch_blend_grid(const float *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
-                             const double *bw, int64_t nb, float *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
+hipError_t launch_blend_grid(const double *tmp, int64_t T, int64_t n_ch, const int64_t *bj, const int64_t *bi,
+                             const double *bw, int64_t nb, double *y, int64_t ys_ch, int64_t ys_t, hipStream_t st,
                              const GridGen &gen) {
   if (nb <= 0 || n_ch <= 0) return hipSuccess;
   k_blend_grid<<<nblk(nb * n_ch, 256), 256, 0, st>>>(tmp, T, n_ch, bj, bi, bw, nb, y, ys_ch, ys_t, gen);

@@ -123,7 +123,7 @@ struct lfd_stream {
   int pin_i = 0;
   float *stage = nullptr;
   size_t stage_bytes = 0;
-  float *out[2] = {};
+  double *out[2] = {};
   size_t out_bytes[2] = {0, 0};
   int out_i = 0;
   lfd_stream_output last{};
@@ -342,8 +342,8 @@ int run_chunks(lfd_stream *s, int64_t t_grid0, const Row *rows, size_t n_rows) {
     return LFD_OK;
   }
   LFD_TRY(ensure_dev(reinterpret_cast<void **>(&s->out[oi]), &s->out_bytes[oi],
-                     sizeof(float) * (size_t)n_ch * (size_t)n_out, s->s_comp));
-  float *y = s->out[oi];
+                     sizeof(double) * (size_t)n_ch * (size_t)n_out, s->s_comp));
+  double *y = s->out[oi];
   const float *x = s->arena[s->cur] + x0;
   lfd_lowpass_plan *plan = nullptr;
   // grid weights from the grid's integer times on device (lattice plans):
@@ -609,7 +609,7 @@ int lfd_stream_last_chunks(const lfd_stream *s, int64_t *counts, int64_t max_chu
   return LFD_OK;
 }
 
-int lfd_stream_fetch(lfd_stream *s, float *y, int64_t ys_ch, int64_t ys_t) {
+int lfd_stream_fetch(lfd_stream *s, double *y, int64_t ys_ch, int64_t ys_t) {
   if (!s) return fail(LFD_EINVAL, "stream is NULL");
   if (s->dry) return LFD_OK;
   DeviceGuard g(s->device);
@@ -619,13 +619,13 @@ int lfd_stream_fetch(lfd_stream *s, float *y, int64_t ys_ch, int64_t ys_t) {
   const int64_t n_ch = s->cfg.n_ch, n = s->last.n_out;
   LFD_HIP(hipEventSynchronize(s->ev_out[s->out_i]));
   if (ys_t == 1 && (n_ch == 1 || ys_ch >= n)) {
-    LFD_HIP(hipMemcpy2DAsync(y, sizeof(float) * (n_ch == 1 ? n : ys_ch), s->last.y, sizeof(float) * n,
-                             sizeof(float) * n, n_ch, hipMemcpyDeviceToHost, s->s_comp));
+    LFD_HIP(hipMemcpy2DAsync(y, sizeof(double) * (n_ch == 1 ? n : ys_ch), s->last.y, sizeof(double) * n,
+                             sizeof(double) * n, n_ch, hipMemcpyDeviceToHost, s->s_comp));
     LFD_HIP(hipStreamSynchronize(s->s_comp));
     return LFD_OK;
   }
-  std::vector<float> tmp((size_t)n_ch * n);
-  LFD_HIP(hipMemcpyAsync(tmp.data(), s->last.y, sizeof(float) * tmp.size(), hipMemcpyDeviceToHost, s->s_comp));
+  std::vector<double> tmp((size_t)n_ch * n);
+  LFD_HIP(hipMemcpyAsync(tmp.data(), s->last.y, sizeof(double) * tmp.size(), hipMemcpyDeviceToHost, s->s_comp));
   LFD_HIP(hipStreamSynchronize(s->s_comp));
   for (int64_t c = 0; c < n_ch; ++c)
     for (int64_t j = 0; j < n; ++j) y[c * ys_ch + j * ys_t] = tmp[c * n + j];

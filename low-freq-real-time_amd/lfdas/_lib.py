@@ -142,6 +142,7 @@ def load():
         "lfd_debug_plan_constants": ([vp, vp, sz, vp, sz, vp, sz], i32),
         "lfd_debug_block_taps": ([vp, vp, sz, P(i32), P(i64)], i32),
         "lfd_lowpass_last_kernel": ([vp], i32),
+        "lfd_lowpass_last_scan": ([vp], i32),
         "lfd_debug_runs": ([vp, vp, vp, i64, P(i64), vp, sz], i32),
         "lfd_sos_filtfilt_resample_f32": ([vp, i64, i64, i64, i64, vp, i32, i32,
                                            vp, vp, i64, vp, i64, i64, vp], i32),
@@ -189,7 +190,7 @@ EXPORTED = (
     "lfd_last_error", "lfd_version", "lfd_device_count", "lfd_set_timing", "lfd_set_option", "lfd_get_option",
     "lfd_lowpass_plan_create", "lfd_lowpass_plan_info", "lfd_lowpass_execute", "lfd_lowpass_execute_split",
     "lfd_lowpass_last_timing", "lfd_lowpass_timings", "lfd_lowpass_plan_destroy",
-    "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_debug_runs",
+    "lfd_debug_plan_constants", "lfd_debug_block_taps", "lfd_lowpass_last_kernel", "lfd_lowpass_last_scan", "lfd_debug_runs",
     "lfd_sos_filtfilt_resample_f32",
     "lfd_sosfiltfilt_workspace_bytes", "lfd_sosfiltfilt_f32", "lfd_sosfiltfilt_last_timing",
     "lfd_interp_linear_f64", "lfd_rolling_mean_f32", "lfd_fir_decimate_f32", "lfd_fir_decimate_last_kernel",

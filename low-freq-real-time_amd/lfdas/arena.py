@@ -18,6 +18,11 @@ while the 72 GB headline input is that size already (no difference).
 permitting; 288 GB per GPU).  The view keeps its allocation alive; freed, the
 block stays in torch's caching allocator, so the next buffer of the pool size
 reuses the same placement.  Smaller buffers are ordinary ``torch.empty``.
+
+It is OPT-IN (bench.py's sample buffers): the view's storage is the whole
+pool, so a caller that holds many such buffers at once, or serialises one,
+pays for the pool each time.  The library's own patch uploads
+(``proc.to_device_ct``) use right-sized buffers.
 """
 from __future__ import annotations
 

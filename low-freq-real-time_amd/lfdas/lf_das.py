@@ -280,7 +280,7 @@ class LFProc:
             nonlocal done
             if o.n_out == 0 and not o.chunk_counts:
                 return
-            y = st.fetch() if o.n_out else np.zeros((n_ch, 0), np.float32)
+            y = st.fetch() if o.n_out else np.zeros((n_ch, 0), np.float64)
             t = o.times_ns
             j = 0
             for cnt in o.chunk_counts:
@@ -290,7 +290,7 @@ class LFProc:
                         print(f"Processing patch {done} (Last portion of data)")
                     else:
                         print("Processing patch ", str(done))
-                seg = y[:, j:j + cnt].astype(np.float64)
+                seg = y[:, j:j + cnt]
                 coords = dict(coords0)
                 coords["time"] = t[j:j + cnt].astype("datetime64[ns]")
                 out = Patch(data=seg.T.copy() if tdim == 0 else seg, coords=coords, dims=p0.dims,
@@ -352,7 +352,7 @@ class LFProc:
     def process_time_range_device(self, bgtime, edtime):
         """``process_time_range`` without the host side: every chunk's
         decimated outputs stay in HBM.  Returns ``(y, times_ns, counts)``:
-        ``y`` a float32 (channel, time) device tensor holding the chunks'
+        ``y`` a float64 (channel, time) device tensor holding the chunks'
         outputs side by side (``counts[i]`` columns each, output times
         ``times_ns``), or None when the range is larger than the device
         budget (the caller then uses ``process_time_range``, which streams).
@@ -375,7 +375,7 @@ class LFProc:
 
     def _device_outputs(self, tg, sched, data_patch, dt):
         """Run ``sched``'s chunks over ``data_patch`` on the device: returns
-        (y, chunks) — y float32 (n_ch, len(tg)) in HBM (NaN outside the
+        (y, chunks) — y float64 (n_ch, len(tg)) in HBM (NaN outside the
         chunks' outputs), chunks ``(s0, s1, oa, ob)`` per chunk."""
         import torch
 
@@ -395,7 +395,7 @@ class LFProc:
             s0, s1 = S.select_range(t0, dt_ns, n, tg[a], tg[b])
             chunks.append((s0, s1, oa, ob))
         lo, w = S.grid_positions(t0, dt_ns, tg)
-        y = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float32, device=x.device)
+        y = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float64, device=x.device)
         try:
             plan = LowpassPlan(sos, n_ch, n, np.clip(lo, 0, n - 1), w, chunks, padlen)
             plan.execute(x, y, plan.alloc_workspace(x.device))
@@ -417,7 +417,7 @@ class LFProc:
                     print(f"Processing patch {i} (Last portion of data)")
                 else:
                     print("Processing patch ", str(i))
-            seg = yh[:, oa:ob].astype(np.float64)
+            seg = yh[:, oa:ob]
             data = seg.T.copy() if tdim == 0 else seg
             coords = dict(data_patch.coords.coord_map)
             coords["time"] = tg[oa:ob].astype("datetime64[ns]")

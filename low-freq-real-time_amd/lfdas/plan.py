@@ -107,10 +107,11 @@ class LowpassPlan:
 
     def execute(self, x, y, workspace, stream=None):
         """Run on device: ``x`` (n_ch, n_t) float32, ``y`` (n_ch, n_grid)
-        float32 (any strides), ``workspace`` >= workspace_bytes."""
+        float64 — SciPy's sosfiltfilt result dtype — (any strides),
+        ``workspace`` >= workspace_bytes."""
         import torch
         _require_cuda(x, "x", torch.float32)
-        _require_cuda(y, "y", torch.float32)
+        _require_cuda(y, "y", torch.float64)
         if tuple(x.shape) != (self.n_ch, self.n_t):
             raise ValueError(f"x shape {tuple(x.shape)} != plan {(self.n_ch, self.n_t)}")
         if tuple(y.shape) != (self.n_ch, self.n_grid):
@@ -129,7 +130,7 @@ class LowpassPlan:
         and the workspace is free once scan_stream has passed this call."""
         import torch
         _require_cuda(x, "x", torch.float32)
-        _require_cuda(y, "y", torch.float32)
+        _require_cuda(y, "y", torch.float64)
         if tuple(x.shape) != (self.n_ch, self.n_t):
             raise ValueError(f"x shape {tuple(x.shape)} != plan {(self.n_ch, self.n_t)}")
         if tuple(y.shape) != (self.n_ch, self.n_grid):
@@ -166,6 +167,12 @@ class LowpassPlan:
         k = self._lib.lfd_lowpass_last_kernel(self._h)
         return {1: "recurrence", 2: "mfma", 3: "mfma_runs", 4: "recurrence_fold",
                 5: "mfma_fold", 6: "mfma_runs_tm"}.get(k, "none")
+
+    def last_scan(self) -> str:
+        """Chunk scan of the last execute (``lfd_lowpass_last_scan``): "blocks"
+        (no run folding), "in_chain", "deferred", "segmented" or "fused"."""
+        k = self._lib.lfd_lowpass_last_scan(self._h)
+        return {0: "blocks", 1: "in_chain", 2: "deferred", 3: "segmented", 4: "fused"}.get(k, "none")
 
     def runs(self):
         """(run_ks, run_len, RunConst record) or None without run mode — testing hook."""
@@ -260,6 +267,12 @@ class LowpassPipeline:
         if self._done[j] is not None:
             self.block.wait_event(self._done[j])  # the scan that last read ws[j]
         self.plan.execute_split(x, y, self.ws[j], self.block, self.scan)
+        # the caching allocator must not hand x / y / ws[j] to another stream
+        # before the pipeline's streams are past them (an x freed by the caller,
+        # or the pipeline itself dropped, with batches in flight)
+        for t in (x, y, self.ws[j]):
+            t.record_stream(self.block)
+            t.record_stream(self.scan)
         ev = torch.cuda.Event()
         ev.record(self.scan)
         self._done[j] = ev
@@ -275,6 +288,14 @@ class LowpassPipeline:
     def synchronize(self):
         self.block.synchronize()
         self.scan.synchronize()
+
+    def __del__(self):  # pragma: no cover
+        # a dropped pipeline waits for its batches (its workspaces go back to
+        # the allocator with it)
+        try:
+            self.synchronize()
+        except Exception:
+            pass
 
 def set_timing(enable: bool, ring: int = 1):
     """HIP-event timing of executes; ``ring`` > 1 keeps the last ``ring``
@@ -318,13 +339,13 @@ def sosfiltfilt_last_timing_ms():
 
 
 def interp_device(yfull, lo, w, stream=None):
-    """Device gather ``y[:, lo] + w*(y[:, lo+1]-y[:, lo])`` → float32."""
+    """Device gather ``y[:, lo] + w*(y[:, lo+1]-y[:, lo])`` → float64."""
     import torch
     lib = load()
     lo_d = torch.as_tensor(np.ascontiguousarray(lo, dtype=np.int64), device=yfull.device)
     w_d = torch.as_tensor(np.ascontiguousarray(w, dtype=np.float64), device=yfull.device)
     n_ch, n_t = yfull.shape
-    out = torch.empty((n_ch, len(lo)), dtype=torch.float32, device=yfull.device)
+    out = torch.empty((n_ch, len(lo)), dtype=torch.float64, device=yfull.device)
     check(lib.lfd_interp_linear_f64(_ptr(yfull), n_ch, n_t, yfull.stride(0), yfull.stride(1),
                                     _ptr(lo_d), _ptr(w_d), len(lo), _ptr(out), out.stride(0),
                                     out.stride(1), _stream_ptr(stream)))
@@ -333,7 +354,7 @@ def interp_device(yfull, lo, w, stream=None):
 
 def filtfilt_resample_device(x, sos, lo, w, padlen: int = -1, stream=None):
     """One-shot ``pass_filter(...).interpolate(...)`` of one patch on device
-    (``lfd_sos_filtfilt_resample_f32``) → float32 (n_ch, n_out)."""
+    (``lfd_sos_filtfilt_resample_f32``) → float64 (n_ch, n_out)."""
     import torch
     _require_cuda(x, "x", torch.float32)
     lib = load()
@@ -341,7 +362,7 @@ def filtfilt_resample_device(x, sos, lo, w, padlen: int = -1, stream=None):
     lo = np.ascontiguousarray(lo, dtype=np.int64)
     w = np.ascontiguousarray(w, dtype=np.float64)
     n_ch, n_t = x.shape
-    y = torch.empty((n_ch, len(lo)), dtype=torch.float32, device=x.device)
+    y = torch.empty((n_ch, len(lo)), dtype=torch.float64, device=x.device)
     _count()
     check(lib.lfd_sos_filtfilt_resample_f32(
         _ptr(x), n_ch, n_t, x.stride(0), x.stride(1), sos.ctypes.data, sos.shape[0], int(padlen),

@@ -47,8 +47,9 @@ def to_device_ct(patch: Patch, device=None, dtype=None):
         if a.ndim != 2:
             raise ValueError("lfdas patches are 2-D (distance, time)")
         npdt = np.float32 if dtype == torch.float32 else np.float64
-        from .arena import device_samples
-        t = device_samples(a.shape, dtype=dtype, device=dev)  # (translation-friendly placement, lfdas.arena)
+        # (a right-sized buffer: lfdas.arena's pooled placement is opt-in, for
+        # callers that own their buffers' lifetime — bench.py's inputs)
+        t = torch.empty(a.shape, dtype=dtype, device=dev)
         t.copy_(torch.from_numpy(np.ascontiguousarray(a, dtype=npdt)))
     return t.permute(*perm)
 
@@ -189,12 +190,12 @@ class ChunkGroup:
             return False
         import torch
         x = to_device_ct(self.parent)
-        y = torch.empty((x.shape[0], len(lo)), dtype=torch.float32, device=x.device)
+        y = torch.empty((x.shape[0], len(lo)), dtype=torch.float64, device=x.device)
         plan.execute(x, y, plan.alloc_workspace(x.device))
         plan.close()
         yh = y.cpu().numpy()
         for r, (_, _, g0, g1) in zip(batch, chunks):
-            seg = yh[:, g0:g1].astype(np.float64)
+            seg = yh[:, g0:g1]
             r._result = seg.T.copy() if r.dims.index("time") == 0 else seg
         return True
 
@@ -222,7 +223,7 @@ class _GroupResample:
         from .plan import filtfilt_resample_device
         x = to_device_ct(self.window)
         y = filtfilt_resample_device(x, self.sos, self.lo, self.w, self.padlen)
-        return _from_ct(y, self.dims).astype(np.float64)
+        return _from_ct(y, self.dims)
 
     def materialize(self, patch: Patch):
         if self._result is None:

@@ -28,6 +28,15 @@ def channel_range(n_ch: int, world: int, rank: int):
     return c0, min(c0 + per, n_ch)
 
 
+def _grouped() -> bool:
+    """A torch.distributed process group is initialised (any world size)."""
+    try:
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized()
+    except ImportError:  # pragma: no cover
+        return False
+
+
 def _world(group=None):
     try:
         import torch.distributed as dist
@@ -82,7 +91,7 @@ def shard_spool(sp, world: int, rank: int):
 
 def lfproc_shard(sub, bgtime, edtime, params, device=None):
     """Default per-rank compute: LFProc on the rank's sub-spool (device plan,
-    no files).  Returns the chunks' outputs as ONE float32 (channel, time)
+    no files).  Returns the chunks' outputs as ONE float64 (channel, time)
     device tensor (``LFProc.process_time_range_device``), so the gather runs
     HBM to HBM; a range too large for the device budget streams through
     ``process_time_range`` and returns its output patches instead."""
@@ -98,7 +107,7 @@ def lfproc_shard(sub, bgtime, edtime, params, device=None):
 
 def _shard_block(outs, counts, n_local, tdim):
     """This rank's outputs as one (n_local, sum(counts)) tensor: a device
-    tensor from ``lfproc_shard`` as is (float32), output patches (an
+    tensor from ``lfproc_shard`` as is (float64), output patches (an
     injected ``run_shard``) side by side in their own dtype.  Raises on a
     wrong chunk count or shape, so the error agreement covers it."""
     import torch
@@ -126,13 +135,14 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
     with ``run_shard(sub_spool, bgtime, edtime, params)`` (default
     ``lfproc_shard``: the device plan), and rank 0 writes the reference's
     full-width files (``LFDAS_<t0>_<t1>.h5``, lf_das.py:230-232) into
-    ``output_folder``.  The decimated float32 outputs move HBM to HBM over
-    RCCL on backend "nccl" (through host memory on gloo):
+    ``output_folder``.  The decimated float64 outputs (SciPy's result dtype)
+    move HBM to HBM over RCCL on backend "nccl" (through host memory on gloo):
 
-    * ``gather=True`` (default): gathered to rank 0 only, the one rank that
-      writes; rank 0 returns the full-width patches (one device→host copy of
-      the full block, on rank 0 alone), every other rank its own block's;
-    * ``gather="all"``: all-gathered; every rank returns the full width;
+    * ``gather=True`` (default) or ``"all"``: all-gathered; every rank
+      returns the full-width patches;
+    * ``gather="root"``: gathered to rank 0 only, the one rank that writes;
+      rank 0 returns the full-width patches (one device→host copy of the
+      full block, on rank 0 alone), every other rank its own block's;
     * ``gather=False``: no collective; every rank returns its own block (and
       nothing is written unless the run has one rank).
 
@@ -162,31 +172,29 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
         if sub is not None:
             blk = _shard_block(run_shard(sub, bgtime, edtime, params), counts, n_local, tdim)
         else:
-            blk = torch.zeros((0, sum(counts)), dtype=torch.float32)
+            blk = torch.zeros((0, sum(counts)), dtype=torch.float64)
     except Exception as e:  # re-raised below, after every rank agreed
         err = e
-    if world > 1:
+    # (inside a process group the agreement and the gathers run at any world
+    # size, world 1 included: the same RCCL / gloo calls as at world N)
+    grouped = _grouped()
+    if grouped:
         import torch.distributed as dist
-        # one agreement for both: did any rank fail, and does any rank
-        # hold float64 outputs (an injected host compute) — every rank then
-        # gathers in that dtype
-        is64 = int(blk is not None and blk.dtype == torch.float64)
-        flag = torch.tensor([1 if err is not None else 0, is64], dtype=torch.int64, device=_comm_device(group))
+        # the agreement: did any rank fail (every rank then raises)
+        flag = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device=_comm_device(group))
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
         if int(flag[0].item()):
             raise err if err is not None else RuntimeError("process_time_range failed on another rank")
-        dtype = torch.float64 if int(flag[1].item()) else torch.float32
     elif err is not None:
         raise err
-    else:
-        dtype = blk.dtype
-    if gather not in (True, False, "all"):
-        raise ValueError('gather must be True (to rank 0), "all" or False')
+    dtype = torch.float64  # DASCore's output dtype (an injected run_shard may return float32 patches)
+    if gather not in (True, False, "all", "root"):
+        raise ValueError('gather must be True / "all" (all-gather), "root" (to rank 0) or False')
     full = None
-    if world > 1 and gather:
+    if grouped and gather:
         # HBM to HBM over RCCL (backend "nccl"); host tensors over gloo
         t = blk.to(device=_comm_device(group), dtype=dtype)
-        if gather == "all":
+        if gather is True or gather == "all":
             full = all_gather_channels(t, n_ch, group=group).cpu().numpy()
         else:
             g = gather_channels_to_root(t, n_ch, group=group)
@@ -200,7 +208,7 @@ def process_time_range_sharded(sp, bgtime, edtime, params=None, output_folder=No
     j = 0
     attrs = p0._attrs_wo_coords()
     for i, ((_, _, oa, ob), cnt) in enumerate(zip(sched, counts), start=1):
-        seg = full[:, j:j + cnt].astype(np.float64)  # DASCore's output dtype
+        seg = np.asarray(full[:, j:j + cnt], dtype=np.float64)  # DASCore's output dtype
         coords = dict(p0.coords.coord_map)
         coords["distance"] = dist_coords
         coords["time"] = tg[oa:ob].astype("datetime64[ns]")

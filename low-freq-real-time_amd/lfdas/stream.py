@@ -208,14 +208,14 @@ class LowpassStream:
                             [int(c) for c in counts[: n.value]], int(o.n_runs))
 
     def fetch(self, out: np.ndarray | None = None) -> np.ndarray:
-        """Wait for the last push and copy its outputs to host, (n_ch, n_out)."""
+        """Wait for the last push and copy its float64 outputs to host, (n_ch, n_out)."""
         o = self.last_output()
         if out is None:
-            out = np.empty((self.n_ch, o.n_out), np.float32)
-        if out.shape != (self.n_ch, o.n_out) or out.dtype != np.float32:
-            raise ValueError("out must be float32 (n_ch, n_out)")
-        check(self._lib.lfd_stream_fetch(self._h, out.ctypes.data, out.strides[0] // 4,
-                                         max(out.strides[1] // 4, 1)))
+            out = np.empty((self.n_ch, o.n_out), np.float64)
+        if out.shape != (self.n_ch, o.n_out) or out.dtype != np.float64:
+            raise ValueError("out must be float64 (n_ch, n_out)")
+        check(self._lib.lfd_stream_fetch(self._h, out.ctypes.data, out.strides[0] // 8,
+                                         max(out.strides[1] // 8, 1)))
         self._keep.clear()
         return out
 
@@ -278,7 +278,7 @@ class LowpassStream:
         for cnt in o.chunk_counts:
             if cnt <= 0:
                 continue
-            seg = y[:, j:j + cnt].astype(np.float64)
+            seg = y[:, j:j + cnt]
             coords = dict(patch.coords.coord_map)
             coords["time"] = times[j:j + cnt].astype("datetime64[ns]")
             out = Patch(data=seg.T.copy() if tax == 0 else seg, coords=coords, dims=patch.dims,

@@ -120,7 +120,8 @@ void plan_case(const double *sos, int n_sec, int64_t n_ch, int64_t n, int64_t sa
   }
   // execute without a device fails cleanly
   float dummy = 0.f;
-  EXPECT_FAIL(lfd_lowpass_execute(p, &dummy, n, 1, &dummy, L, 1, &dummy, nullptr));
+  double ydummy = 0.0;
+  EXPECT_FAIL(lfd_lowpass_execute(p, &dummy, n, 1, &ydummy, L, 1, &dummy, nullptr));
   lfd_lowpass_plan_destroy(p);
 }
 

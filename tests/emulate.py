@@ -98,7 +98,7 @@ def emulate(plan, x, padlen, fir32=True, k1="recurrence"):
     # ---------------- K2
     PhiF, PhiR, M = sc["PhiF"][:n, :n], sc["PhiR"][:n, :n], sc["M"][:n, :n]
     G0, H0, Kc = sc["G0"][:n], sc["H0"][:n], sc["Kc"][: 2 * n + 1, :J]
-    y = np.full((n_ch, plan.n_grid), np.nan, np.float32)
+    y = np.full((n_ch, plan.n_grid), np.nan, np.float64)
     E = padlen
 
     def fwd(Sf, h, xv):

@@ -9,6 +9,7 @@ import os
 import numpy as np
 import pytest
 
+import gates
 import oracle
 import synth
 
@@ -91,8 +92,8 @@ def test_out_of_core_lfproc_matches_resident(tmp_path, capsys, dims):
         np.testing.assert_array_equal(b.coords["time"].astype(np.int64), rt)
         da = a.data if dims[0] == "distance" else a.data.T
         db = b.data if dims[0] == "distance" else b.data.T
-        assert _rel(db, da) < 1e-6
-        assert _rel(db, ry) < 1e-4
+        gates.check(f"archive_stream_vs_resident {dims}", _rel(db, da), gates.PATHS)
+        gates.check(f"archive_oracle {dims}", _rel(db, ry), gates.STREAM)
 
 
 @pytest.mark.gpu
@@ -143,5 +144,5 @@ def test_jittered_boundary_same_rule_resident_and_stream(tmp_path, jitter_ns, me
     for a, b, (rt, ry) in zip(res["resident"], res["stream"], ref):
         np.testing.assert_array_equal(a.coords["time"].astype(np.int64), rt)
         np.testing.assert_array_equal(b.coords["time"].astype(np.int64), rt)
-        assert _rel(b.data, a.data) < 1e-6
-        assert _rel(a.data, ry) < 1e-4
+        gates.check("jitter_stream_vs_resident", _rel(b.data, a.data), gates.PATHS)
+        gates.check("jitter_oracle", _rel(a.data, ry), gates.MFMA)

@@ -68,11 +68,11 @@ def _sharded_worker(rank, world, port, out_dir, out_q):
     sp = dc.get_example_spool()  # 3 x (300 ch x 2000) @ 250 Hz
     sub, (c0, c1) = shard_spool(sp, world, rank)
     assert sub[0].shape[0] == c1 - c0
-    # default: gathered to rank 0 only (the writer); the others keep their block
+    # gather="root": gathered to rank 0 only (the writer); the others keep their block
     outs = process_time_range_sharded(sp, T1, T2, PARAMS, output_folder=out_dir, run_shard=_oracle_shard,
-                                      verbose=False)
-    # gather="all": every rank full width
-    outs_all = process_time_range_sharded(sp, T1, T2, PARAMS, run_shard=_oracle_shard, gather="all", verbose=False)
+                                      gather="root", verbose=False)
+    # default (gather=True, all-gather): every rank full width
+    outs_all = process_time_range_sharded(sp, T1, T2, PARAMS, run_shard=_oracle_shard, verbose=False)
     out_q.put((rank, (c0, c1), [(o.coords["time"].astype(np.int64), o.data) for o in outs],
                [(o.coords["time"].astype(np.int64), o.data) for o in outs_all]))
     dist.barrier()
@@ -81,9 +81,10 @@ def _sharded_worker(rank, world, port, out_dir, out_q):
 
 def test_gloo_world3_sharded_lfproc_driver(tmp_path):
     """process_time_range_sharded over 3 gloo ranks (300 channels: 100 each):
-    rank 0 gets the full-width outputs of every chunk (the others their own
-    100-channel block), equal to one process over the whole spool, and wrote
-    the reference's files; with gather="all" every rank gets the full width."""
+    with gather="root" rank 0 gets the full-width outputs of every chunk (the
+    others their own 100-channel block), equal to one process over the whole
+    spool, and wrote the reference's files; by default (all-gather) every rank
+    gets the full width."""
     here = os.path.dirname(os.path.abspath(__file__))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

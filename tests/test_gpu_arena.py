@@ -35,7 +35,7 @@ def test_device_samples_pool_view_and_parity():
     chunks = [(*S.select_range(t0, dt_ns, n, tg[a], tg[b]), oa, ob) for a, b, oa, ob in sched]
     plan = LowpassPlan(lowpass_sos(fs, 0.45), n_ch, n, lo, w, chunks)
     ws = plan.alloc_workspace()
-    ya = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float32, device="cuda")
+    ya = torch.full((n_ch, len(tg)), float("nan"), dtype=torch.float64, device="cuda")
     yb = torch.full_like(ya, float("nan"))
     plan.execute(x, ya, ws)
     plan.execute(xc, yb, ws)

@@ -1,9 +1,11 @@
 """The multi-GPU driver with the DEVICE compute (lfdas.shard.
 process_time_range_sharded, default ``lfproc_shard``): world_size-2 gloo
 ranks, both on cuda:0 (a 1-GPU box cannot run RCCL with two ranks), each
-running LFProc's device plan on its channel block and gathering the float32
+running LFProc's device plan on its channel block and gathering the float64
 device outputs.  Compared with the oracle's process_time_range over the
-whole spool (relRMS <= 1e-4, identical times, the reference's files)."""
+whole spool (tests/gates.py, identical times, the reference's files).  The
+RCCL branch (backend "nccl", HBM-to-HBM gathers) runs at world_size 1 on the
+one GPU (test_rccl_world1_*)."""
 import os
 import queue
 import socket
@@ -11,6 +13,8 @@ import socket
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
+
+import gates
 
 pytestmark = pytest.mark.gpu
 
@@ -106,8 +110,8 @@ def test_sharded_device_compute_world2_matches_oracle(tmp_path, dims):
             assert d.shape == ry.shape == (300, len(rt))
             assert d.dtype == np.float64
             rel = float(np.sqrt(np.sum((d - ry) ** 2) / np.sum(ry ** 2)))
-            assert rel < 1e-4, rel
-    # both ranks hold the identical full-width result (gathered float32)
+            gates.check(f"sharded_world2 {dims} rank{rank}", rel, gates.MFMA)
+    # both ranks hold the identical full-width result (gathered float64)
     for (_, d0, _), (_, d1, _) in zip(got[0][3], got[1][3]):
         np.testing.assert_array_equal(d0, d1)
     files = sorted(os.listdir(out_dir))
@@ -189,8 +193,8 @@ def test_shard_stream_world2_device_matches_oracle(time_major):
     """cfg5 geometry (200 Hz, dt = 10 s, P = 120, B = 6) streamed in 60 s
     pushes through ``shard_stream`` + ``push_rows`` on two gloo ranks sharing
     cuda:0: each rank's device outputs for its channel block (19 + 18 of 37)
-    equal the oracle's process_time_range over the whole spool (relRMS <=
-    1e-4 per rank, on every channel incl. each block's first and last),
+    equal the oracle's process_time_range over the whole spool (gates.STREAM
+    per rank, on every channel incl. each block's first and last),
     with identical output times and chunk (file) boundaries."""
     here = os.path.dirname(os.path.abspath(__file__))
     os.environ["PYTHONPATH"] = os.pathsep.join([here, os.path.dirname(here),
@@ -230,8 +234,82 @@ def test_shard_stream_world2_device_matches_oracle(time_major):
         assert counts == [len(tt) for tt, _ in ref if len(tt)]
         assert y.shape == (c1 - c0, want.shape[1])
         w = want[c0:c1]
-        rel = float(np.sqrt(np.sum((y.astype(np.float64) - w) ** 2) / np.sum(w ** 2)))
-        assert rel < 1e-4, rel
+        assert y.dtype == np.float64
+        rel = float(np.sqrt(np.sum((y - w) ** 2) / np.sum(w ** 2)))
+        gates.check(f"shard_stream tm={time_major} {c0}", rel, gates.STREAM)
         for r in (0, c1 - c0 - 1):  # the block's first and last channel alone
-            rr = float(np.sqrt(np.sum((y[r].astype(np.float64) - w[r]) ** 2) / np.sum(w[r] ** 2)))
-            assert rr < 1e-4, (c0 + r, rr)
+            rr = float(np.sqrt(np.sum((y[r] - w[r]) ** 2) / np.sum(w[r] ** 2)))
+            gates.check(f"shard_stream tm={time_major} ch{c0 + r}", rr, gates.STREAM)
+
+
+# --- the RCCL branch on the one GPU (backend "nccl", world_size 1) ----------
+
+def _rccl_rank(port, out_dir, q):
+    """One rank on backend "nccl": process_time_range_sharded with the
+    all-gather (default) and the gather to rank 0, plus the gather helpers on
+    HBM tensors — RCCL's all_gather / gather on device memory, the branch
+    that the gloo tests never reach (_comm_device -> cuda)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import lfdas.dc as dc
+        from lfdas.shard import (_comm_device, all_gather_channels, gather_channels_to_root,
+                                 process_time_range_sharded)
+        assert dist.get_backend() == "nccl" and _comm_device().type == "cuda"
+        sp = dc.get_example_spool()
+        res = {}
+        for mode in (True, "root", "all"):
+            outs = process_time_range_sharded(sp, T1, T2, PARAMS, output_folder=out_dir if mode == "root" else None,
+                                              device="cuda:0", gather=mode, verbose=False)
+            res[str(mode)] = [(o.coords["time"].astype(np.int64), o.data) for o in outs]
+        y = torch.arange(21 * 5, dtype=torch.float64, device="cuda").reshape(21, 5)
+        a = all_gather_channels(y, 21)
+        g = gather_channels_to_root(y, 21)
+        ok = bool(a.is_cuda and g.is_cuda and torch.equal(a, y) and torch.equal(g, y))
+        q.put(("ok", res, ok))
+    except Exception as e:  # reported, so the test fails with the rank's error
+        q.put(("error", repr(e), False))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_sharded_driver_matches_oracle(tmp_path):
+    """The "nccl" (RCCL) backend of the sharded driver, executed: one rank on
+    the box's GPU gathers its device outputs HBM to HBM through RCCL's
+    all_gather (gather=True / "all") and gather (gather="root"), and the
+    results equal the oracle's process_time_range over the whole spool.  No
+    scaling is claimed from it (one rank)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, os.path.dirname(here),
+                                                os.path.join(os.path.dirname(here), "low-freq-real-time_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    out_dir = str(tmp_path / "rccl")
+    p = ctx.Process(target=_rccl_rank, args=(_free_port(), out_dir, q))
+    p.start()
+    try:
+        status, res, ok = q.get(timeout=100)
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    except queue.Empty:
+        pytest.fail("the RCCL rank did not report within 100 s")
+    finally:
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=10)
+    assert status == "ok", res
+    assert ok  # all_gather_channels / gather_channels_to_root on HBM tensors
+    ref = _oracle_outputs()
+    for mode, outs in res.items():
+        assert len(outs) == len(ref) == 4, mode
+        for (t, d), (rt, ry) in zip(outs, ref):
+            np.testing.assert_array_equal(t, rt)
+            assert d.shape == ry.shape == (300, len(rt)) and d.dtype == np.float64
+            gates.check(f"rccl_world1 gather={mode}", gates.relrms(d, ry), gates.MFMA)
+    files = sorted(os.listdir(out_dir))
+    assert len(files) == 4 and all(f.startswith("LFDAS_2017-09-18T") for f in files)

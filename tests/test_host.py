@@ -6,6 +6,7 @@ import re
 import numpy as np
 import pytest
 
+import gates
 import oracle
 import synth
 from emulate import emulate
@@ -254,7 +255,7 @@ def test_plan_constants_reproduce_golden(name):
     m = ~np.isnan(ref)
     assert np.array_equal(np.isnan(y), ~m)
     rel = np.sqrt(np.sum((y[m] - ref[m]) ** 2) / np.sum(ref[m] ** 2))
-    assert rel < 1e-6
+    gates.check(f"emulate_recurrence {name}", rel, gates.EMU_REC)
 
 
 @pytest.mark.parametrize("name", ["lfproc_cfg1.npz", "lfproc_cfg5_slice.npz"])
@@ -280,7 +281,7 @@ def test_block_taps_reproduce_golden(name):
         y = emulate(plan, x, 15, k1=k1)
         assert np.array_equal(np.isnan(y), ~m)
         rel = np.sqrt(np.sum((y[m] - ref[m]) ** 2) / np.sum(ref[m] ** 2))
-        assert rel < 1e-6, (k1, rel)
+        gates.check(f"emulate_{k1} {name}", rel, gates.EMU_TAPS)
 
 
 def _plan_off(fs, dt_out, P, B, n_ch, n, off_ns, grid_start_s=1.0):
@@ -329,7 +330,7 @@ def test_offsample_and_subblock_plans_match_oracle(cfg, k1):
         num += float(np.sum((y[:, oa:ob] - r) ** 2))
         den += float(np.sum(r ** 2))
         produced[oa:ob] = True
-    assert (num / den) ** 0.5 < 1e-6
+    gates.check(f"emulate_offgrid {k1}", (num / den) ** 0.5, gates.EMU_REC if k1 == "recurrence" else gates.EMU_TAPS)
     assert np.all(np.isnan(y[:, ~produced]))
 
 
@@ -348,7 +349,7 @@ def test_offsample_tail_output_blends_two_samples():
     y = emulate(plan, x, 15, k1="runs")
     yf = oracle.sosfiltfilt(oracle.butter_sos(4, 1.0 / 125.0), x)
     ref = yf[:, lo] + 0.25 * (yf[:, lo + 1] - yf[:, lo])
-    assert np.sqrt(np.sum((y - ref) ** 2) / np.sum(ref ** 2)) < 1e-6
+    gates.check("emulate_runs_blended", np.sqrt(np.sum((y - ref) ** 2) / np.sum(ref ** 2)), gates.EMU_TAPS)
 
 
 def test_host_only_plan_cannot_execute():

@@ -13,6 +13,7 @@ import os
 import numpy as np
 import pytest
 
+import gates
 import oracle
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -139,7 +140,8 @@ def test_bandpass_interpolate_uses_block_path():
     grid = p.coords["time"][::25][1:-2]
     out = p.pass_filter(time=(0.5, 4.0)).interpolate(time=grid)
     ref = oracle.sosfiltfilt(oracle.dascore_pass_filter_sos(fs, 0.5, 4.0), x)[:, 25::25][:, :len(grid)]
-    assert _rel(out.data, ref) < 1e-4
+    assert out.data.dtype == np.float64
+    gates.check("bandpass_interpolate", _rel(out.data, ref), gates.REC)
 
 
 @pytest.mark.gpu
@@ -152,8 +154,10 @@ def test_decimate_iir_device(q):
     ref = oracle.decimate_iir(x.astype(np.float32).astype(np.float64), q)
     assert out.data.shape == ref.shape
     np.testing.assert_array_equal(out.coords["time"], p.coords["time"][::q])
-    assert _rel(out.data, ref) < 1e-4
-    assert _rel(out.data, g[f"dec_{q}"]) < 1e-4  # SciPy on the float64 data
+    gates.check(f"decimate_iir q={q}", _rel(out.data, ref), gates.REC)
+    # SciPy on the float64 data: the float32 sample quantisation (~3e-8 of
+    # the samples) bounds this one
+    gates.check(f"decimate_iir_golden q={q}", _rel(out.data, g[f"dec_{q}"]), gates.Q32)
     with pytest.raises(ValueError):
         p.decimate(time=q, filter_type="kaiser")
 

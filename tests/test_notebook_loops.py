@@ -10,8 +10,8 @@ of DASDAE files, against the oracle's restatement of the same loops.
 * rolling_mean_dascore(_edge).ipynb cell 9 (per-file rolling(time=d_t*s,
   step=d_t*s).mean() * scale_iDAS, written, merged, dropna('time')).
 
-Tolerances: relRMS <= 1e-4 for the low-pass outputs (north_star), <= 1e-6 for
-rolling means; output times identical.  The archive is (time, distance) like
+Tolerances: tests/gates.py for the float64 low-pass outputs (<= 10x the
+measured relRMS; north_star's bar is 1e-4), <= 1e-6 for rolling means; output times identical.  The archive is (time, distance) like
 the reference's raw files; the sleep between real-time runs is replaced by the
 arrival of the next file."""
 import os
@@ -19,6 +19,7 @@ import os
 import numpy as np
 import pytest
 
+import gates
 import oracle
 
 pytestmark = pytest.mark.gpu
@@ -142,7 +143,7 @@ def test_low_pass_notebook_batch(tmp_path, mode):
     assert len(lfp.outputs) == len(ref) and len(ref) >= 4
     for out, (tr, yr) in zip(lfp.outputs, ref):
         np.testing.assert_array_equal(out.coords["time"].astype(np.int64), tr)
-        assert _rel(out.data.T, yr) < 1e-4
+        gates.check(f"notebook_batch {mode}", _rel(out.data.T, yr), gates.STREAM if mode == "stream" else gates.MFMA)
 
     # cell 13: read the results back and merge them into one patch
     sp_result = dc.spool(out_folder)
@@ -153,7 +154,8 @@ def test_low_pass_notebook_batch(tmp_path, mode):
     tr, yr = _concat(ref)
     np.testing.assert_array_equal(merged.coords["time"].astype(np.int64), tr)
     assert merged.dims == ("time", "distance") and merged.shape == (len(tr), CH_END - CH_START + 1)
-    assert _rel(merged.data.T, yr) < 1e-4
+    gates.check(f"notebook_batch_merged {mode}", _rel(merged.data.T, yr),
+                gates.STREAM if mode == "stream" else gates.MFMA)
     assert merged.attrs["time_step"] == np.timedelta64(int(d_t * 1e9), "ns")
 
 
@@ -209,14 +211,14 @@ def test_low_pass_notebook_realtime(tmp_path):
         assert len(got) == len(exp) >= 1
         for (tg, yg), (te, ye) in zip(got, exp):
             np.testing.assert_array_equal(tg, te)
-            assert _rel(yg, ye) < 1e-4
+            gates.check("notebook_realtime", _rel(yg, ye), gates.MFMA)
 
     # every run continues the previous one's output grid: one merged patch
     merged = dc.spool(output_data_folder).chunk(time=None)
     assert len(merged) == 1
     te, ye = _concat([c for run in ref for c in run])
     np.testing.assert_array_equal(merged[0].coords["time"].astype(np.int64), te)
-    assert _rel(merged[0].data.T, ye) < 1e-4
+    gates.check("notebook_realtime_merged", _rel(merged[0].data.T, ye), gates.MFMA)
 
 
 @pytest.mark.parametrize("realtime", [False, True])
