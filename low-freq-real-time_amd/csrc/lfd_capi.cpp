@@ -1039,7 +1039,10 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     if ((size_t)Lp * nc * nvar * sizeof(double) <= (size_t)lfd::TAP_LDS_MAX) {
       p->taps.resize(Kx.size());
       for (size_t i = 0; i < Kx.size(); ++i) p->taps[i] = (double)Kx[i];
-      p->tg = lfd::TapGeom{Lp, J, nc, nvar, v0};
+      // 16-rows x 64-B sample order; the diagnostic build's LFD_K1_LINES=1
+      // selects the whole-line loads + DPP exchange (lfd_kernels.hip
+      // mf_load_lines), measured 1-1.5 % slower (profiles/r06_k1_lines_ab.txt)
+      p->tg = lfd::TapGeom{Lp, J, nc, nvar, v0, lfd::knob("LFD_K1_LINES") ? std::atoi(lfd::knob("LFD_K1_LINES")) : 0};
     }
   }
   if (n_off > 0 && (p->taps.empty() ||
@@ -1315,7 +1318,10 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
         for (int q = 0; q < 4; ++q)
           for (int cc = 0; cc < tg.nc; ++cc)
             for (int el = 0; el < 4; ++el) {
-              const int pos = 16 * t + 4 * q + el - v;
+              // (t: 16-sample group = iteration t / 4, operand group j = t % 4)
+              const int j = t & 3;
+              const int pos = (tg.lines ? 64 * (t >> 2) + 4 * (8 * (j >> 1) + 2 * q + (j & 1)) : 16 * t + 4 * q) +
+                              el - v;
               if (pos >= 0 && pos < row)
                 dev[vi * tab + ((size_t)(t * 4 + q) * tg.nc + cc) * 4 + el] =
                     p->taps[(size_t)cc * row + pos];

@@ -2811,18 +2811,62 @@ __device__ __forceinline__ f4v mf_load_guarded(const float *__restrict__ xr, int
   return v;
 }
 
+// Sample layout of one 64-sample iteration in the MFMA operands: lane
+// (q, col) holds in group j the 4 samples at iteration offset mf_off(j, q)
+// of channel col (MFMA step (j, e) uses sample mf_off + e as row k = q).
+//   LINES = false: offset 16 j + 4 q (a wave-instruction loads 16 rows x 64 B);
+//   LINES = true (TapGeom::lines): 16-B piece P = 8 (j >> 1) + 2 q + (j & 1),
+//   the order in which whole 128-B lines arrive (mf_load_lines): the wave
+//   loads 4 x (8 rows x 128 B) and one DPP exchange per register pair puts
+//   channel col on lane 16 q + col.  The host packs the tap table in the same
+//   order (lfd_capi.cpp upload_taps).
+template <bool LINES>
+__device__ __forceinline__ int mf_off(int j, int q) {
+  return LINES ? 4 * (8 * (j >> 1) + 2 * q + (j & 1)) : 16 * j + 4 * q;
+}
+
 // finite-mask the elements of one 64-sample iteration that lie outside the
-// block's own samples (row offsets [lo, hi) = [J + v, J + v + L)); o0 = this
-// lane's first offset (64 it + 4 q).  Only a block's first iteration (FIR
+// block's own samples (row offsets [lo, hi) = [J + v, J + v + L)); o_it = the
+// iteration's first offset (64 it).  Only a block's first iteration (FIR
 // history) and last iteration (zero-tap padding) hold such elements.
-__device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o0, int lo, int hi) {
+template <bool LINES>
+__device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o_it, int q, int lo, int hi) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int o = o0 + 16 * j + e;
+      const int o = o_it + mf_off<LINES>(j, q) + e;
       if ((o < lo || o >= hi) && !__builtin_isfinite(cur[j][e])) cur[j][e] = 0.0f;
     }
+}
+
+// Whole-line loads (LINES; diagnostic A/B, LFD_K1_LINES=1): lane 16 k + 8 h +
+// m reads 16 B of channel row m (instructions 0, 2; xa) or 8 + m (1, 3; xb)
+// at iteration offset 8 k + 4 h (+ 32 for instructions 2, 3): every
+// wave-instruction reads 8 whole 128-B lines.  Loads alone that shape streams
+// faster (0.734-0.746 -> 0.749-0.775 of HBM at cfg3's 10,000 channels,
+// 0.64 -> 0.70-0.71 at an 8-GPU shard's 1,248: profiles/r06_k1_shape.txt),
+// but in K1 the 16 DPP exchanges per iteration cost more than it gains:
+// 12.47 -> 12.66 ms at 10,000 channels, 1.635 -> 1.650 ms at 1,250
+// (profiles/r06_k1_lines_ab.txt), so production keeps 16 rows x 64 B.
+// pa / pb: the lane's addresses in xa / xb.
+__device__ __forceinline__ void mf_load_lines(const float *pa, const float *pb, f4v (&b)[4]) {
+  b[0] = *reinterpret_cast<const f4u *>(pa);
+  b[1] = *reinterpret_cast<const f4u *>(pb);
+  b[2] = *reinterpret_cast<const f4u *>(pa + 32);
+  b[3] = *reinterpret_cast<const f4u *>(pb + 32);
+}
+// ... then the exchange into the MFMA layout: in each 16-lane row, lanes
+// 8..15 of a (channel m, piece 2k+1) and lanes 0..7 of b (channel 8 + m,
+// piece 2k) trade places (DPP row_ror:8 under a bank mask, no LDS), leaving
+// a = piece 2k and b = piece 2k + 1 of channel (lane & 15) in every lane.
+__device__ __forceinline__ void mf_lines_swap(f4v &a, f4v &b) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ai = __float_as_int(a[e]), bi = __float_as_int(b[e]);
+    a[e] = __int_as_float(__builtin_amdgcn_update_dpp(ai, bi, 0x128, 0xf, 0xc, false));
+    b[e] = __int_as_float(__builtin_amdgcn_update_dpp(bi, ai, 0x128, 0xf, 0x3, false));
+  }
 }
 
 
@@ -2866,7 +2910,7 @@ __device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<c
 // invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
 // ceiling of the x stream + F stores; 3 = no MFMA and no F stores = the
 // x-stream ceiling alone.
-template <int PF, int MODE>
+template <int PF, int MODE, bool LINES = true>
 __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs,
@@ -2908,13 +2952,13 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
     const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
-    const int64_t a = s - v + 4 * q;
+    const int64_t a = s - v;
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     for (int it = 0; it < nit; ++it) {
       f4v cur[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
-      if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + mf_off<LINES>(j, q), n_t);
+      if (it == 0 || it == nit - 1) mf_mask_outside<LINES>(cur, 64 * it, q, tg.J + v, tg.J + v + L);
       mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
     mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
@@ -2923,8 +2967,19 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
 
   // interior: flattened (block, iteration) stream; the loads of the next PF
   // iterations are in flight behind the current iteration's MFMAs
-  const float *xl = xr + 4 * q;
+  const int64_t rla = cg * 16 + (lane & 7), rlb = rla + 8;
+  const float *xl = LINES ? x + (rla < g.n_ch ? rla : g.n_ch - 1) * s_ch + 8 * q + 4 * ((lane >> 3) & 1)
+                          : xr + 4 * q;
+  const int64_t dlb = LINES ? ((rlb < g.n_ch ? rlb : g.n_ch - 1) - (rla < g.n_ch ? rla : g.n_ch - 1)) * s_ch : 0;
   auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
+  auto load_it = [&](const float *p, f4v (&b)[4]) {
+    if constexpr (LINES) {
+      mf_load_lines(p, p + dlb, b);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = ldx4(p + 16 * j);
+    }
+  };
   int64_t k = ka, s = s0 + ka * L;  // consumer position
   int it = 0;
   int64_t kp = ka, sp = s;          // producer position
@@ -2945,8 +3000,7 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
   f4v buf[PF + 1][4];
 #pragma unroll
   for (int d = 0; d < PF; ++d) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) buf[d][j] = ldx4(pp + 16 * j);
+    load_it(pp, buf[d]);
     produce();
   }
   const double *kt = table(s);
@@ -2959,17 +3013,20 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     for (int u = 0; u <= PF; ++u) {
       constexpr int NB = PF + 1;
       const int lb = (u + PF) % NB;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) buf[lb][j] = ldx4(pp + 16 * j);
+      load_it(pp, buf[lb]);
       produce();
       if (MODE == 1 || MODE == 3) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
       } else {
+        if constexpr (LINES) {
+          mf_lines_swap(buf[u][0], buf[u][1]);
+          mf_lines_swap(buf[u][2], buf[u][3]);
+        }
         if (it == 0 || it == nit - 1) {
           const int v = (int)(s & 3);
-          mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+          mf_mask_outside<LINES>(buf[u], 64 * it, q, tg.J + v, tg.J + v + L);
         }
         mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
       }
@@ -3091,7 +3148,7 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 struct LatAcc {
   double S0 = 0.0, T1 = 0.0, v0 = 0.0, ya = 0.0, yb = 0.0;
 };
-template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false>
+template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false, bool LINES = true>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -3255,13 +3312,13 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
     const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
-    const int64_t a = s - v + 4 * q;
+    const int64_t a = s - v;
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     for (int it = 0; it < nit; ++it) {
       f4v cur[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
-      if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + mf_off<LINES>(j, q), n_t);
+      if (it == 0 || it == nit - 1) mf_mask_outside<LINES>(cur, 64 * it, q, tg.J + v, tg.J + v + L);
       mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
     block_done(acc0 + acc1, k);
@@ -3273,7 +3330,10 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   kb = uniform64(kb > k1 ? k1 : (kb < ka ? ka : kb));
   for (int64_t k = k0; k < ka; ++k) guarded_block(k);
   if (ka < kb) {
-    const float *xl = xr + 4 * q;
+    const int64_t rla = cg * 16 + (lane & 7), rlb = rla + 8;
+    const float *xl = LINES ? x + (rla < g.n_ch ? rla : g.n_ch - 1) * s_ch + 8 * q + 4 * ((lane >> 3) & 1)
+                            : xr + 4 * q;
+    const int64_t dlb = LINES ? ((rlb < g.n_ch ? rlb : g.n_ch - 1) - (rla < g.n_ch ? rla : g.n_ch - 1)) * s_ch : 0;
     auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
     int64_t k = ka, s = s0 + ka * L;
     int it = 0;
@@ -3290,8 +3350,12 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       pp = addr(sp, itp);
     };
     auto load_iter = [&](f4v (&b)[4]) {
+      if constexpr (LINES) {
+        mf_load_lines(pp, pp + dlb, b);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
+        for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
+      }
     };
     f4v buf[PF + 1][4];
 #pragma unroll
@@ -3314,12 +3378,16 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
           for (int j = 0; j < 4; ++j)
             acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
         } else {
+          if constexpr (LINES) {
+            mf_lines_swap(buf[u][0], buf[u][1]);
+            mf_lines_swap(buf[u][2], buf[u][3]);
+          }
           // every chunk's first and last full block is a run end, and inside
           // a run the out-of-block samples belong to the run's own blocks:
           // only a run's first and last iteration need the finite mask
           if ((it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen)) {
             const int v = (int)(s & 3);
-            mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+            mf_mask_outside<LINES>(buf[u], 64 * it, q, tg.J + v, tg.J + v + L);
           }
           mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
         }
@@ -3800,11 +3868,15 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
+    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0, true>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0, false>),
 #ifdef LFD_DIAG
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1, true>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3, true>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6, true>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1, false>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3, false>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6, false>),
 #endif
                            }) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3851,9 +3923,15 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   const int64_t n_runs = (g.nb + bpw - 1) / bpw;
   const int64_t units = n_cg * n_runs;
   const unsigned grid = nblk(units, threads / 64);
-#define LFD_MF(PF_, MODE_)                                                                      \
-  k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
-                                                                   n_runs, bpw)
+#define LFD_MF(PF_, MODE_)                                                                                    \
+  do {                                                                                                        \
+    if (tg.lines)                                                                                             \
+      k_block_functionals_mfma<PF_, MODE_, true><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F,   \
+                                                                             n_runs, bpw);                    \
+    else                                                                                                      \
+      k_block_functionals_mfma<PF_, MODE_, false><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F,  \
+                                                                              n_runs, bpw);                   \
+  } while (0)
 #ifdef LFD_DIAG
   // timing-only modes (results invalid, LFD_MF_MODE): 1 loads only, 3 no
   // stores, 6 stores into an L2-resident window
@@ -3883,12 +3961,15 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   const size_t lds = LAT ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
                          : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  auto kern = &k_block_runs_mfma<PF, MODE, NT, MINW, LAT>;
+  auto kern = tg.lines ? &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, true>
+                       : &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, false>;
   static std::once_flag attr_once;
   hipError_t ea = hipSuccess;
   std::call_once(attr_once, [&] {
-    ea = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             TAP_LDS_MAX);
+    for (const void *fn : {reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, true>),
+                           reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, false>)})
+      if (ea == hipSuccess)
+        ea = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
   });
   if (ea != hipSuccess) return ea;
   kern<<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);

@@ -6,7 +6,10 @@
 // narrow shard can be streamed from its own allocation or from inside a wide
 // one (placement vs width).
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/ubench_narrow tools/ubench_narrow.hip
-// Run:   tools/ubench_narrow <nch> <alloc_ch> <off> <bpu> [order]
+// Run:   tools/ubench_narrow <nch> <alloc_ch> <off> <bpu> [order] [shape]
+// shape 0: K1's 16 rows x 64 B per wave instruction; shape 1: 8 rows x 128 B
+// (whole lines: lanes 8i..8i+7 read one row's 128 B; the same 16 rows x 256 B
+// per 64-sample iteration in 4 instructions)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -18,6 +21,7 @@ constexpr int64_t NT = 1800000;
 constexpr int L = 500;
 
 // order 0: unit = cg + n_cg * time group (K1's); 1: unit = time group + n_tg * cg
+template <int SHAPE>
 __global__ __launch_bounds__(512) void k_rows(const float *__restrict__ x, float *out, int64_t nch, int bpu,
                                               int order) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -28,13 +32,22 @@ __global__ __launch_bounds__(512) void k_rows(const float *__restrict__ x, float
   const int64_t cg = order ? unit / n_tg : unit % n_cg, tg = order ? unit % n_tg : unit / n_cg;
   const int col = lane & 15, q = lane >> 4;
   const float *xr = x + (cg * 16 + col) * NT + 4 * q;
+  // shape 1: rows lane / 8 (instructions 0, 2) and 8 + lane / 8 (1, 3), piece lane % 8
+  const float *xa = x + (cg * 16 + (lane >> 3)) * NT + 4 * (lane & 7);
+  const float *xb = xa + 8 * NT;
   float acc = 0.f;
   f4v v[2][4];
   int64_t k = tg * bpu, it = 0;
   auto ld = [&](f4v (&b)[4], int64_t kk, int64_t ii) {
     const int64_t a = (kk * L) & ~(int64_t)3;
+    if (SHAPE == 0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const f4v *>(xr + a + 64 * ii + 16 * j);
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const f4v *>(xr + a + 64 * ii + 16 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *reinterpret_cast<const f4v *>((j & 1 ? xb : xa) + a + 64 * ii + 32 * (j >> 1));
+    }
   };
   ld(v[0], k, 0);
   const int64_t n_it = (int64_t)bpu * 8;
@@ -67,7 +80,7 @@ int main(int argc, char **argv) {
     return 2;
   }
   const int64_t nch = atoll(argv[1]), alloc_ch = atoll(argv[2]), off = atoll(argv[3]);
-  const int bpu = atoi(argv[4]), order = argc > 5 ? atoi(argv[5]) : 0;
+  const int bpu = atoi(argv[4]), order = argc > 5 ? atoi(argv[5]) : 0, shape = argc > 6 ? atoi(argv[6]) : 0;
   if (nch % 16 || off + nch > alloc_ch || bpu < 1) return 2;
   float *x, *out;
   if (hipMalloc(&x, sizeof(float) * alloc_ch * NT) != hipSuccess) return 1;
@@ -81,12 +94,18 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  k_rows<<<grid, 512>>>(xs, out, nch, bpu, order);
+  auto launch = [&]() {
+    if (shape)
+      k_rows<1><<<grid, 512>>>(xs, out, nch, bpu, order);
+    else
+      k_rows<0><<<grid, 512>>>(xs, out, nch, bpu, order);
+  };
+  launch();
   float best = 1e30f, sum = 0.f;
   const int reps = 5;
   for (int r = 0; r < reps; ++r) {
     (void)hipEventRecord(e0);
-    k_rows<<<grid, 512>>>(xs, out, nch, bpu, order);
+    launch();
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -95,8 +114,8 @@ int main(int argc, char **argv) {
     sum += ms;
   }
   const double bytes = (double)nch * (double)(nb / bpu * bpu) * L * 4.0;
-  printf("nch %6lld alloc %6lld off %6lld bpu %3d order %d: mean %.3f ms min %.3f ms  %.2f TB/s (%.3f of 8)\n",
-         (long long)nch, (long long)alloc_ch, (long long)off, bpu, order, sum / reps, best,
+  printf("shape %d nch %6lld alloc %6lld off %6lld bpu %3d order %d: mean %.3f ms min %.3f ms  %.2f TB/s (%.3f of 8)\n",
+         shape, (long long)nch, (long long)alloc_ch, (long long)off, bpu, order, sum / reps, best,
          bytes / (sum / reps * 1e-3) / 1e12, bytes / (sum / reps * 1e-3) / 8e12);
   (void)hipFree(x);
   (void)hipFree(out);
