@@ -1086,7 +1086,7 @@ __device__ uint64_t g_fr_times[16384 * 8];
 #ifndef FRS_Q
 // k_fullrate_scan: big blocks per load batch (8: 0.83 ms vs 0.91 at 4 on the
 // 2,000 x 600,000 band-pass; a software-pipelined next batch spills and is
-// slower, profiles/r02_fullrate_scan_ab.txt)
+// slower, profiles/archive_r01_r03.md (r02_fullrate_scan_ab.txt))
 #define FRS_Q 8
 #endif
 #ifndef FR_WAVES
@@ -1365,7 +1365,7 @@ __device__ __forceinline__ void rows_transpose4(double &v0, double &v1, double &
 
 // one k-step of A (this lane's 16x16x4 A value) against four column tiles
 // (the 4x4x4_4b form of the same products measured slower,
-// profiles/r02_ubench_mfma64b.txt)
+// profiles/archive_r01_r03.md (r02_ubench_mfma64b.txt))
 __device__ __forceinline__ void mfma_k4(double av, const double (&b)[4], fr_d4v (&acc)[4]) {
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[nt], acc[nt], 0, 0, 0);
@@ -2811,64 +2811,19 @@ __device__ __forceinline__ f4v mf_load_guarded(const float *__restrict__ xr, int
   return v;
 }
 
-// Sample layout of one 64-sample iteration in the MFMA operands: lane
-// (q, col) holds in group j the 4 samples at iteration offset mf_off(j, q)
-// of channel col (MFMA step (j, e) uses sample mf_off + e as row k = q).
-//   LINES = false: offset 16 j + 4 q (a wave-instruction loads 16 rows x 64 B);
-//   LINES = true (TapGeom::lines): 16-B piece P = 8 (j >> 1) + 2 q + (j & 1),
-//   the order in which whole 128-B lines arrive (mf_load_lines): the wave
-//   loads 4 x (8 rows x 128 B) and one DPP exchange per register pair puts
-//   channel col on lane 16 q + col.  The host packs the tap table in the same
-//   order (lfd_capi.cpp upload_taps).
-template <bool LINES>
-__device__ __forceinline__ int mf_off(int j, int q) {
-  return LINES ? 4 * (8 * (j >> 1) + 2 * q + (j & 1)) : 16 * j + 4 * q;
-}
-
 // finite-mask the elements of one 64-sample iteration that lie outside the
-// block's own samples (row offsets [lo, hi) = [J + v, J + v + L)); o_it = the
-// iteration's first offset (64 it).  Only a block's first iteration (FIR
+// block's own samples (row offsets [lo, hi) = [J + v, J + v + L)); o0 = this
+// lane's first offset (64 it + 4 q).  Only a block's first iteration (FIR
 // history) and last iteration (zero-tap padding) hold such elements.
-template <bool LINES>
-__device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o_it, int q, int lo, int hi) {
+__device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o0, int lo, int hi) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int o = o_it + mf_off<LINES>(j, q) + e;
+      const int o = o0 + 16 * j + e;
       if ((o < lo || o >= hi) && !__builtin_isfinite(cur[j][e])) cur[j][e] = 0.0f;
     }
 }
-
-// Whole-line loads (LINES; diagnostic A/B, LFD_K1_LINES=1): lane 16 k + 8 h +
-// m reads 16 B of channel row m (instructions 0, 2; xa) or 8 + m (1, 3; xb)
-// at iteration offset 8 k + 4 h (+ 32 for instructions 2, 3): every
-// wave-instruction reads 8 whole 128-B lines.  Loads alone that shape streams
-// faster (0.734-0.746 -> 0.749-0.775 of HBM at cfg3's 10,000 channels,
-// 0.64 -> 0.70-0.71 at an 8-GPU shard's 1,248: profiles/r06_k1_shape.txt),
-// but in K1 the 16 DPP exchanges per iteration cost more than it gains:
-// 12.47 -> 12.66 ms at 10,000 channels, 1.635 -> 1.650 ms at 1,250
-// (profiles/r06_k1_lines_ab.txt), so production keeps 16 rows x 64 B.
-// pa / pb: the lane's addresses in xa / xb.
-__device__ __forceinline__ void mf_load_lines(const float *pa, const float *pb, f4v (&b)[4]) {
-  b[0] = *reinterpret_cast<const f4u *>(pa);
-  b[1] = *reinterpret_cast<const f4u *>(pb);
-  b[2] = *reinterpret_cast<const f4u *>(pa + 32);
-  b[3] = *reinterpret_cast<const f4u *>(pb + 32);
-}
-// ... then the exchange into the MFMA layout: in each 16-lane row, lanes
-// 8..15 of a (channel m, piece 2k+1) and lanes 0..7 of b (channel 8 + m,
-// piece 2k) trade places (DPP row_ror:8 under a bank mask, no LDS), leaving
-// a = piece 2k and b = piece 2k + 1 of channel (lane & 15) in every lane.
-__device__ __forceinline__ void mf_lines_swap(f4v &a, f4v &b) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int ai = __float_as_int(a[e]), bi = __float_as_int(b[e]);
-    a[e] = __int_as_float(__builtin_amdgcn_update_dpp(ai, bi, 0x128, 0xf, 0xc, false));
-    b[e] = __int_as_float(__builtin_amdgcn_update_dpp(bi, ai, 0x128, 0xf, 0x3, false));
-  }
-}
-
 
 // 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur.
 // Lanes of A rows c >= nc read a copy of row nc-1 instead of zeros: MFMA rows
@@ -2910,7 +2865,7 @@ __device__ __forceinline__ f4v ldx4(const float *p) { return *reinterpret_cast<c
 // invalid; LFD_MF_MODE): 1 = no MFMA (VALU sum of the loads) = the memory
 // ceiling of the x stream + F stores; 3 = no MFMA and no F stores = the
 // x-stream ceiling alone.
-template <int PF, int MODE, bool LINES = true>
+template <int PF, int MODE>
 __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, double *__restrict__ F, int64_t n_runs,
@@ -2952,13 +2907,13 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
     const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
-    const int64_t a = s - v;
+    const int64_t a = s - v + 4 * q;
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     for (int it = 0; it < nit; ++it) {
       f4v cur[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + mf_off<LINES>(j, q), n_t);
-      if (it == 0 || it == nit - 1) mf_mask_outside<LINES>(cur, 64 * it, q, tg.J + v, tg.J + v + L);
+      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+      if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
       mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
     mf_store(acc0, acc1, F, k, tg.nc, q, ch, g);
@@ -2967,18 +2922,11 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
 
   // interior: flattened (block, iteration) stream; the loads of the next PF
   // iterations are in flight behind the current iteration's MFMAs
-  const int64_t rla = cg * 16 + (lane & 7), rlb = rla + 8;
-  const float *xl = LINES ? x + (rla < g.n_ch ? rla : g.n_ch - 1) * s_ch + 8 * q + 4 * ((lane >> 3) & 1)
-                          : xr + 4 * q;
-  const int64_t dlb = LINES ? ((rlb < g.n_ch ? rlb : g.n_ch - 1) - (rla < g.n_ch ? rla : g.n_ch - 1)) * s_ch : 0;
+  const float *xl = xr + 4 * q;
   auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
   auto load_it = [&](const float *p, f4v (&b)[4]) {
-    if constexpr (LINES) {
-      mf_load_lines(p, p + dlb, b);
-    } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = ldx4(p + 16 * j);
-    }
+    for (int j = 0; j < 4; ++j) b[j] = ldx4(p + 16 * j);
   };
   int64_t k = ka, s = s0 + ka * L;  // consumer position
   int it = 0;
@@ -3020,13 +2968,9 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
         for (int j = 0; j < 4; ++j)
           acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
       } else {
-        if constexpr (LINES) {
-          mf_lines_swap(buf[u][0], buf[u][1]);
-          mf_lines_swap(buf[u][2], buf[u][3]);
-        }
         if (it == 0 || it == nit - 1) {
           const int v = (int)(s & 3);
-          mf_mask_outside<LINES>(buf[u], 64 * it, q, tg.J + v, tg.J + v + L);
+          mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
         }
         mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
       }
@@ -3127,6 +3071,77 @@ __device__ __forceinline__ void run_block_stream(const double *__restrict__ cst,
   st.yb = db >= 0 ? yb : (db == -1 ? pg : st.yb);
 }
 
+// ---- whole-line K1 (TapGeom::lines, 4th-order cascades, nc = 9) ----
+// A wave-instruction of K1's sample stream reads 8 whole 128-B lines: lane
+// 16 k + 8 h + m reads 16 B of channel row m (registers 0, 2) or 8 + m (1, 3)
+// at iteration offset 8 k + 4 h (+ 32 for registers 2, 3).  Loads alone, this
+// shape streams at 0.749-0.775 of HBM vs 0.734-0.746 for 16 rows x 64 B at
+// cfg3's 10,000 channels, 0.70-0.71 vs 0.64 at an 8-GPU shard's 1,248
+// (profiles/r06_k1_shape.txt).  Moving the samples into the 16x16x4 layout
+// (channel = lane & 15) costs 16 DPP exchanges per iteration, more than the
+// shape gains (profiles/r06_k1_lines_ab.txt); instead the products run as
+// v_mfma_f64_4x4x4_4b, whose blocks b = (lane >> 2) & 3 each take their own A:
+// block b holds channels 4 (b & 1) + j (+ 8 for registers 1, 3) at pieces
+// 2k + (b >> 1), so its A is the taps of that piece parity.  Three such
+// products per (register, sample) give functionals 4g + i (g = 0, 1, 2; the
+// p0 row 8 alone in g = 2), in 6 accumulators (channel half x g); at a
+// block's end the two parities of a channel (lanes 8 apart) are summed and
+// lane (q, col) then holds functional 4 g + q of channel col: the 16x16x4
+// layout's a[g], so the run epilogue is unchanged.  The MFMA issue is 48 x
+// 4x4x4 (18.5 cycles) instead of 16 x 16x16x4 (87) per iteration.
+// Tap table per 64-sample iteration: [s][e][g0: 32 | g1: 32 | g2: 8] doubles
+// (576), g0 / g1 indexed k 8 + h 4 + i, g2 k 2 + h: Lp x 9 doubles per row
+// shift, the 16x16x4 table's size (lfd_capi.cpp upload_taps).
+constexpr int KL_IT = 576;  // doubles per 64-sample iteration
+constexpr int KL_SE = 72;   // doubles per (half s, component e)
+__device__ __forceinline__ void kl_load(const float *pa, const float *pb, f4v (&b)[4]) {
+  b[0] = *reinterpret_cast<const f4u *>(pa);
+  b[1] = *reinterpret_cast<const f4u *>(pb);
+  b[2] = *reinterpret_cast<const f4u *>(pa + 32);
+  b[3] = *reinterpret_cast<const f4u *>(pb + 32);
+}
+// finite mask (as mf_mask_outside) for the lane's samples at iteration offsets
+// 32 (r >> 1) + o_l + e, o_l = 8 k + 4 h
+__device__ __forceinline__ void kl_mask_outside(f4v (&cur)[4], int o_it, int o_l, int lo, int hi) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = o_it + 32 * (r >> 1) + o_l + e;
+      if ((o < lo || o >= hi) && !__builtin_isfinite(cur[r][e])) cur[r][e] = 0.0f;
+    }
+}
+// the 48 products of one iteration; kt = this iteration's table + the lane's
+// (g0, g1) slot, kt2 = its g2 slot
+__device__ __forceinline__ void kl_iter(const double *kt, const double *kt2, const f4v (&cur)[4], double (&acc)[6]) {
+#pragma unroll
+  for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int o = (sh * 4 + e) * KL_SE;
+      const double a0 = kt[o], a1 = kt[o + 32], a2 = kt2[o];
+      const double b0 = (double)cur[2 * sh][e], b1 = (double)cur[2 * sh + 1][e];
+      acc[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, b0, acc[0], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, b1, acc[3], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, b0, acc[1], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, b1, acc[4], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, b0, acc[2], 0, 0, 0);
+      acc[5] = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, b1, acc[5], 0, 0, 0);
+    }
+}
+// parities summed (DPP row_ror:8), lanes h = 1 take the channels 8..15
+__device__ __forceinline__ d4v kl_combine(const double (&acc)[6], bool h) {
+  d4v a;
+#pragma unroll
+  for (int gg = 0; gg < 3; ++gg) {
+    const double t0 = acc[gg] + dpp_row_d<0x128>(acc[gg]);
+    const double t1 = acc[3 + gg] + dpp_row_d<0x128>(acc[3 + gg]);
+    a[gg] = h ? t1 : t0;
+  }
+  a[3] = 0.0;
+  return a;
+}
+
 constexpr int RUN_WB = RUN_R * 5 * 16;  // doubles per wave run buffer
 constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 
@@ -3148,7 +3163,7 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 struct LatAcc {
   double S0 = 0.0, T1 = 0.0, v0 = 0.0, ya = 0.0, yb = 0.0;
 };
-template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false, bool LINES = true>
+template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false, bool LINES = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -3307,21 +3322,42 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       }
     }
   };
+  // (LINES) the lane's two channel rows, its sample offset in an iteration,
+  // its tap slots
+  const int hl = (lane >> 3) & 1, o_l = 8 * q + 4 * hl;
+  const int64_t rla = cg * 16 + (lane & 7), rlb = rla + 8;
+  const float *xla = x + (rla < g.n_ch ? rla : g.n_ch - 1) * s_ch;
+  const float *xlb = x + (rlb < g.n_ch ? rlb : g.n_ch - 1) * s_ch;
+  const double *kll = Ks + q * 8 + hl * 4 + (lane & 3), *kll2 = Ks + 64 + q * 2 + hl;
   // one block through the guarded (edge) path
   auto guarded_block = [&](int64_t k) {
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
-    const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
-    const int64_t a = s - v;
-    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    for (int it = 0; it < nit; ++it) {
-      f4v cur[4];
+    if constexpr (LINES) {
+      const int vo = tg.nvar == 1 ? 0 : v * tab;
+      const int64_t a = s - v + o_l;
+      double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int it = 0; it < nit; ++it) {
+        f4v cur[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + mf_off<LINES>(j, q), n_t);
-      if (it == 0 || it == nit - 1) mf_mask_outside<LINES>(cur, 64 * it, q, tg.J + v, tg.J + v + L);
-      mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+        for (int r = 0; r < 4; ++r) cur[r] = mf_load_guarded(r & 1 ? xlb : xla, a + 64 * it + 32 * (r >> 1), n_t);
+        if (it == 0 || it == nit - 1) kl_mask_outside(cur, 64 * it, o_l, tg.J + v, tg.J + v + L);
+        kl_iter(kll + vo + it * KL_IT, kll2 + vo + it * KL_IT, cur, acc);
+      }
+      block_done(kl_combine(acc, hl), k);
+    } else {
+      const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
+      const int64_t a = s - v + 4 * q;
+      d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+      for (int it = 0; it < nit; ++it) {
+        f4v cur[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+        if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+        mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
+      }
+      block_done(acc0 + acc1, k);
     }
-    block_done(acc0 + acc1, k);
   };
 
   int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
@@ -3330,10 +3366,8 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   kb = uniform64(kb > k1 ? k1 : (kb < ka ? ka : kb));
   for (int64_t k = k0; k < ka; ++k) guarded_block(k);
   if (ka < kb) {
-    const int64_t rla = cg * 16 + (lane & 7), rlb = rla + 8;
-    const float *xl = LINES ? x + (rla < g.n_ch ? rla : g.n_ch - 1) * s_ch + 8 * q + 4 * ((lane >> 3) & 1)
-                            : xr + 4 * q;
-    const int64_t dlb = LINES ? ((rlb < g.n_ch ? rlb : g.n_ch - 1) - (rla < g.n_ch ? rla : g.n_ch - 1)) * s_ch : 0;
+    const float *xl = LINES ? xla + o_l : xr + 4 * q;
+    const int64_t dlb = LINES ? xlb - xla : 0;
     auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
     int64_t k = ka, s = s0 + ka * L;
     int it = 0;
@@ -3351,7 +3385,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     };
     auto load_iter = [&](f4v (&b)[4]) {
       if constexpr (LINES) {
-        mf_load_lines(pp, pp + dlb, b);
+        kl_load(pp, pp + dlb, b);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
@@ -3364,7 +3398,9 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       produce();
     }
     const double *kt = table(s);
+    int ko = tg.nvar == 1 ? 0 : (int)(s & 3) * tab;  // (LINES) the row shift's table
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    double accl[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     bool fin = false;
     while (!fin) {
 #pragma unroll
@@ -3377,22 +3413,29 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
-        } else {
-          if constexpr (LINES) {
-            mf_lines_swap(buf[u][0], buf[u][1]);
-            mf_lines_swap(buf[u][2], buf[u][3]);
+        } else if constexpr (LINES) {
+          if ((it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen)) {
+            const int v = (int)(s & 3);
+            kl_mask_outside(buf[u], 64 * it, o_l, tg.J + v, tg.J + v + L);
           }
+          kl_iter(kll + ko + it * KL_IT, kll2 + ko + it * KL_IT, buf[u], accl);
+        } else {
           // every chunk's first and last full block is a run end, and inside
           // a run the out-of-block samples belong to the run's own blocks:
           // only a run's first and last iteration need the finite mask
           if ((it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen)) {
             const int v = (int)(s & 3);
-            mf_mask_outside<LINES>(buf[u], 64 * it, q, tg.J + v, tg.J + v + L);
+            mf_mask_outside(buf[u], 64 * it + 4 * q, tg.J + v, tg.J + v + L);
           }
           mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
         }
         if (++it == nit) {
-          const d4v a = acc0 + acc1;
+          d4v a = acc0 + acc1;
+          if constexpr (LINES) {
+            a = kl_combine(accl, hl);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) accl[i] = 0.0;
+          }
           if (MODE == 4) {
             Y0[(cg * g.nb + k) * 16 + col] = a[q & 3];
           } else {
@@ -3408,6 +3451,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
             break;
           }
           kt = table(s);
+          ko = tg.nvar == 1 ? 0 : (int)(s & 3) * tab;
         }
       }
     }
@@ -3518,7 +3562,7 @@ __device__ __forceinline__ void tm_load_buf(__amdgpu_buffer_rsrc_t rs, uint32_t 
 // taps and RUN_CST_S constants; no backward sweep at run ends, during which
 // a wave issued no loads.  MINW: waves per SIMD the registers are capped for
 // (production: 256-thread groups, 2 per SIMD: 8 waves per CU, the occupancy
-// at which this access shape streams fastest, profiles/r03_ubench_tm.txt).
+// at which this access shape streams fastest, profiles/archive_r01_r03.md (r03_ubench_tm.txt)).
 // MODE 0: production.  Diagnostics (timing only, results invalid;
 // LFD_TM_MODE): 3 = loads only (a VALU sum of the samples, no MFMA, no run
 // epilogue, no stores) = the floor of this access shape; 4 = loads + MFMAs,
@@ -3823,7 +3867,7 @@ hipError_t launch_block_runs_mfma_tm(const float *x, int64_t s_t, int64_t n_t, c
   if (x2 && s_t < (int64_t)1 << 22) {
     // buffer loads at prefetch depth 1 (14.01 vs 14.18 ms) with the streaming
     // run epilogue, taps + constants only in LDS (13.85 vs 14.35 ms) on cfg3
-    // stored time-major (profiles/r03_ab_tm_sepi.txt); 256-thread groups (4
+    // stored time-major (profiles/archive_r01_r03.md (r03_ab_tm_sepi.txt)); 256-thread groups (4
     // per CU, registers for 2 waves per SIMD as before): 13.06 vs 13.50 ms
     // median against 512-thread groups, bit-identical; 128-thread groups 15.03
     // (profiles/r04q_ab_tm_w.txt)
@@ -3868,15 +3912,11 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0, true>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0, false>),
+    for (const void *fn : {reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 0>),
 #ifdef LFD_DIAG
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1, true>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3, true>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6, true>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1, false>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3, false>),
-                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6, false>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 1>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 3>),
+                           reinterpret_cast<const void *>(&k_block_functionals_mfma<2, 6>),
 #endif
                            }) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3923,15 +3963,9 @@ hipError_t launch_block_functionals_mfma(const float *x, int64_t s_ch, int64_t n
   const int64_t n_runs = (g.nb + bpw - 1) / bpw;
   const int64_t units = n_cg * n_runs;
   const unsigned grid = nblk(units, threads / 64);
-#define LFD_MF(PF_, MODE_)                                                                                    \
-  do {                                                                                                        \
-    if (tg.lines)                                                                                             \
-      k_block_functionals_mfma<PF_, MODE_, true><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F,   \
-                                                                             n_runs, bpw);                    \
-    else                                                                                                      \
-      k_block_functionals_mfma<PF_, MODE_, false><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F,  \
-                                                                              n_runs, bpw);                   \
-  } while (0)
+#define LFD_MF(PF_, MODE_)                                                                      \
+  k_block_functionals_mfma<PF_, MODE_><<<grid, threads, lds, st>>>(x, s_ch, n_t, g, taps, tg, F, \
+                                                                   n_runs, bpw)
 #ifdef LFD_DIAG
   // timing-only modes (results invalid, LFD_MF_MODE): 1 loads only, 3 no
   // stores, 6 stores into an L2-resident window
@@ -3961,12 +3995,15 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   const size_t lds = LAT ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
                          : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  auto kern = tg.lines ? &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, true>
+  // (whole-line products: 4th-order channel-major plans, lfd_capi.cpp tg_l)
+  constexpr bool LN = !LAT;
+  if (tg.lines && (LAT || tg.nc != 2 * RUN_N + 1)) return hipErrorInvalidValue;
+  auto kern = tg.lines ? &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, LN>
                        : &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, false>;
   static std::once_flag attr_once;
   hipError_t ea = hipSuccess;
   std::call_once(attr_once, [&] {
-    for (const void *fn : {reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, true>),
+    for (const void *fn : {reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, LN>),
                            reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, false>)})
       if (ea == hipSuccess)
         ea = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
@@ -3983,7 +4020,7 @@ hipError_t launch_block_runs_mfma(const float *x, int64_t s_ch, int64_t n_t, con
   const int64_t units = ((g.n_ch + 15) / 16) * rg.n_groups;
   // 512-thread workgroups (2 per CU: 16 waves), prefetch depth 1, registers
   // capped for 4 waves per SIMD: 12.77 ms vs 13.09-13.12 for depth 2 at the
-  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/r02_ab_k1_minw.txt)
+  // compiler's 144 VGPRs on cfg3 (in-process A/B, profiles/archive_r01_r03.md (r02_ab_k1_minw.txt))
 #ifdef LFD_DIAG
   // timing-only modes (results invalid): LFD_RUN_MODE=1 loads only, =4 no run epilogue
   if (const char *v = knob("LFD_RUN_MODE")) {
@@ -4891,12 +4928,12 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
     *scan_used = LFD_SCAN_DEFERRED;
     // narrow shards: 64-thread workgroups (one wave per CU instead of four
     // sharing one): 1,250 channels 0.150 -> 0.126 ms, bit-identical
-    // (profiles/r03_ab_scan_narrow.txt; A/B knob LFD_SCAN_DEFER_THREADS)
+    // (profiles/archive_r01_r03.md (r03_ab_scan_narrow.txt); A/B knob LFD_SCAN_DEFER_THREADS)
     int dthr = n_chunks * g.n_ch < 40000 ? 64 : 256;
     if (const char *tv = knob("LFD_SCAN_DEFER_THREADS")) dthr = std::atoi(tv) == 64 ? 64 : (std::atoi(tv) == 128 ? 128 : 256);
     const unsigned nb = nblk(n_chunks * g.n_ch, dthr);
     // 16 / 8 runs in flight instead of 4 / 2: dt = 10 s at 1 kHz 0.401 ->
-    // 0.352 ms (profiles/r03_ab_scan_deep.txt); the 1,250- / 2,500-channel
+    // 0.352 ms (profiles/archive_r01_r03.md (r03_ab_scan_deep.txt)); the 1,250- / 2,500-channel
     // shards' scan kernel 90.6 -> 74.4 / 99.6 -> 78.3 us by rocprofv3 kernel
     // trace (profiles/r04l_scan_deep.txt); bit-identical (A/B knob
     // LFD_SCAN_DEEP=0/1)
@@ -5355,7 +5392,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // lanes load their 8 positions directly, outputs leave through LDS as
     // coalesced float4 stores (cfg2 at S = 1: 4.77 ms vs 5.93 with the loads
     // staged through LDS too; deeper prefetch and 4 waves per SIMD measured
-    // slower: profiles/r02_ab_roll_*.txt, r05_roll_scan_ab.txt)
+    // slower: profiles/archive_r01_r03.md (r02_ab_roll_)*.txt, r05_roll_scan_ab.txt)
     // the per-step wave scan on DPP lane moves (A/B knob LFD_ROLL_DPP=0: shuffles)
     bool dpp = true;
     if (const char *v = knob("LFD_ROLL_DPP")) dpp = std::atoi(v) != 0;
@@ -5513,7 +5550,7 @@ constexpr int fdm_rl() {
   return a < b ? a : b;
 }
 // (one X buffer, two barriers per tile, 3 workgroups per CU; a double-buffered
-// X at 1 workgroup per CU measured slower, profiles/r03_ab_fir.txt)
+// X at 1 workgroup per CU measured slower, profiles/archive_r01_r03.md (r03_ab_fir.txt))
 template <int Q>
 constexpr size_t fdm_lds_bytes() {
   return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32);

@@ -4,9 +4,9 @@ knobs on one input allocation, alternating:
     python tools/roll_ab.py W S "SPEC" "SPEC" ...     (SPEC: NAME=VALUE ..., "" = defaults)
 
 e.g. the segment prefix-sum kernel against the running-sum scan
-(``1000 250 "" "LFD_ROLL_SEGSUM=0"``, profiles/r03_ab_roll_segsum.txt) or the
+(``1000 250 "" "LFD_ROLL_SEGSUM=0"``, profiles/archive_r01_r03.md (r03_ab_roll_segsum.txt)) or the
 scan's LDS ring / DPP steps (``1000 1 "" "LFD_ROLL_RING=0" "LFD_ROLL_DPP=0"``,
-profiles/r02_ab_roll_ring.txt).  Loads liblfdas_diag.so (the product library
+profiles/archive_r01_r03.md (r02_ab_roll_ring.txt)).  Loads liblfdas_diag.so (the product library
 reads no environment); every variant's output is compared with the first
 spec's after a NaN fill."""
 import os
