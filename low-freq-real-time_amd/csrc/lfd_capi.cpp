@@ -1059,10 +1059,9 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
         sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 8 * lfd::RUN_R * 5 * 16) <=
             (size_t)lfd::TAP_LDS_MAX;
     // the whole-line products (lfd_kernels.hip kl_iter: 9 functionals, the
-    // same LDS size); the diagnostic build's LFD_K1_LINES=0 keeps the
-    // 16-rows x 64-B order (A/B)
+    // same LDS size): the diagnostic build's LFD_K1_LINES=1 (A/B)
     if (p->run_mfma_ok && p->tg.nc == 2 * lfd::RUN_N + 1 && n_off == 0 &&
-        !(lfd::knob("LFD_K1_LINES") && std::atoi(lfd::knob("LFD_K1_LINES")) == 0)) {
+        lfd::knob("LFD_K1_LINES") && std::atoi(lfd::knob("LFD_K1_LINES")) == 1) {
       p->tg_l = p->tg;
       p->tg_l.lines = 1;
     }
