@@ -762,8 +762,6 @@ struct lfd_lowpass_plan {
   std::vector<double> taps;      // natural layout [nc][L+J]
   lfd::TapGeom tg{};
   double *d_taps = nullptr;      // device layout (lfd_internal.h TapGeom)
-  lfd::TapGeom tg_l{};           // the run-mode K1's whole-line table (lines = 1; Lp = 0: none)
-  double *d_taps_l = nullptr;
   lfd::TapGeom tg_tm{};          // (time, channel) rows: one table, row shift 0
   double *d_taps_tm = nullptr;
   // run mode (lfd_internal.h RunConst): run table, K1 units, constants
@@ -1058,13 +1056,6 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     p->run_mfma_ok = !p->taps.empty() &&
         sizeof(double) * ((size_t)p->tg.Lp * p->tg.nc * p->tg.nvar + 64 + 8 * lfd::RUN_R * 5 * 16) <=
             (size_t)lfd::TAP_LDS_MAX;
-    // the whole-line products (lfd_kernels.hip kl_iter: 9 functionals, the
-    // same LDS size): the diagnostic build's LFD_K1_LINES=1 (A/B)
-    if (p->run_mfma_ok && p->tg.nc == 2 * lfd::RUN_N + 1 && n_off == 0 &&
-        lfd::knob("LFD_K1_LINES") && std::atoi(lfd::knob("LFD_K1_LINES")) == 1) {
-      p->tg_l = p->tg;
-      p->tg_l.lines = 1;
-    }
     // (time, channel) rows: k_block_runs_mfma_tm reads each block row from
     // its first sample (no 16-B shift): one table, shift 0; its 512-thread
     // workgroup holds 8 waves x 2 channel tiles of run buffers
@@ -1325,28 +1316,10 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
           for (int cc = 0; cc < tg.nc; ++cc)
             for (int el = 0; el < 4; ++el) {
               const int pos = 16 * t + 4 * q + el - v;
-              if (pos >= 0 && pos < row && !tg.lines)
+              if (pos >= 0 && pos < row)
                 dev[vi * tab + ((size_t)(t * 4 + q) * tg.nc + cc) * 4 + el] =
                     p->taps[(size_t)cc * row + pos];
             }
-      // whole-line order (lfd_kernels.hip kl_iter): per 64-sample iteration
-      // it, half sh, component e: [g0: 32 | g1: 32 | g2: 8], g0 / g1 slot
-      // k 8 + h 4 + i = functional 4 g + i at iteration offset 32 sh + 8 k +
-      // 4 h + e; g2 slot k 2 + h = functional 8 (p0) there
-      for (int it = 0; tg.lines && it < tg.Lp / 64; ++it)
-        for (int sh = 0; sh < 2; ++sh)
-          for (int el = 0; el < 4; ++el)
-            for (int k = 0; k < 4; ++k)
-              for (int h = 0; h < 2; ++h) {
-                const int pos = 64 * it + 32 * sh + 8 * k + 4 * h + el - v;
-                if (pos < 0 || pos >= row) continue;
-                double *d = dev.data() + vi * tab + (size_t)it * 576 + (sh * 4 + el) * 72;
-                for (int i = 0; i < 4; ++i) {
-                  d[k * 8 + h * 4 + i] = p->taps[(size_t)i * row + pos];
-                  d[32 + k * 8 + h * 4 + i] = p->taps[(size_t)(4 + i) * row + pos];
-                }
-                d[64 + k * 2 + h] = p->taps[(size_t)8 * row + pos];
-              }
     }
     hipError_t e2 = hipMalloc(dst, dev.size() * sizeof(double));
     if (e2 == hipSuccess)
@@ -1354,7 +1327,6 @@ static int plan_create_uniform(lfd_lowpass_plan **out, const double *sos, int n_
     return e2;
   };
   if (e == hipSuccess && !p->taps.empty()) e = upload_taps(p->tg, &p->d_taps);
-  if (e == hipSuccess && p->tg_l.Lp > 0) e = upload_taps(p->tg_l, &p->d_taps_l);
   if (e == hipSuccess && p->tg_tm.Lp > 0) e = upload_taps(p->tg_tm, &p->d_taps_tm);
   if (e == hipSuccess && p->run_ok) {
     e = hipMalloc(&p->d_run_ks, sizeof(int64_t) * p->run_ks.size());
@@ -1742,10 +1714,7 @@ int lfd::lowpass_execute_gen(const lfd_lowpass_plan *p, const float *x, int64_t 
     double *AG = reinterpret_cast<double *>(ws + p->off_AG);
     double *SR = reinterpret_cast<double *>(ws + p->off_SR);
     if (mfma_runs) {
-      if (p->d_taps_l)
-        LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps_l, p->tg_l, rg, Y0, AG, st));
-      else
-        LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
+      LFD_HIP(lfd::launch_block_runs_mfma(x, s_ch, p->n_t, p->bg, p->d_taps, p->tg, rg, Y0, AG, st));
     } else if (mfma_tm) {
       LFD_HIP(lfd::launch_block_runs_mfma_tm(x, s_t, p->n_t, p->bg, p->d_taps_tm, p->tg_tm, rg, Y0, AG, st));
     } else {
@@ -1889,7 +1858,6 @@ void lfd_lowpass_plan_destroy(lfd_lowpass_plan *p) {
     if (d) (void)hipFree(d);
   if (p->d_chunks) (void)hipFree(p->d_chunks);
   if (p->d_taps) (void)hipFree(p->d_taps);
-  if (p->d_taps_l) (void)hipFree(p->d_taps_l);
   if (p->d_taps_tm) (void)hipFree(p->d_taps_tm);
   for (void *d : {(void *)p->d_run_ks, (void *)p->d_run_len, (void *)p->d_group_r0, (void *)p->d_rc,
                   (void *)p->d_slot_chunk})

@@ -155,7 +155,6 @@ struct TapGeom {
   int nc;       // functionals per block (<= 16: one MFMA row tile)
   int nvar;     // 1: single shift v0 for every block; 4: table index = shift
   int v0;
-  int lines = 0;  // 1: the whole-line run-mode K1's table (lfd_kernels.hip kl_iter; nc = 9)
 };
 constexpr int TAP_LDS_MAX = 160 * 1024;  // taps must fit one workgroup's LDS
 

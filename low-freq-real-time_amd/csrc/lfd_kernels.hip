@@ -2825,6 +2825,7 @@ __device__ __forceinline__ void mf_mask_outside(f4v (&cur)[4], int o0, int lo, i
     }
 }
 
+
 // 16 MFMAs of one 64-sample iteration: taps kt (this lane's A column) x cur.
 // Lanes of A rows c >= nc read a copy of row nc-1 instead of zeros: MFMA rows
 // are independent (D[c][:] depends on A[c][:] only) and rows >= nc of D are
@@ -2856,6 +2857,13 @@ __device__ __forceinline__ void mf_store(const d4v &acc0, const d4v &acc1, doubl
     if (q + 4 * r < nc) Fo[(q + 4 * r) * F_CSTRIDE] = acc[r];
 }
 
+// (Round 6, measured and not kept: whole 128-B lines per wave instruction —
+// 8 rows x 128 B, which streams 2-4 % faster loads-only at full width and
+// 10 % at an 8-GPU shard (profiles/r06_k1_shape.txt) — either moved into this
+// layout by 16 DPP row exchanges per iteration (1-1.5 % slower,
+// profiles/r06_k1_lines_ab.txt) or fed as is to 4x4x4_4b products whose blocks
+// take the taps of their piece parity (3-7 % slower,
+// profiles/r06_k1_lines4x4_ab.txt).)
 // (non-temporal loads of the sample stream were measured 40 % slower on cfg3:
 // 18.5 vs 13.1 ms — the 64-B row pieces of consecutive iterations no longer
 // meet in L2)
@@ -2924,10 +2932,6 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
   // iterations are in flight behind the current iteration's MFMAs
   const float *xl = xr + 4 * q;
   auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
-  auto load_it = [&](const float *p, f4v (&b)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = ldx4(p + 16 * j);
-  };
   int64_t k = ka, s = s0 + ka * L;  // consumer position
   int it = 0;
   int64_t kp = ka, sp = s;          // producer position
@@ -2948,7 +2952,8 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
   f4v buf[PF + 1][4];
 #pragma unroll
   for (int d = 0; d < PF; ++d) {
-    load_it(pp, buf[d]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) buf[d][j] = ldx4(pp + 16 * j);
     produce();
   }
   const double *kt = table(s);
@@ -2961,7 +2966,8 @@ __global__ __launch_bounds__(1024) void k_block_functionals_mfma(
     for (int u = 0; u <= PF; ++u) {
       constexpr int NB = PF + 1;
       const int lb = (u + PF) % NB;
-      load_it(pp, buf[lb]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) buf[lb][j] = ldx4(pp + 16 * j);
       produce();
       if (MODE == 1 || MODE == 3) {
 #pragma unroll
@@ -3071,77 +3077,6 @@ __device__ __forceinline__ void run_block_stream(const double *__restrict__ cst,
   st.yb = db >= 0 ? yb : (db == -1 ? pg : st.yb);
 }
 
-// ---- whole-line K1 (TapGeom::lines, 4th-order cascades, nc = 9) ----
-// A wave-instruction of K1's sample stream reads 8 whole 128-B lines: lane
-// 16 k + 8 h + m reads 16 B of channel row m (registers 0, 2) or 8 + m (1, 3)
-// at iteration offset 8 k + 4 h (+ 32 for registers 2, 3).  Loads alone, this
-// shape streams at 0.749-0.775 of HBM vs 0.734-0.746 for 16 rows x 64 B at
-// cfg3's 10,000 channels, 0.70-0.71 vs 0.64 at an 8-GPU shard's 1,248
-// (profiles/r06_k1_shape.txt).  Moving the samples into the 16x16x4 layout
-// (channel = lane & 15) costs 16 DPP exchanges per iteration, more than the
-// shape gains (profiles/r06_k1_lines_ab.txt); instead the products run as
-// v_mfma_f64_4x4x4_4b, whose blocks b = (lane >> 2) & 3 each take their own A:
-// block b holds channels 4 (b & 1) + j (+ 8 for registers 1, 3) at pieces
-// 2k + (b >> 1), so its A is the taps of that piece parity.  Three such
-// products per (register, sample) give functionals 4g + i (g = 0, 1, 2; the
-// p0 row 8 alone in g = 2), in 6 accumulators (channel half x g); at a
-// block's end the two parities of a channel (lanes 8 apart) are summed and
-// lane (q, col) then holds functional 4 g + q of channel col: the 16x16x4
-// layout's a[g], so the run epilogue is unchanged.  The MFMA issue is 48 x
-// 4x4x4 (18.5 cycles) instead of 16 x 16x16x4 (87) per iteration.
-// Tap table per 64-sample iteration: [s][e][g0: 32 | g1: 32 | g2: 8] doubles
-// (576), g0 / g1 indexed k 8 + h 4 + i, g2 k 2 + h: Lp x 9 doubles per row
-// shift, the 16x16x4 table's size (lfd_capi.cpp upload_taps).
-constexpr int KL_IT = 576;  // doubles per 64-sample iteration
-constexpr int KL_SE = 72;   // doubles per (half s, component e)
-__device__ __forceinline__ void kl_load(const float *pa, const float *pb, f4v (&b)[4]) {
-  b[0] = *reinterpret_cast<const f4u *>(pa);
-  b[1] = *reinterpret_cast<const f4u *>(pb);
-  b[2] = *reinterpret_cast<const f4u *>(pa + 32);
-  b[3] = *reinterpret_cast<const f4u *>(pb + 32);
-}
-// finite mask (as mf_mask_outside) for the lane's samples at iteration offsets
-// 32 (r >> 1) + o_l + e, o_l = 8 k + 4 h
-__device__ __forceinline__ void kl_mask_outside(f4v (&cur)[4], int o_it, int o_l, int lo, int hi) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int o = o_it + 32 * (r >> 1) + o_l + e;
-      if ((o < lo || o >= hi) && !__builtin_isfinite(cur[r][e])) cur[r][e] = 0.0f;
-    }
-}
-// the 48 products of one iteration; kt = this iteration's table + the lane's
-// (g0, g1) slot, kt2 = its g2 slot
-__device__ __forceinline__ void kl_iter(const double *kt, const double *kt2, const f4v (&cur)[4], double (&acc)[6]) {
-#pragma unroll
-  for (int sh = 0; sh < 2; ++sh)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int o = (sh * 4 + e) * KL_SE;
-      const double a0 = kt[o], a1 = kt[o + 32], a2 = kt2[o];
-      const double b0 = (double)cur[2 * sh][e], b1 = (double)cur[2 * sh + 1][e];
-      acc[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, b0, acc[0], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, b1, acc[3], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, b0, acc[1], 0, 0, 0);
-      acc[4] = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, b1, acc[4], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, b0, acc[2], 0, 0, 0);
-      acc[5] = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, b1, acc[5], 0, 0, 0);
-    }
-}
-// parities summed (DPP row_ror:8), lanes h = 1 take the channels 8..15
-__device__ __forceinline__ d4v kl_combine(const double (&acc)[6], bool h) {
-  d4v a;
-#pragma unroll
-  for (int gg = 0; gg < 3; ++gg) {
-    const double t0 = acc[gg] + dpp_row_d<0x128>(acc[gg]);
-    const double t1 = acc[3 + gg] + dpp_row_d<0x128>(acc[3 + gg]);
-    a[gg] = h ? t1 : t0;
-  }
-  a[3] = 0.0;
-  return a;
-}
-
 constexpr int RUN_WB = RUN_R * 5 * 16;  // doubles per wave run buffer
 constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 
@@ -3163,7 +3098,7 @@ constexpr int RUN_CST = 64;             // doubles of epilogue constants in LDS
 struct LatAcc {
   double S0 = 0.0, T1 = 0.0, v0 = 0.0, ya = 0.0, yb = 0.0;
 };
-template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false, bool LINES = false>
+template <int PF, int MODE = 0, int NT = 512, int MINW = 0, bool LAT = false>
 __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
     const float *__restrict__ x, int64_t s_ch, int64_t n_t, BlockGeom g,
     const double *__restrict__ taps, TapGeom tg, RunGeom rg, double *__restrict__ Y0,
@@ -3322,42 +3257,21 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       }
     }
   };
-  // (LINES) the lane's two channel rows, its sample offset in an iteration,
-  // its tap slots
-  const int hl = (lane >> 3) & 1, o_l = 8 * q + 4 * hl;
-  const int64_t rla = cg * 16 + (lane & 7), rlb = rla + 8;
-  const float *xla = x + (rla < g.n_ch ? rla : g.n_ch - 1) * s_ch;
-  const float *xlb = x + (rlb < g.n_ch ? rlb : g.n_ch - 1) * s_ch;
-  const double *kll = Ks + q * 8 + hl * 4 + (lane & 3), *kll2 = Ks + 64 + q * 2 + hl;
   // one block through the guarded (edge) path
   auto guarded_block = [&](int64_t k) {
     const int64_t s = s0 + k * L;
     const int v = (int)(((s % 4) + 4) % 4);
-    if constexpr (LINES) {
-      const int vo = tg.nvar == 1 ? 0 : v * tab;
-      const int64_t a = s - v + o_l;
-      double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      for (int it = 0; it < nit; ++it) {
-        f4v cur[4];
+    const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
+    const int64_t a = s - v + 4 * q;
+    d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int it = 0; it < nit; ++it) {
+      f4v cur[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cur[r] = mf_load_guarded(r & 1 ? xlb : xla, a + 64 * it + 32 * (r >> 1), n_t);
-        if (it == 0 || it == nit - 1) kl_mask_outside(cur, 64 * it, o_l, tg.J + v, tg.J + v + L);
-        kl_iter(kll + vo + it * KL_IT, kll2 + vo + it * KL_IT, cur, acc);
-      }
-      block_done(kl_combine(acc, hl), k);
-    } else {
-      const double *kt = tg.nvar == 1 ? kl : kl + v * tab;
-      const int64_t a = s - v + 4 * q;
-      d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-      for (int it = 0; it < nit; ++it) {
-        f4v cur[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
-        if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
-        mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
-      }
-      block_done(acc0 + acc1, k);
+      for (int j = 0; j < 4; ++j) cur[j] = mf_load_guarded(xr, a + 64 * it + 16 * j, n_t);
+      if (it == 0 || it == nit - 1) mf_mask_outside(cur, 64 * it + 4 * q, tg.J + v, tg.J + v + L);
+      mf_iter(kt + (4 * it) * kstride, kstride, colv, cur, acc0, acc1);
     }
+    block_done(acc0 + acc1, k);
   };
 
   int64_t ka = s0 < 0 ? (-s0 + L - 1) / L : 0;
@@ -3366,8 +3280,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
   kb = uniform64(kb > k1 ? k1 : (kb < ka ? ka : kb));
   for (int64_t k = k0; k < ka; ++k) guarded_block(k);
   if (ka < kb) {
-    const float *xl = LINES ? xla + o_l : xr + 4 * q;
-    const int64_t dlb = LINES ? xlb - xla : 0;
+    const float *xl = xr + 4 * q;
     auto addr = [&](int64_t ss, int ii) { return xl + (ss & ~(int64_t)3) + 64 * ii; };
     int64_t k = ka, s = s0 + ka * L;
     int it = 0;
@@ -3384,12 +3297,8 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       pp = addr(sp, itp);
     };
     auto load_iter = [&](f4v (&b)[4]) {
-      if constexpr (LINES) {
-        kl_load(pp, pp + dlb, b);
-      } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
-      }
+      for (int j = 0; j < 4; ++j) b[j] = ldx4(pp + 16 * j);
     };
     f4v buf[PF + 1][4];
 #pragma unroll
@@ -3398,9 +3307,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
       produce();
     }
     const double *kt = table(s);
-    int ko = tg.nvar == 1 ? 0 : (int)(s & 3) * tab;  // (LINES) the row shift's table
     d4v acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    double accl[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     bool fin = false;
     while (!fin) {
 #pragma unroll
@@ -3413,12 +3320,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc0[j] += (double)(buf[u][j].x + buf[u][j].y + buf[u][j].z + buf[u][j].w);
-        } else if constexpr (LINES) {
-          if ((it == 0 && k == rks) || (it == nit - 1 && k + 1 == rks + rlen)) {
-            const int v = (int)(s & 3);
-            kl_mask_outside(buf[u], 64 * it, o_l, tg.J + v, tg.J + v + L);
-          }
-          kl_iter(kll + ko + it * KL_IT, kll2 + ko + it * KL_IT, buf[u], accl);
         } else {
           // every chunk's first and last full block is a run end, and inside
           // a run the out-of-block samples belong to the run's own blocks:
@@ -3430,12 +3331,7 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
           mf_iter(kt + (4 * it) * kstride, kstride, colv, buf[u], acc0, acc1);
         }
         if (++it == nit) {
-          d4v a = acc0 + acc1;
-          if constexpr (LINES) {
-            a = kl_combine(accl, hl);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) accl[i] = 0.0;
-          }
+          const d4v a = acc0 + acc1;
           if (MODE == 4) {
             Y0[(cg * g.nb + k) * 16 + col] = a[q & 3];
           } else {
@@ -3451,7 +3347,6 @@ __global__ __launch_bounds__(NT, MINW > 0 ? MINW : 1) void k_block_runs_mfma(
             break;
           }
           kt = table(s);
-          ko = tg.nvar == 1 ? 0 : (int)(s & 3) * tab;
         }
       }
     }
@@ -3995,18 +3890,12 @@ hipError_t run_k1(const float *x, int64_t s_ch, int64_t n_t, const BlockGeom &g,
   const size_t lds = LAT ? sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST_S)
                          : sizeof(double) * ((size_t)tg.Lp * tg.nc * tg.nvar + RUN_CST + (MODE == 4 ? 0 : W) * RUN_WB);
   if (lds > (size_t)TAP_LDS_MAX) return hipErrorInvalidValue;
-  // (whole-line products: 4th-order channel-major plans, lfd_capi.cpp tg_l)
-  constexpr bool LN = !LAT;
-  if (tg.lines && (LAT || tg.nc != 2 * RUN_N + 1)) return hipErrorInvalidValue;
-  auto kern = tg.lines ? &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, LN>
-                       : &k_block_runs_mfma<PF, MODE, NT, MINW, LAT, false>;
+  auto kern = &k_block_runs_mfma<PF, MODE, NT, MINW, LAT>;
   static std::once_flag attr_once;
   hipError_t ea = hipSuccess;
   std::call_once(attr_once, [&] {
-    for (const void *fn : {reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, LN>),
-                           reinterpret_cast<const void *>(&k_block_runs_mfma<PF, MODE, NT, MINW, LAT, false>)})
-      if (ea == hipSuccess)
-        ea = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, TAP_LDS_MAX);
+    ea = hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             TAP_LDS_MAX);
   });
   if (ea != hipSuccess) return ea;
   kern<<<nblk(units, W), NT, lds, st>>>(x, s_ch, n_t, g, taps, tg, rg, Y0, AG);
