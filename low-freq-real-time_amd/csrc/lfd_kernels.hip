@@ -5415,12 +5415,16 @@ __global__ __launch_bounds__(FD_THREADS) void k_fir_decimate(const float *__rest
 // 16k + 4b + j, D[i][j] at 16i + 4b + j.  Blocks b = 4 consecutive output
 // groups, j = 4 channels: one MFMA = 16 outputs x 4 channels x 4 indices;
 // a wave owns 64 consecutive outputs (4 accumulators) of 4 channels.
-// A workgroup (NW waves) stages its 4 channels' span of input through LDS as
-// the q polyphase rows X_v (coalesced reads, zeros outside the record; row
-// starts offset so one B read — 4 rows x 16 consecutive indices — hits 64
-// distinct banks); the A pieces sit in LDS ([v][d][16 lanes]).  Each B value
-// read from LDS (one ds_read_b32 + cvt) feeds every (tile, d) pair with the
-// same index offset.  Slots of the Toeplitz pieces outside a row's taps
+// A workgroup (4 waves) stages its 4 channels' span of input in LDS by
+// LDS-DMA (global_load_lds_dwordx4, wave w = channel w, 1 KB per
+// instruction, no VGPRs, no ds_write): the raw sample image, from which a B
+// read takes polyphase row v, index n as sample n q + q - 1 - v (a stride-q
+// ds_read_b32; the channels' image bases are offset so one B read — 4 rows x
+// 16 consecutive indices — hits distinct banks, fdd_bank_offsets).  Tiles
+// whose span leaves the record, or rows that are not 16-B aligned, stage
+// through registers into the same image (zeros outside the record).  The A
+// pieces sit in LDS ([v][d][16 lanes]).  Each B value (one ds_read_b32 +
+// cvt) feeds every (tile, d) pair with the same index offset.  Slots of the Toeplitz pieces outside a row's taps
 // multiply neighbouring samples by 0, so a non-finite sample there would
 // poison a finite output: every non-finite result is recomputed by the
 // direct sum (SciPy's value: NaN / +-inf exactly where 0 * NaN, inf * h
@@ -5433,54 +5437,44 @@ __global__ __launch_bounds__(FD_THREADS) void k_fir_decimate(const float *__rest
 constexpr int FDM_DM = 6;
 constexpr int FDM_NO = 256;                          // outputs per tile: 4 waves x 64
 constexpr int FDM_NN = FDM_NO + 4 * (FDM_DM - 1) + 1;  // polyphase indices per tile (+1: the u = 21 tap)
-// row length >= NN and = +-4 (mod 32): staging writes <= 2-way conflicts
-constexpr int fdm_rl() {
-  const int a = FDM_NN + ((4 - FDM_NN) % 32 + 32) % 32, b = FDM_NN + ((28 - FDM_NN) % 32 + 32) % 32;
-  return a < b ? a : b;
-}
-// (one X buffer, two barriers per tile, 3 workgroups per CU; a double-buffered
-// X at 1 workgroup per CU measured slower, profiles/archive_r01_r03.md (r03_ab_fir.txt))
+// Staging (round 6): the LDS-DMA image replaced register staging into the
+// polyphase rows (16-B global loads, then per-element ds_write at computed
+// row / index): 1.540 -> 1.497 ms at q = 10, 1.745 -> 1.676 at q = 5 on
+// 2,000 x 600,000, bit-identical (profiles/r06_fir_dma_ab.txt).  Single
+// buffer: fill, barrier, products, barrier; 3 workgroups per CU (53 KB of
+// LDS each) overlap one group's fill with the others' products (a
+// double-buffered image at 1 workgroup per CU measured slower,
+// profiles/archive_r01_r03.md (r03_ab_fir.txt)).  A scheduling barrier
+// closes every phase: without it the compiler hoisted the next phase's
+// f32 -> f64 conversions — and so the wait for that phase's LDS reads —
+// into this phase's first MFMAs (1.648 -> 1.565 ms, profiles/r05_fir_sched.txt).
+// cj: the channel images' bank offsets (launcher).
 template <int Q>
-constexpr size_t fdm_lds_bytes() {
-  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * (Q * fdm_rl() + 32);
+constexpr int fdd_nrd() { return (FDM_NN * Q + 3 + 255) / 256; }
+template <int Q>
+constexpr int fdd_raw() { return 256 * fdd_nrd<Q>() + 32; }
+template <int Q>
+constexpr size_t fdd_lds_bytes() {
+  return sizeof(double) * Q * FDM_DM * 16 + sizeof(float) * 4 * fdd_raw<Q>();
 }
-// A scheduling barrier closes every phase: without it the compiler hoisted
-// the next phase's f32 -> f64 conversions — and so the wait for that phase's
-// LDS reads, issued at this phase's start — in between this phase's first
-// MFMAs: 2,000 x 600,000 at q = 10 1.648 -> 1.565 ms (barrier after 0 / 3 / 4
-// / 5 / 6 of the 6 Toeplitz steps: 1.648 / 1.653 / 1.623 / 1.593 / 1.565,
-// profiles/r05_fir_sched.txt)
-// The staging loads are 16-B pieces (lane 4l + 256r + e): 11 load
-// instructions per lane and tile at q = 10 instead of 44 dword loads (lane
-// l + 64r): 1.630 -> 1.539 ms at q = 10, 1.853 -> 1.763 at q = 4, bit-identical
-// (profiles/r05_fir_f4.txt)
 template <int Q>
 __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__restrict__ x, int64_t n_ch, int64_t n_t,
                                                           int64_t s_ch, const double *__restrict__ h, int n_taps,
                                                           int64_t delay, int64_t n_out, int64_t tiles_o, int strip,
                                                           double *__restrict__ y, int64_t ys_ch, int64_t ys_t,
-                                                          int diag) {
-  constexpr int DM = FDM_DM, NO = FDM_NO, NN = FDM_NN, RL = fdm_rl();
-  diag = LFD_DG(diag);                     // production: 0, the diagnostics compile out
-  constexpr int SPAN = NN * Q;             // samples per channel and tile
-  constexpr int JB = Q * RL + 32;          // j-block stride (floats)
+                                                          int4 cj, int dma_ok) {
+  constexpr int DM = FDM_DM, NO = FDM_NO, NRD = fdd_nrd<Q>(), RAW = fdd_raw<Q>();
   extern __shared__ double fdm_lds[];
   double *At = fdm_lds;                                          // [v][d][16]
-  float *Xs = reinterpret_cast<float *>(fdm_lds + Q * DM * 16);  // [j][v][RL] (+ off_j)
-  // a workgroup walks `strip` consecutive tiles of one 4-channel group; the
-  // next tile's input is loaded into registers while the current one computes
+  float *Xr = reinterpret_cast<float *>(fdm_lds + Q * DM * 16);  // [j][RAW] raw sample images
   const int64_t n_strips = (tiles_o + strip - 1) / strip;
   int64_t bid = blockIdx.x;
   const int64_t nb = (int64_t)gridDim.x;
-  // XCD-aware order: consecutive strips of one channel group on one XCD
-  // (their input halos meet in that XCD's L2)
   if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
   const int64_t cg = bid / n_strips;
   const int64_t t_begin = (bid % n_strips) * strip;
   const int64_t t_end = t_begin + strip < tiles_o ? t_begin + strip : tiles_o;
-  // row (j, v) starts at j JB + v RL + off_j; off_j puts the 4 rows of one
-  // phase at banks {0, 2, 16, 18} (mod 32): a B read is conflict-free
-  auto offj = [](int j) { return (((j & 1) * 2 + (j >> 1) * 16 - j * JB) % 32 + 32) % 32; };
+  auto cof = [&](int j) { return j == 0 ? cj.x : (j == 1 ? cj.y : (j == 2 ? cj.z : cj.w)); };
   for (int e = threadIdx.x; e < Q * DM * 16; e += blockDim.x) {
     const int l16 = e & 15, vd = e >> 4;
     const int v = vd / DM, d = vd - v * DM;
@@ -5490,84 +5484,57 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
     At[e] = (u >= 0 && ti < n_taps) ? h[ti] : 0.0;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // staging: wave w loads channel w of the group, samples m = 4 lane + e +
-  // 256 r of the tile's span (16-B pieces), polyphase row v = Q - 1 - m % Q,
-  // index m / Q
   const int64_t ch_ld = cg * 4 + w;
   const bool live = ch_ld < n_ch;
   const float *xr_ld = x + (live ? ch_ld : 0) * s_ch;
-  float *row_ld = Xs + w * JB + offj(w);
-  constexpr int NR4 = (SPAN + 255) / 256;  // 16-B pieces per lane
-  float pf4[4 * NR4];
-  auto issue = [&](int64_t Ot) {
+  float *img_ld = Xr + w * RAW + cof(w);
+  // the tile's image: samples s0a .. s0a + 256 NRD of channel w (s0a = s0
+  // rounded down to 16 B; the reads add sh = s0 - s0a)
+  auto fill = [&](int64_t Ot) {
     const int64_t s0 = (Ot - 4 * (DM - 1) - 1) * Q + delay - (Q - 1);
-    if (live && s0 >= 0 && s0 + 256 * NR4 <= n_t) {
-      const float *p = xr_ld + s0 + 4 * lane;  // (any alignment: 4-B aligned 16-B pieces)
+    const int64_t s0a = s0 & ~(int64_t)3;
+    if (!live) return;
+    if (dma_ok && s0a >= 0 && s0a + 256 * NRD <= n_t) {
+      const float *g = xr_ld + s0a + 4 * lane;
 #pragma unroll
-      for (int r = 0; r < NR4; ++r) {
-        const f4v v = *reinterpret_cast<const f4u *>(p + 256 * r);
+      for (int r = 0; r < NRD; ++r)
+        __builtin_amdgcn_global_load_lds(g + 256 * r, img_ld + 256 * r, 16, 0, 0);
+    } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pf4[4 * r + e] = v[e];
-      }
-    } else {  // record edges / channels past n_ch: clamped loads, zeros outside
-#pragma unroll
-      for (int r = 0; r < NR4; ++r)
+      for (int r = 0; r < NRD; ++r)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int64_t t = s0 + 4 * lane + e + 256 * r;
+          const int64_t t = s0a + 256 * r + 4 * lane + e;
           const int64_t tc = t < 0 ? 0 : (t >= n_t ? n_t - 1 : t);
           const float v = xr_ld[tc];
-          pf4[4 * r + e] = (live && t >= 0 && t < n_t) ? v : 0.0f;
+          img_ld[256 * r + 4 * lane + e] = (t >= 0 && t < n_t) ? v : 0.0f;
         }
     }
   };
-  auto commit = [&]() {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int ln = 4 * lane + e;
-      asm volatile("" : "+v"(ln));  // recomputed per tile, not hoisted into registers
-      const int n_l = ln / Q, r_l = ln - n_l * Q;
-      float *a0 = row_ld + (Q - 1 - r_l) * RL + n_l;
-#pragma unroll
-      for (int r = 0; r < NR4; ++r) {
-        // 256 r = f Q + c: the sample's row and index relative to the lane's
-        const int c = (256 * r) % Q, f = (256 * r) / Q;
-        const bool carry = r_l + c >= Q;
-        float *dst = a0 + (f - c * RL) + (carry ? Q * RL + 1 : 0);
-        if (256 * r + 255 < SPAN || ln + 256 * r < SPAN) *dst = pf4[4 * r + e];
-      }
-    }
-  };
-  const int jl = lane & 3;                                  // B / D channel
-  const int lane_n = 4 * ((lane >> 2) & 3) + (lane >> 4);  // B index 4b + k
-  const int lane_a = 4 * (lane >> 4) + (lane & 3);         // A slot (k, i)
+  const int jl = lane & 3;
+  const int lane_n = 4 * ((lane >> 2) & 3) + (lane >> 4);
+  const int lane_a = 4 * (lane >> 4) + (lane & 3);
   const int64_t ch = cg * 4 + jl;
   const int io = lane >> 4, bo = (lane >> 2) & 3;
-  const float *xb = Xs + jl * JB + offj(jl) + 64 * w + lane_n + 1;
-  // phase 0's tap u = 21 (row-0 outputs only): X_0[o - 21] at index 64 w + 16 t + 4 b
+  const float *xbase = Xr + jl * RAW + cof(jl);
   const double h21 = (io == 0 && 21 * Q < n_taps) ? h[21 * Q] : 0.0;
-  const float *x21 = Xs + jl * JB + offj(jl) + 64 * w + 4 * ((lane >> 2) & 3);
-  // diag (LFD_FIR_DIAG, timing breakdowns only): 1 = staging without the
-  // MFMA phase loop, 2 = MFMA phase loop without the staging
-  if ((diag & 3) != 2) issue(t_begin * NO);
   for (int64_t tt = t_begin; tt < t_end; ++tt) {
-    __syncthreads();  // the previous tile's reads of X are done
-    if ((diag & 3) != 2) commit();
-    __syncthreads();
-    // the next tile's input loads while this one computes
-    const bool pf_next = tt + 1 < t_end && (diag & 3) != 2;
-    if (pf_next) issue((tt + 1) * NO);
+    const int64_t O = tt * NO;
+    fill(O);
+    __syncthreads();  // the image has landed (the barrier waits for the DMA)
+    const int sh = (int)(((O - 4 * (DM - 1) - 1) * Q + delay - (Q - 1)) & 3);
+    // row v, index n of the polyphase rows = image sample n Q + Q - 1 - v
+    const float *xb = xbase + sh + (64 * w + lane_n + 1) * Q + Q - 1;
+    const float *x21 = xbase + sh + (64 * w + 4 * bo) * Q + Q - 1;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    if ((diag & 3) != 1) {
-      // phase v: acc[t] += sum_d A_{v,d} B(index offset 4 (4t + DM - 1 - d));
-      // the next phase's A / B values load while this phase's MFMAs run
+    {
       constexpr int NB = DM + 12;
       double an[DM];
       float bn[NB];
 #pragma unroll
       for (int d = 0; d < DM; ++d) an[d] = At[d * 16 + lane_a];
 #pragma unroll
-      for (int si = 0; si < NB; ++si) bn[si] = xb[4 * si];
+      for (int si = 0; si < NB; ++si) bn[si] = xb[4 * si * Q];
 #pragma unroll
       for (int v = 0; v < Q; ++v) {
         double ac[DM], bd[NB];
@@ -5579,26 +5546,23 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
 #pragma unroll
           for (int d = 0; d < DM; ++d) an[d] = At[((v + 1) * DM + d) * 16 + lane_a];
 #pragma unroll
-          for (int si = 0; si < NB; ++si) bn[si] = xb[(v + 1) * RL + 4 * si];
+          for (int si = 0; si < NB; ++si) bn[si] = xb[4 * si * Q - (v + 1)];
         }
-        // the four tiles' accumulators alternate: dependent MFMAs sit 4 apart
 #pragma unroll
         for (int d = DM - 1; d >= 0; --d) {
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(ac[d], bd[4 * t + DM - 1 - d], acc[t], 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);  // (the phase's end: see above)
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    const int64_t O = tt * NO;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int64_t o = O + 64 * w + 16 * t + 4 * bo + io;
       if (ch >= n_ch || o >= n_out) continue;
-      double val = fma(h21, (double)x21[16 * t], acc[t]);
+      double val = fma(h21, (double)x21[16 * t * Q], acc[t]);
       if (!isfinite(val)) {
-        // direct sum (rare: a non-finite sample within reach of this output)
         const float *xr = x + ch * s_ch;
         double a2 = 0.0;
         for (int i = 0; i < n_taps; ++i) {
@@ -5609,7 +5573,34 @@ __global__ __launch_bounds__(256, 3) void k_fir_decimate_mfma(const float *__res
       }
       y[ch * ys_ch + o * ys_t] = val;
     }
+    __syncthreads();  // the image's reads are done before the next fill
   }
+}
+
+// the raw images' bank offsets: the fewest conflicts of one B read (lanes
+// 0-31: 4 channel rows x indices 4a + b, stride q floats; ds_read_b32 banks
+// (a / 4) mod 32), brute force per q
+static int4 fdd_bank_offsets(int q, int raw) {
+  int best = 1 << 30;
+  int4 bo{0, 0, 0, 0};
+  for (int c1 = 0; c1 < 32; ++c1)
+    for (int c2 = 0; c2 < 32; ++c2)
+      for (int c3 = 0; c3 < 32; ++c3) {
+        const int c[4] = {0, c1, c2, c3};
+        int cnt[32] = {0};
+        for (int l = 0; l < 32; ++l) {
+          const int j = l & 3, n = 4 * ((l >> 2) & 3) + (l >> 4);
+          ++cnt[(((j * raw + c[j] + n * q) % 32) + 32) % 32];
+        }
+        int worst = 0;
+        for (int b = 0; b < 32; ++b) worst = std::max(worst, cnt[b]);
+        if (worst < best) {
+          best = worst;
+          bo = int4{0, c1, c2, c3};
+          if (best == 1) return bo;
+        }
+      }
+  return bo;
 }
 
 hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_t s_ch, int64_t s_t,
@@ -5626,27 +5617,25 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
     if (const char *sv = knob("LFD_FIR_STRIP")) strip = std::max(1, std::atoi(sv));
     if (strip > tiles_o) strip = (int)tiles_o;
     const int64_t grid = (n_ch + 3) / 4 * ((tiles_o + strip - 1) / strip);
-    int diag = 0;  // (diag build: LFD_FIR_DIAG timing breakdowns)
-    if (const char *dv = knob("LFD_FIR_DIAG")) diag = std::atoi(dv);
     bool launched = false;
     hipError_t e = hipSuccess;
-#define LFD_FDM1(QV)                                                                                    \
-  {                                                                                                          \
-    static bool attr = false;                                                                                \
-    if (!attr) {                                                                                             \
-      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                 \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdm_lds_bytes<QV>());         \
-      if (e != hipSuccess) return e;                                                                         \
-      attr = true;                                                                                           \
-    }                                                                                                        \
-    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdm_lds_bytes<QV>(), st>>>(                         \
-        x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, diag);                  \
-  }
-#define LFD_FDM(QV)            \
-  case QV: {                   \
-    LFD_FDM1(QV)               \
-    launched = true;           \
-    break;                     \
+    // LDS-DMA needs 16-B aligned rows (else every tile stages through registers)
+    const int dma_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && s_ch % 4 == 0;
+#define LFD_FDM(QV)                                                                                      \
+  case QV: {                                                                                             \
+    static bool attr = false;                                                                            \
+    static int4 cj{};                                                                                    \
+    if (!attr) {                                                                                         \
+      e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_fir_decimate_mfma<QV>),                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)fdd_lds_bytes<QV>());     \
+      if (e != hipSuccess) return e;                                                                     \
+      cj = fdd_bank_offsets(QV, fdd_raw<QV>());                                                          \
+      attr = true;                                                                                       \
+    }                                                                                                    \
+    k_fir_decimate_mfma<QV><<<(unsigned)grid, 256, fdd_lds_bytes<QV>(), st>>>(                           \
+        x, n_ch, n_t, s_ch, h, n_taps, delay, n_out, tiles_o, strip, y, ys_ch, ys_t, cj, dma_ok);        \
+    launched = true;                                                                                     \
+    break;                                                                                               \
   }
     if (grid <= (int64_t)INT32_MAX) {
       switch (q) {
@@ -5659,7 +5648,6 @@ hipError_t launch_fir_decimate(const float *x, int64_t n_ch, int64_t n_t, int64_
       }
     }
 #undef LFD_FDM
-#undef LFD_FDM1
     if (launched) {
       if (kernel_used) *kernel_used = 1;
       return hipGetLastError();

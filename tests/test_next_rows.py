@@ -226,18 +226,21 @@ def test_fir_mfma_toeplitz_model_matches_oracle(q):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("q", [4, 10])
-def test_decimate_fir_device_nulls_and_ragged(q):
+@pytest.mark.parametrize("aligned", [False, True])
+def test_decimate_fir_device_nulls_and_ragged(q, aligned):
     """Matrix-core FIR decimation on a ragged array (6 channels: one
     partial 4-channel group; several 256-output tiles) with NaN / +-inf
     samples at tile edges, inside the zero pre-pad taps' reach and in the
     Toeplitz corners: the NaN / inf footprint and every finite value match
-    the oracle (relRMS 1e-12 over finite outputs)."""
+    the oracle (relRMS 1e-12 over finite outputs).  Odd record lengths stage
+    every tile through registers; aligned ones (16-B rows) by LDS-DMA except
+    at the record's edges."""
     import torch
     from lfdas._lib import load
     from lfdas.plan import fir_decimate_device
     from lfdas.proc import fir_decimate_design
     rng = np.random.default_rng(7 + q)
-    n_ch, n_t = 6, 256 * q * 3 + 17 * q + 5
+    n_ch, n_t = 6, (256 * q * 5 if aligned else 256 * q * 3 + 17 * q + 5)
     x = rng.standard_normal((n_ch, n_t)).astype(np.float32)
     tile = 256 * q
     x[0, tile - 1] = np.nan
