@@ -53,7 +53,7 @@ out = {
     "hbm_read_bytes_per_launch": fetch * fetch_unit,
     "hbm_write_bytes_per_launch": write * write_unit,
     "hbm_bytes_per_launch": fetch * fetch_unit + write * write_unit,
-    "algorithmic_bytes_per_launch": 10000 * 1800000 * (4.0 + 4.0 / 500),
+    "algorithmic_bytes_per_launch": 10000 * 1800000 * (4.0 + 8.0 / 500),  # float64 outputs (round 6)
     "source": src,
 }
 # rolling-mean kernels (tools/roll_only.py: cfg2 5,000 x 600,000)
