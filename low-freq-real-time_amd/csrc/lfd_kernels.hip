@@ -503,7 +503,8 @@ struct SeqR {  // sequential realization-R steps in float64 (edges)
 #endif
 // LFD_SCAN_DIAG (timing experiments only, results invalid): bit 1 skips the
 // left pad/head, 2 the forward run scan, 4 the right pad and its reverse,
-// 8 the backward run scan.
+// 8 the backward run scan, 16 the backward scan's y0 loads (zeros), 32 its
+// output stores.
 #ifdef LFD_DIAG
 __constant__ int g_scan_diag = 0;
 #endif
@@ -811,7 +812,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     static_assert(N == RUN_N, "run mode is 4th order");
     const RunConst &rc = rcs[0];
     // software-pipelined through a ring of SCAN_DF runs: the aggregates and
-    // lengths of runs r+1 .. r+SCAN_DF are in flight while run r is applied
+    // lengths of runs r+1 .. r+SCAN_DF-1 are in flight while run r is applied
     // (the step is ~150 cycles, a load ~1.5 us)
     constexpr int DF = DFT;
     const double *agb = F + (((ch >> 4) * rg.n_runs) * 8) * 16 + (ch & 15);
@@ -829,32 +830,29 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       for (int u = 0; u < DF; ++u) {
         const int64_t r = rb + u;
         if (r >= G.r1) break;
-        double agc[N];
-#pragma unroll
-        for (int i = 0; i < N; ++i) agc[i] = agq[u][i];
         const int len = lenq[u];
-        {
-          // unconditional (clamped) prefetch: a conditional load makes the
-          // compiler wait for every load in flight (vmcnt(0)) before using
-          // the ring, so the ring never overlapped anything
-          const int64_t rn = min(r + DF, G.r1 - 1);
-          lenq[u] = rg.run_len[rn];
-#pragma unroll
-          for (int i = 0; i < N; ++i) agq[u][i] = agb[(rn * 8 + i) * 16];
-        }
         double *sr = SF + sf_index(G.sr_off + (r - G.r0), 0, ch, rg.n_sr, N);
         const double *P = rc.PhiFp[len];
         double ns[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) {
           sr[i * SF_ISTRIDE] = S[i];
-          double acc = agc[i] + (r == G.r0 ? corr[i] : 0.0);
+          double acc = agq[u][i] + (r == G.r0 ? corr[i] : 0.0);
 #pragma unroll
           for (int j = 0; j < N; ++j) acc = fma(P[i * 4 + j], S[j], acc);
           ns[i] = acc;
         }
 #pragma unroll
         for (int i = 0; i < N; ++i) S[i] = ns[i];
+        {
+          // unconditional (clamped) refill of slot u after its last use: a
+          // conditional load, or a copy of the slot before refilling it,
+          // makes the compiler wait for every load in flight (vmcnt(0))
+          const int64_t rn = min(r + DF, G.r1 - 1);
+          lenq[u] = rg.run_len[rn];
+#pragma unroll
+          for (int i = 0; i < N; ++i) agq[u][i] = agb[(rn * 8 + i) * 16];
+        }
       }
     }
   }
@@ -917,12 +915,16 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       }
       // every y0 slot loaded (clamped to the plan's blocks; unused ones are
       // masked where they are consumed): a fixed number of loads per run
-      if (!DEFER) {
+      if (!DEFER && !(LFD_DG(g_scan_diag) & 16)) {
 #pragma unroll
         for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = y0b[min(o.ks + pp, g.nb - 1) * 16];
+      } else if (!DEFER) {
+#pragma unroll
+        for (int pp = 0; pp < RUN_R; ++pp) o.y0[pp] = 0.0;
       }
     };
-    // ring of SCAN_DB runs (r-1 .. r-SCAN_DB in flight while run r is applied)
+    // ring of SCAN_DB slots (runs r-1 .. r-SCAN_DB+1 in flight while run r is
+    // applied)
     constexpr int DB = DBT;
     // q[u] holds run r's inputs, gq[u] run r-DB's geometry (slot u = r mod DB)
     RunIn q[DB];
@@ -944,10 +946,10 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
     for (int u = 0; u < DB; ++u) {
       const int64_t r = rb - u;
       if (r < G.r0) break;
-      const RunIn cur = q[u];
-      // unconditional (clamped) prefetch, see the forward scan
-      load_run(max(r - DB, G.r0), gq[u], q[u]);
-      load_geo(max(r - 2 * DB, G.r0), gq[u]);
+      // slot u is applied in place and refilled after its last use (below):
+      // copying it out before the refill made the compiler wait for every
+      // load in flight (vmcnt(0)) at each step, so the ring overlapped nothing
+      const RunIn &cur = q[u];
       const int len = cur.len;
       const int64_t ks = cur.ks;
       const double *sin = cur.sin;
@@ -988,7 +990,7 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
         for (int m = 0; m < 8; ++m) {
           const int row = m * 8 + (lane >> 3);
           const double v = wl[row][e];
-          if (ok) yb[row * ys_ch] = v;
+          if (ok && !(LFD_DG(g_scan_diag) & 32)) yb[row * ys_ch] = v;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1008,6 +1010,9 @@ __global__ __launch_bounds__(256) void k_chunk_scan(
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) T[i] = nr[i];
+      // unconditional (clamped) refill of slot u, see the forward scan
+      load_run(max(r - DB, G.r0), gq[u], q[u]);
+      load_geo(max(r - 2 * DB, G.r0), gq[u]);
     }
     return;
   }
@@ -2587,6 +2592,46 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
     // ring of NPF + 1 tiles: NPF steps of loads in flight behind the step
     // being processed (indices static: the ring is unrolled)
     Tile R[NPF + 1];
+    if constexpr (RING) {
+      // whole tiles (tb + RS_P <= n_t) through the ring with unconditional
+      // buffer loads — wave-uniform row descriptor, tile base in soffset, the
+      // prefetch index clamped to the last whole tile — so each step waits
+      // only for its own tile (a conditional load made the compiler wait for
+      // every load in flight); the partial tiles at the row end afterwards
+      const __amdgpu_buffer_rsrc_t rrow =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(row), (short)0, n_t * 4, 0x00020000);
+      auto load_i = [&](int tb, Tile &T) {
+#pragma unroll
+        for (int h = 0; h < RS_E / 4; ++h) {
+          const auto a = __builtin_bit_cast(
+              f4v, __builtin_amdgcn_raw_buffer_load_b128(rrow, 4u * (uint32_t)(RS_E * lane + 4 * h), 4 * tb, 0));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T.xi[4 * h + e] = a[e];
+        }
+      };
+      const int n_tiles = (p1 - tb0) / RS_P + 1;
+      const int nI = min(n_tiles, n_t - RS_P - tb0 >= 0 ? (n_t - RS_P - tb0) / RS_P + 1 : 0);
+      if (nI > 0) {
+#pragma unroll
+        for (int d = 0; d < NPF; ++d) load_i(tb0 + min(d, nI - 1) * RS_P, R[d]);
+      }
+      halo();  // the first window's sum (its loads queue behind the ring's)
+      int i = 0;
+      while (i < nI) {
+#pragma unroll
+        for (int u = 0; u <= NPF; ++u) {
+          load_i(tb0 + min(i + NPF, nI - 1) * RS_P, R[(u + NPF) % (NPF + 1)]);
+          process(tb0 + i * RS_P, R[u]);
+          if (++i == nI) break;
+        }
+      }
+      for (; i < n_tiles; ++i) {
+        Tile T;
+        load(tb0 + i * RS_P, T);
+        process(tb0 + i * RS_P, T);
+      }
+      continue;
+    }
     int tb = tb0;
 #pragma unroll
     for (int d = 0; d < NPF; ++d)
@@ -2616,8 +2661,9 @@ __global__ __launch_bounds__(256, MINW) void k_rolling_scan_tc(
 // kQ - M + 1 .. kQ over W:
 //   out[k] = (SP(kQ) - SP(kQ - M)) / W,   SP(j) = sum of x over (jA g, j g]
 // with SP relative to the unit's first needed boundary jA = ka Q - M.  A
-// wave owns (channel, range of outputs); per tile of 1,024 positions (16
-// consecutive per lane, 4 float4 loads, NPF tiles in flight) every lane sums
+// wave owns (channel, range of outputs); per tile of 1,024 positions (4
+// lane-contiguous 16-B buffer loads per lane, NPF tiles in flight, then a
+// wave-private LDS stage to 16 consecutive positions per lane) every lane sums
 // its 16 samples in float64 and the sum up to the one segment boundary
 // (g >= 16) its positions may hold; one DPP wave scan of the lane sums gives
 // SP at every boundary of the tile, written to a wave-private LDS ring of
@@ -2639,6 +2685,14 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
   return v;
 }
 
+// Loads: lane l, load h reads positions 256 h + 4 l .. + 3 (one 1-KB span
+// per wave-instruction, as the W = S kernel reads) and the tile goes through
+// a wave-private 4-KB LDS stage to the 16-consecutive-positions-per-lane
+// layout; lane l reads its 4 pieces in the rotated order (j + l / 4) & 3,
+// which keeps every ds_read_b128 lane group on distinct banks.  (Round 6,
+// with the unconditional interior loads below: cfg2 S = 250 0.719 -> 0.733
+// of HBM; lanes loading their own 64 B — 64 lines per wave-instruction —
+// measured equal or slower.)
 template <int NPF>
 __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x, int64_t n_ch, int n_t, int64_t s_ch,
                                                      int W, int S, int g, float *__restrict__ y, int64_t ys_ch,
@@ -2652,6 +2706,8 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
   double *spr = rg_ring_all + (size_t)(threadIdx.x >> 6) * 2 * R;   // SP(j) at slot j & ring_mask
   int64_t *cdr = reinterpret_cast<int64_t *>(spr + R);              // packed null counts, same slots
   const int lane = threadIdx.x & 63;
+  // the wave's 4-KB transpose stage, past the 4 waves' rings
+  float *stg = reinterpret_cast<float *>(rg_ring_all + (size_t)8 * R) + (size_t)(threadIdx.x >> 6) * RG_P;
   const int M = W / g, Q = S / g;
   const int n_out = (n_t + S - 1) / S;
   const int n_seg = (n_out + seg_out - 1) / seg_out;
@@ -2683,27 +2739,59 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
     struct Tile {
       float v[RG_E];
     };
-    auto load = [&](int tb, Tile &T) {
-      const int p = tb + RG_E * lane;
-      if (tb >= pos0 && tb + RG_P - 1 <= pend) {
+    // position of element i of a loaded tile (lane-contiguous 16-B pieces)
+    auto lpos = [&](int tb, int i) { return tb + 256 * (i >> 2) + 4 * lane + (i & 3); };
+    // interior tile (every position in [pos0, pend]): unconditional 16-B
+    // buffer loads at the wave-uniform row descriptor, the tile base in
+    // soffset and a fixed per-lane voffset — no per-tile address VGPRs, so
+    // the ring's waits count only the loads before them (with 64-bit
+    // addresses recomputed per tile the register reuse forced vmcnt(0))
+    const __amdgpu_buffer_rsrc_t rrow =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(row), (short)0, n_t * 4, 0x00020000);
+    auto load_i = [&](int tb, Tile &T) {
 #pragma unroll
-        for (int h = 0; h < RG_E / 4; ++h) {
-          const f4v a = *reinterpret_cast<const f4u *>(row + p + 4 * h);
+      for (int h = 0; h < RG_E / 4; ++h) {
+        const uint32_t vo = 4u * (uint32_t)(lpos(0, 4 * h));
+        const auto a = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrow, vo, 4 * tb, 0));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) T.v[4 * h + e] = a[e];
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < RG_E; ++e) T.v[e] = (p + e >= pos0 && p + e <= pend) ? row[p + e] : 0.0f;
+        for (int e = 0; e < 4; ++e) T.v[4 * h + e] = a[e];
       }
     };
-    auto process = [&](int tb, const Tile &T) {
+    // edge tile: positions outside [pos0, pend] read as 0
+    auto load_g = [&](int tb, Tile &T) {
+#pragma unroll
+      for (int i = 0; i < RG_E; ++i) {
+        const int q = lpos(tb, i);
+        T.v[i] = (q >= pos0 && q <= pend) ? row[q] : 0.0f;
+      }
+    };
+    auto process = [&](int tb, const Tile &Tin) {
       const int p = tb + RG_E * lane;
       // this lane's segment boundary (a multiple of g), if any: offset eb
       const int bq = (p + g - 1) / g;
       const int bpos = bq * g;
       const int eb = bpos - p;
       const bool has = eb < RG_E && bpos > jA * g && bpos <= pend;
+      // T.v[i] = position p + off(i) (the rotated pieces)
+      Tile T;
+#pragma unroll
+      for (int h = 0; h < RG_E / 4; ++h)
+        *reinterpret_cast<f4v *>(stg + 256 * h + 4 * lane) =
+            f4v{Tin.v[4 * h], Tin.v[4 * h + 1], Tin.v[4 * h + 2], Tin.v[4 * h + 3]};
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int rot = lane >> 2;
+#pragma unroll
+      for (int j = 0; j < RG_E / 4; ++j) {
+        const f4v b = *reinterpret_cast<const f4v *>(stg + RG_E * lane + 4 * ((j + rot) & 3));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) T.v[4 * j + e] = b[e];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      auto off = [&](int i) { return 4 * (((i >> 2) + rot) & 3) + (i & 3); };
       double tot = 0.0, part = 0.0;
       bool bad = false;
 #pragma unroll
@@ -2713,7 +2801,7 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
         bad |= !f;
         const double d = f ? (double)v : 0.0;
         tot += d;
-        part += e <= eb ? d : 0.0;
+        part += off(e) <= eb ? d : 0.0;
       }
       if (diag & 1) {
         if (tot + part == 1234.5 && !bad) yo[0] = 0.f;
@@ -2728,7 +2816,7 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
         for (int e = 0; e < RG_E; ++e) {
           const int64_t c = null_code(T.v[e]);  // 0 for the masked positions (0.0f)
           ct += c;
-          cp += e <= eb ? c : 0;
+          cp += off(e) <= eb ? c : 0;
         }
         const int64_t ci = wave_incl_scan_i64(ct, lane);
         if (has) cdr[bq & ring_mask] = ccarry + (ci - ct) + cp;
@@ -2756,23 +2844,39 @@ __global__ __launch_bounds__(256) void k_rolling_seg(const float *__restrict__ x
         kn = kend;
       }
     };
-    Tile Tr[NPF + 1];
-    int tb = pos0 & ~3;
+    // edge tile at the head, interior tiles through a ring of NPF + 1 (NPF
+    // tiles' loads in flight behind the one processed; the prefetch index is
+    // clamped to the last interior tile, never a branch), edge tiles at the tail
+    const int tb0 = pos0 & ~3;
+    const int tI0 = tb0 >= pos0 ? tb0 : tb0 + RG_P;
+    const int nI = pend + 1 - tI0 >= RG_P ? (pend + 1 - tI0) / RG_P : 0;
+    if (tb0 < tI0) {
+      Tile T;
+      load_g(tb0, T);
+      process(tb0, T);
+    }
+    if (nI > 0) {
+      Tile Tr[NPF + 1];
 #pragma unroll
-    for (int d = 0; d < NPF; ++d)
-      if (tb + d * RG_P <= pend) load(tb + d * RG_P, Tr[d]);
-    bool fin = false;
-    while (!fin) {
+      for (int d = 0; d < NPF; ++d) load_i(tI0 + min(d, nI - 1) * RG_P, Tr[d]);
+      int i = 0;
+      bool fin = false;
+      while (!fin) {
 #pragma unroll
-      for (int uu = 0; uu <= NPF; ++uu) {
-        if (tb + NPF * RG_P <= pend) load(tb + NPF * RG_P, Tr[(uu + NPF) % (NPF + 1)]);
-        process(tb, Tr[uu]);
-        tb += RG_P;
-        if (tb > pend) {
-          fin = true;
-          break;
+        for (int uu = 0; uu <= NPF; ++uu) {
+          load_i(tI0 + min(i + NPF, nI - 1) * RG_P, Tr[(uu + NPF) % (NPF + 1)]);
+          process(tI0 + i * RG_P, Tr[uu]);
+          if (++i == nI) {
+            fin = true;
+            break;
+          }
         }
       }
+    }
+    for (int tb = tI0 + nI * RG_P; tb <= pend; tb += RG_P) {
+      Tile T;
+      load_g(tb, T);
+      process(tb, T);
     }
   }
 }
@@ -4846,8 +4950,10 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
 #endif
   const unsigned nb = nblk(n_chunks * g.n_ch, threads);
   *scan_used = LFD_SCAN_IN_CHAIN;
-  k_chunk_scan<2, true><<<nb, threads, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
-                                            tp_len, y, ys_ch, ys_t, rg, Y0);
+  // (ring depth: 3 slots = 2 runs in flight; 2 / 4 / 6 measured equal or
+  // slower on cfg3, r06)
+  k_chunk_scan<2, true, false, 4, 3><<<nb, threads, 0, st>>>(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, AG, SR, TP,
+                                                             tp_len, y, ys_ch, ys_t, rg, Y0);
   return hipGetLastError();
 }
 
@@ -5224,7 +5330,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     while (ebatch > 1 && ring_for(ebatch) > 1024) ebatch /= 2;
     const int64_t ring = ring_for(ebatch);
     // (rows of any stride: 4-B aligned 16-B pieces, f4u)
-    bool seg = s_t == 1 && S > 1 && S < W && g >= 16 && ring <= 1024 && n_t < (int64_t)INT32_MAX - 2 * RG_P &&
+    bool seg = s_t == 1 && S > 1 && S < W && g >= 16 && ring <= 1024 && n_t < ((int64_t)1 << 29) &&
                (reinterpret_cast<uintptr_t>(x) & 3) == 0;
     if (const char *v = knob("LFD_ROLL_SEGSUM")) seg = seg && std::atoi(v) != 0;
     if (seg) {
@@ -5242,7 +5348,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
       const int64_t units = n_ch * ((n_out + seg_out - 1) / seg_out);
       int64_t blocks = (units + 3) / 4;
       if (blocks > cap_unit) blocks = cap_unit;
-      const size_t lds = sizeof(double) * 2 * (size_t)ring * 4;
+      const size_t lds = sizeof(double) * 2 * (size_t)ring * 4 + sizeof(float) * RG_P * 4;
       static bool attr = false;
       if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rolling_seg<2>),
@@ -5288,7 +5394,7 @@ hipError_t launch_rolling_mean(const float *x, int64_t n_ch, int64_t n_t,
     // LDS ring for x[t - W] (vector rows, W + 512 <= 4096): A/B knob LFD_ROLL_RING
     int ring = 0;
     while (ring < W + RS_P) ring = ring ? 2 * ring : 1024;
-    bool use_ring = vec && ring <= 4096;
+    bool use_ring = vec && ring <= 4096 && n_t < ((int64_t)1 << 29);
     if (const char *v = knob("LFD_ROLL_RING")) use_ring = use_ring && std::atoi(v) != 0;
     if (use_ring) {
       static bool attr = false;

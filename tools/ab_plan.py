@@ -58,11 +58,11 @@ else:
     xp = torch.empty((max(a.ch + a.alloc_off, a.alloc_ch), n + a.pad), dtype=torch.float32, device=dev)
     bench.synth_fill(xp, a.fs, 77)
     x = xp[a.alloc_off:a.alloc_off + a.ch, :n]
-y = torch.empty((a.ch, plan.n_grid), dtype=torch.float32, device=dev)
+y = torch.empty((a.ch, plan.n_grid), dtype=torch.float64, device=dev)
 wsb = plan.alloc_workspace(dev)
 st = torch.cuda.current_stream(dev)
 R = int(round(a.fs * a.dt))
-alg = a.ch * n * (4.0 + 4.0 / R)
+alg = a.ch * n * (4.0 + 8.0 / R)
 set_timing(True)
 keys = sorted({kv.split("=", 1)[0] for s in specs for kv in s.split()})
 ref = None
