@@ -86,6 +86,32 @@ def test_lfproc_parity(cfg, dc, layout, off_ns):
     assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
+@pytest.mark.parametrize("cfg", [
+    (250.0, 0.2, 40, 6, 1, 24.0),      # one channel
+    (250.0, 0.2, 1000, 6, 5, 24.0),    # process_patch_size beyond the grid: one chunk
+    (250.0, 0.2, 13, 6, 3, 24.0),      # P = 2B + 1 (the smallest the reference terminates on): 1 output per chunk
+    (250.0, 0.2, 40, 6, 3, 6.0),       # a record barely longer than the edge buffers
+    (500.0, 1.0, 20, 2, 65, 40.0),     # 65 channels (one past a 64-channel group), B = 2
+])
+def test_lfproc_parity_degenerate(cfg):
+    """Degenerate LFProc geometries (lf_das.py:252-290): a single channel, a
+    single chunk, one output per chunk, a record barely longer than the edge
+    buffers, a ragged 64-channel group — identical chunk shapes and outputs
+    within the gate of the regular cases."""
+    fs, dt_out, P, B, n_ch, dur = cfg
+    n = int(dur * fs)
+    rng = np.random.default_rng(23)
+    x = (rng.standard_normal((n_ch, n)) + 3.0).astype(np.float32)
+    y, ref, sched = _run(x, fs, dt_out, P, B)
+    assert len(ref) == len(sched) and len(sched) >= 1
+    num = den = 0.0
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        assert r.shape == (n_ch, ob - oa)
+        num += float(np.sum((y[:, oa:ob] - r) ** 2))
+        den += float(np.sum(r ** 2))
+    gates.check(f"lfproc_parity_degenerate {cfg}", (num / den) ** 0.5, gates.MFMA)
+
+
 @pytest.mark.parametrize("phases", [False, True])
 @pytest.mark.parametrize("layout,off_ns,null", [("tc", 0, False), ("tc", 123_457, False), ("cc", 123_457, False),
                                                 ("tc", 0, True)])
