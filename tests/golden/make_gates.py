@@ -13,10 +13,11 @@ import sys
 
 def main(paths):
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gates_measured.json")
-    measured, fresh = {}, {}
+    measured, fresh, sources = {}, {}, []
     if os.path.exists(out):  # checks no log re-measured keep their value
         with open(out) as f:
-            measured = json.load(f)["measured"]
+            old = json.load(f)
+        measured, sources = old["measured"], list(old.get("source", []))
     for p in paths:
         with open(p) as f:
             for line in f:
@@ -24,7 +25,8 @@ def main(paths):
                 fresh[r["tag"]] = max(fresh.get(r["tag"], 0.0), float(r["rel"]))
     measured.update(fresh)
     with open(out, "w") as f:
-        json.dump({"source": [os.path.basename(p) for p in paths], "factor": 10.0,
+        sources += [os.path.basename(p) for p in paths if os.path.basename(p) not in sources]
+        json.dump({"source": sources, "factor": 10.0,
                    "measured": dict(sorted(measured.items()))}, f, indent=1)
         f.write("\n")
     vals = sorted(measured.values())
