@@ -23,6 +23,9 @@ back to its category's constant:
               itself;
 * ``Q32``     vs SciPy on the float64 data the float32 samples were rounded
               from (the input quantisation bounds it);
+* ``ROLL``    rolling means (float32 like numpy's mean of float32 windows,
+              summed in float64): the oracle rounds the same float64 window
+              sums, so most checks measure 0 and are held bit-exact;
 * ``EMU_*``   the NumPy model of the kernels (tests/emulate.py) on CPU.
 
 ``LFD_GATE_LOG=<file>`` appends every measured value (one JSON line per
@@ -42,6 +45,7 @@ PATHS = 1e-8
 STREAM = 1e-8
 DC = 1e-10
 Q32 = 1e-6
+ROLL = 1e-6
 EMU_TAPS = 1e-8
 EMU_REC = 5e-8
 

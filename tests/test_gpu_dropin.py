@@ -149,7 +149,7 @@ def test_rolling_mean_patch(dims):
     d = r.data if dims[0] == "distance" else r.data.T
     assert d.shape == ref.shape and np.array_equal(np.isnan(d), np.isnan(ref))
     m = ~np.isnan(ref)
-    assert _rel(d[m], ref[m]) < 1e-6
+    gates.check(f"rolling_patch {dims}", _rel(d[m], ref[m]), gates.ROLL)
     np.testing.assert_array_equal(r.coords["time"], t[::1000])
     dn = r.dropna("time")
     assert dn.shape[dims.index("time")] == 9

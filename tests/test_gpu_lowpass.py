@@ -287,7 +287,7 @@ def test_rolling_mean_window_step(W, S_):
         assert y.shape == ref.shape
         m = ~np.isnan(ref)
         assert np.array_equal(np.isnan(y), ~m), layout
-        assert _relrms(y[m], ref[m]) < 1e-6, layout
+        gates.check(f"rolling_window_step W={W} S={S_} {layout}", _relrms(y[m], ref[m]), gates.ROLL)
 
 
 @pytest.mark.parametrize("W,S_,n", [
@@ -313,7 +313,7 @@ def test_rolling_seg_output_batches(W, S_, n):
     np.testing.assert_array_equal(np.isnan(y), np.isnan(ref))
     np.testing.assert_array_equal(np.isposinf(y), np.isposinf(ref))
     m = np.isfinite(ref)
-    assert _relrms(y[m], ref[m]) < 1e-6
+    gates.check(f"rolling_seg_batches W={W} S={S_} n={n}", _relrms(y[m], ref[m]), gates.ROLL)
 
 
 @pytest.mark.parametrize("S_", [1, 250, 200])
@@ -341,7 +341,7 @@ def test_rolling_mean_overlapping_nulls(S_):
         assert np.array_equal(np.isposinf(y), np.isposinf(ref)), layout
         assert np.array_equal(np.isneginf(y), np.isneginf(ref)), layout
         m = np.isfinite(ref)
-        assert _relrms(y[m], ref[m]) < 1e-6, layout
+        gates.check(f"rolling_overlapping_nulls S={S_} {layout}", _relrms(y[m], ref[m]), gates.ROLL)
 
 
 def test_rolling_mean_parity():
@@ -357,7 +357,7 @@ def test_rolling_mean_parity():
             assert y.shape == ref.shape
             m = ~np.isnan(ref)
             assert np.array_equal(np.isnan(y), ~m)
-            assert _relrms(y[m], ref[m]) < 1e-6
+            gates.check(f"rolling_parity {(n_ch, n, W, S_)} {layout}", _relrms(y[m], ref[m]), gates.ROLL)
 
 
 def test_rolling_mean_nulls():
@@ -381,7 +381,7 @@ def test_rolling_mean_nulls():
         assert np.array_equal(np.isposinf(y), np.isposinf(ref))
         assert np.array_equal(np.isneginf(y), np.isneginf(ref))
         m = np.isfinite(ref)
-        assert _relrms(y[m], ref[m]) < 1e-6
+        gates.check(f"rolling_nulls {layout}", _relrms(y[m], ref[m]), gates.ROLL)
 
 
 def test_full_rate_filtfilt_parity():

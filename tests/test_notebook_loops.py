@@ -291,4 +291,4 @@ def test_rolling_mean_notebook(tmp_path, realtime):
     tr = np.concatenate(ts)
     np.testing.assert_array_equal(merged.coords["time"].astype(np.int64), tr)
     assert merged.shape == (len(tr), CH_END - CH_START + 1)
-    assert _rel(merged.data.T, yr) < 1e-6
+    gates.check(f"rolling_notebook realtime={realtime}", _rel(merged.data.T, yr), gates.ROLL)
