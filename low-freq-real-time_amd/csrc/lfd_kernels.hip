@@ -4887,13 +4887,13 @@ hipError_t launch_chunk_scan_runs(const float *x, int64_t s_ch, int64_t s_t, con
   }
 #endif
   // the fused one-launch segmented scan (option scan_defer = 4; by default
-  // when its (chunk, 16-channel) workgroups fit the chip at once, <= 3 per CU:
-  // latency-bound narrow shards — 1,250 channels x 7 chunks (an 8-GPU share
-  // of cfg3): 0.109 -> 0.087 ms; from 2,500 channels (two rounds of
-  // workgroups) the two-launch deferred scan is as fast or faster,
-  // profiles/r05_scan_fused.txt)
+  // when its (chunk, 16-channel) workgroups number <= 6 per CU: latency-bound
+  // narrow shards — 1,250 channels x 7 chunks (an 8-GPU share of cfg3):
+  // 0.109 -> 0.087 ms (profiles/r05_scan_fused.txt); 2,500 channels (a 4-GPU
+  // share) 0.1445 -> 0.1315 ms after the round-6 ring changes; 5,000 equal
+  // (profiles/r06_scan_variants.txt)
   const int64_t o_scan = option(LFD_OPT_SCAN_DEFER);
-  const bool fused_fits = n_chunks * ((g.n_ch + 15) / 16) <= 3 * (int64_t)cu_count();
+  const bool fused_fits = n_chunks * ((g.n_ch + 15) / 16) <= 6 * (int64_t)cu_count();
   if (seg_fu && nw_fu == FU_SEG && TR && (o_scan == 4 || (o_scan == 0 && fused_fits))) {
     *scan_used = LFD_SCAN_FUSED;
     return launch_scan_fused(x, s_ch, s_t, g, padlen, sc, cg, n_chunks, rg, seg_fu, Y0, AG, SR, TR, TP, y, ys_ch,
