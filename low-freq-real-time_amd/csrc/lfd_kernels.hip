@@ -1083,9 +1083,19 @@ __device__ uint64_t g_fr_times[16384 * 8];
       if (threadIdx.x == 0) g_fr_times[(size_t)blockIdx.x * 8 + (i)] = t_;                            \
     }                                                                                                 \
   } while (0)
+// LFD_FRS_TIMES (diag): phase stamps of k_fullrate_scan_seg's first 256
+// workgroups (thread 0, after each workgroup barrier)
+__device__ uint64_t g_frs_times[256 * 8];
+#define FRS_STAMP(i)                                                                                  \
+  do {                                                                                                \
+    if (blockIdx.x < 256 && threadIdx.x == 0) g_frs_times[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define FR_STAMP(i) \
   do {              \
+  } while (0)
+#define FRS_STAMP(i) \
+  do {               \
   } while (0)
 #endif
 #ifndef FRS_Q
@@ -1833,6 +1843,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
   __shared__ double slotL[CW][N], slotR[CW][N];
   extern __shared__ double agg[];  // [G][CW][N]
   const int tid = threadIdx.x, col = tid % CW, seg = tid / CW;
+  FRS_STAMP(0);
   for (int i = tid; i < N * N; i += blockDim.x) {
     const int r = i / N, c = i % N;
     cPB[i] = fc->PhiP[4][r * MAX_N + c];
@@ -1862,6 +1873,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     }
   }
   __syncthreads();
+  FRS_STAMP(1);
   const int64_t ch = (int64_t)blockIdx.x * CW + col;
   const bool active = ch < n_ch;
   const int64_t m0 = (int64_t)seg * sg.seglen;
@@ -1883,11 +1895,13 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     }
   };
   double *ag = agg + ((size_t)seg * CW + col) * N;
-  // Every walk loads QF (forward) / QR (reverse) blocks before applying them,
-  // at clamped indices (unconditional loads: a conditional load made the
-  // compiler wait for everything in flight), so the chain waits one memory
-  // latency per batch instead of per block.
-  constexpr int QF = 4, QR = 2;
+  // Every walk runs through a ring of QF (forward) / QR (reverse) block
+  // slots loaded at clamped indices (unconditional loads: a conditional load
+  // made the compiler wait for everything in flight); a slot is applied in
+  // place and refilled with the block QF / QR ahead, so the chain waits one
+  // memory latency per walk rather than per batch (round 6; the batched form
+  // waited once per QF / QR blocks).
+  constexpr int QF = 4, QR = 4;
   auto fload = [&](int64_t m, int c0, double (&f)[N]) {
 #pragma unroll
     for (int n = 0; n < N; ++n) f[n] = Fc[(m * 2 * N + c0 + n) * 16];
@@ -1897,17 +1911,21 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
 #pragma unroll
   for (int n = 0; n < N; ++n) a[n] = 0.0;
   if (live) {
+    // ring of QF slots: slot u is applied in place, then refilled with the
+    // block QF ahead (clamped), so QF - 1 blocks' loads stay in flight
+    double fq[QF][N];
+#pragma unroll
+    for (int u = 0; u < QF; ++u) fload(m0 + u < m1 ? m0 + u : m1 - 1, 0, fq[u]);
     for (int64_t mb = m0; mb < m1; mb += QF) {
-      double fq[QF][N];
 #pragma unroll
-      for (int u = 0; u < QF; ++u) fload(mb + u < m1 ? mb + u : m1 - 1, 0, fq[u]);
+      for (int u = 0; u < QF; ++u) {
+        const int64_t m = mb + u;
+        if (m >= m1) break;
+        mv(cPB, a, fq[u], true);
 #pragma unroll
-      for (int u = 0; u < QF; ++u)
-        if (mb + u < m1) {
-          mv(cPB, a, fq[u], true);
-#pragma unroll
-          for (int n = 0; n < N; ++n) a[n] = fq[u][n];
-        }
+        for (int n = 0; n < N; ++n) a[n] = fq[u][n];
+        fload(m + QF < m1 ? m + QF : m1 - 1, 0, fq[u]);
+      }
     }
   }
 #pragma unroll
@@ -1927,6 +1945,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     for (int n = 0; n < N; ++n) slotL[col][n] = z[n];
   }
   __syncthreads();
+  FRS_STAMP(2);
   // ---- entering state of the segment
   double z[N];
 #pragma unroll
@@ -1942,20 +1961,20 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
   }
   // ---- C: true forward states
   if (live) {
-    for (int64_t mb = m0; mb < m1; mb += QF) {
-      double fq[QF][N];
+    double fq[QF][N];
 #pragma unroll
-      for (int u = 0; u < QF; ++u) fload(mb + u < m1 ? mb + u : m1 - 1, 0, fq[u]);
+    for (int u = 0; u < QF; ++u) fload(m0 + u < m1 ? m0 + u : m1 - 1, 0, fq[u]);
+    for (int64_t mb = m0; mb < m1; mb += QF) {
 #pragma unroll
       for (int u = 0; u < QF; ++u) {
         const int64_t m = mb + u;
-        if (m < m1) {
+        if (m >= m1) break;
 #pragma unroll
-          for (int n = 0; n < N; ++n) SFm[(m * N + n) * n_ch + ch] = z[n];
-          mv(cPB, z, fq[u], true);
+        for (int n = 0; n < N; ++n) SFm[(m * N + n) * n_ch + ch] = z[n];
+        mv(cPB, z, fq[u], true);
 #pragma unroll
-          for (int n = 0; n < N; ++n) z[n] = fq[u][n];
-        }
+        for (int n = 0; n < N; ++n) z[n] = fq[u][n];
+        fload(m + QF < m1 ? m + QF : m1 - 1, 0, fq[u]);
       }
     }
     if (seg == sg.Gu - 1 && xl > 0) {
@@ -2025,6 +2044,7 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
     }
   }
   __syncthreads();
+  FRS_STAMP(3);
   // ---- A': reverse aggregate of the segment from zero T (true S_f coupling)
   auto rload = [&](int64_t m, double (&f)[N], double (&sf)[N]) {
     fload(m, N, f);
@@ -2034,23 +2054,26 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
 #pragma unroll
   for (int n = 0; n < N; ++n) a[n] = 0.0;
   if (live) {
+    double fq[QR][N], sq[QR][N];
+#pragma unroll
+    for (int u = 0; u < QR; ++u) rload(m1 - 1 - u >= m0 ? m1 - 1 - u : m0, fq[u], sq[u]);
     for (int64_t mb = m1 - 1; mb >= m0; mb -= QR) {
-      double fq[QR][N], sq[QR][N];
 #pragma unroll
-      for (int u = 0; u < QR; ++u) rload(mb - u >= m0 ? mb - u : m0, fq[u], sq[u]);
+      for (int u = 0; u < QR; ++u) {
+        const int64_t m = mb - u;
+        if (m < m0) break;
+        mv(cPB, a, fq[u], true);
+        mv(cMB, sq[u], fq[u], false);
 #pragma unroll
-      for (int u = 0; u < QR; ++u)
-        if (mb - u >= m0) {
-          mv(cPB, a, fq[u], true);
-          mv(cMB, sq[u], fq[u], false);
-#pragma unroll
-          for (int n = 0; n < N; ++n) a[n] = fq[u][n];
-        }
+        for (int n = 0; n < N; ++n) a[n] = fq[u][n];
+        rload(m - QR >= m0 ? m - QR : m0, fq[u], sq[u]);
+      }
     }
   }
 #pragma unroll
   for (int n = 0; n < N; ++n) ag[n] = a[n];
   __syncthreads();
+  FRS_STAMP(4);
   // ---- T entering the segment from its right end
 #pragma unroll
   for (int n = 0; n < N; ++n) z[n] = slotR[col][n];
@@ -2065,25 +2088,26 @@ __global__ __launch_bounds__(512) void k_fullrate_scan_seg(
   }
   // ---- C': true reverse states
   if (live) {
-    for (int64_t mb = m1 - 1; mb >= m0; mb -= QR) {
-      double fq[QR][N], sq[QR][N];
+    double fq[QR][N], sq[QR][N];
 #pragma unroll
-      for (int u = 0; u < QR; ++u) rload(mb - u >= m0 ? mb - u : m0, fq[u], sq[u]);
+    for (int u = 0; u < QR; ++u) rload(m1 - 1 - u >= m0 ? m1 - 1 - u : m0, fq[u], sq[u]);
+    for (int64_t mb = m1 - 1; mb >= m0; mb -= QR) {
 #pragma unroll
       for (int u = 0; u < QR; ++u) {
         const int64_t m = mb - u;
-        if (m >= m0) {
-          mv(cPB, z, fq[u], true);
-          mv(cMB, sq[u], fq[u], false);
+        if (m < m0) break;
+        mv(cPB, z, fq[u], true);
+        mv(cMB, sq[u], fq[u], false);
 #pragma unroll
-          for (int n = 0; n < N; ++n) {
-            z[n] = fq[u][n];
-            STm[(m * N + n) * n_ch + ch] = z[n];
-          }
+        for (int n = 0; n < N; ++n) {
+          z[n] = fq[u][n];
+          STm[(m * N + n) * n_ch + ch] = z[n];
         }
+        rload(m - QR >= m0 ? m - QR : m0, fq[u], sq[u]);
       }
     }
   }
+  FRS_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -5255,6 +5279,24 @@ hipError_t launch_fullrate_scan_seg(int n_sec, const float *x, int64_t s_ch, int
     default: return hipErrorInvalidValue;
   }
 #undef LFD_FRSS
+#ifdef LFD_DIAG
+  if (knob_flag("LFD_FRS_TIMES")) {
+    // phase durations (us, mean over the first workgroups): 0-1 LDS windows,
+    // 1-2 forward aggregates + left edge, 2-3 forward states + tail, 3-4
+    // reverse aggregates, 4-5 entering T + reverse states
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    const size_t nw = (size_t)std::min<int64_t>(g, 256);
+    std::vector<uint64_t> t(nw * 8);
+    e = hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_frs_times), t.size() * sizeof(uint64_t));
+    if (e != hipSuccess) return e;
+    double d[5] = {0, 0, 0, 0, 0};
+    for (size_t b = 0; b < nw; ++b)
+      for (int i = 0; i < 5; ++i) d[i] += 0.01 * (double)(t[b * 8 + i + 1] - t[b * 8 + i]);
+    fprintf(stderr, "k_fullrate_scan_seg us/group: windows %.2f fagg %.2f fstates+tail %.2f ragg %.2f rstates %.2f (%zu groups)\n",
+            d[0] / nw, d[1] / nw, d[2] / nw, d[3] / nw, d[4] / nw, nw);
+  }
+#endif
   return hipGetLastError();
 }
 
