@@ -112,6 +112,51 @@ def test_lfproc_parity_degenerate(cfg):
     gates.check(f"lfproc_parity_degenerate {cfg}", (num / den) ** 0.5, gates.MFMA)
 
 
+def _random_geometry(seed):
+    """A seeded random LFProc geometry: sampling rate, output interval
+    (R = fs dt_out >= 10 samples per output), edge buffer, patch size, grid
+    length, channel count, start offset and storage layout."""
+    rng = np.random.default_rng(1000 + seed)
+    while True:
+        fs = float(rng.choice([100.0, 200.0, 250.0, 500.0, 1000.0, 2000.0]))
+        dt_out = float(rng.choice([0.2, 0.5, 1.0, 2.0, 5.0, 10.0]))
+        if abs(fs * dt_out - round(fs * dt_out)) < 1e-9 and fs * dt_out >= 10:
+            break
+    B = int(rng.integers(1, 9))
+    P = int(rng.integers(2 * B + 1, 2 * B + 61))
+    n_grid = int(rng.integers(P, 4 * P + 1))
+    n = int(n_grid * dt_out * fs) + int(rng.integers(1, int(fs) + 2))
+    n_ch = int(rng.integers(1, 81))
+    while n_ch * n > 30_000_000 and n_ch > 1:
+        n_ch //= 2
+    dt_ns = int(round(1e9 / fs))
+    off_ns = 0 if rng.random() < 0.4 else int(rng.integers(1, dt_ns))
+    layout = "tc" if rng.random() < 0.7 else "cc"
+    return fs, dt_out, P, B, n_ch, n, off_ns, layout
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_lfproc_parity_random_geometry(seed):
+    """Twelve seeded random LFProc geometries (rates 100 Hz - 2 kHz, output
+    intervals 0.2 - 10 s, edge buffers 1 - 8, patch sizes 2B + 1 .. 2B + 60,
+    1 - 80 channels, on- and off-sample starts, both layouts) against the
+    oracle: identical chunk shapes, NaN-free produced outputs, and relRMS
+    gated per geometry at 10x its measured value."""
+    fs, dt_out, P, B, n_ch, n, off_ns, layout = _random_geometry(seed)
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / fs
+    x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.5 / dt_out * 0.3 * t) + 2.0).astype(np.float32)
+    y, ref, sched = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
+    num = den = 0.0
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        assert r.shape == (n_ch, ob - oa)
+        assert not np.isnan(y[:, oa:ob]).any()
+        num += float(np.sum((y[:, oa:ob] - r) ** 2))
+        den += float(np.sum(r ** 2))
+    gates.check(f"lfproc_parity_random seed={seed} {(fs, dt_out, P, B, n_ch, n, off_ns, layout)}",
+                (num / den) ** 0.5, gates.MFMA)
+
+
 @pytest.mark.parametrize("phases", [False, True])
 @pytest.mark.parametrize("layout,off_ns,null", [("tc", 0, False), ("tc", 123_457, False), ("cc", 123_457, False),
                                                 ("tc", 0, True)])
