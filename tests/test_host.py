@@ -99,6 +99,32 @@ def test_schedule_matches_oracle(L, P, B):
         assert b0 == a1
 
 
+def test_schedule_property_random():
+    """Property check over 300 seeded random (L, P, B) with P > 2B: the Python
+    and the native (C-ABI) chunk schedules equal the oracle's restatement of
+    lf_das.py:258-290, and the output ranges tile [B, ...) contiguously."""
+    from lfdas.stream import lfproc_schedule as native_schedule
+    rng = np.random.default_rng(77)
+    for _ in range(300):
+        B = int(rng.integers(0, 12))
+        P = int(rng.integers(2 * B + 1, 2 * B + 80))
+        L = int(rng.integers(2, 6 * P + 10))
+        try:
+            want = oracle.lfproc_schedule(L, P, B)
+        except ValueError:  # P clipped to L - 1 <= 2B: the reference never ends; all three refuse
+            with pytest.raises(ValueError):
+                S.lfproc_chunks(L, P, B)
+            with pytest.raises(Exception):
+                native_schedule(L, P, B)
+            continue
+        assert S.lfproc_chunks(L, P, B) == want, (L, P, B)
+        got = [tuple(int(v) for v in row) for row in native_schedule(L, P, B)]
+        assert got == [tuple(w) for w in want], (L, P, B)
+        outs = [(a, b) for _, _, a, b in want]
+        for (a0, b0), (a1, b1) in zip(outs, outs[1:]):
+            assert b0 == a1
+
+
 def test_schedule_rejects_non_advancing():
     with pytest.raises(ValueError):
         S.lfproc_chunks(100, 10, 5)
