@@ -335,6 +335,43 @@ def test_rolling_mean_window_step(W, S_):
         gates.check(f"rolling_window_step W={W} S={S_} {layout}", _relrms(y[m], ref[m]), gates.ROLL)
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_rolling_mean_random_geometry(seed):
+    """Twelve seeded random rolling-mean geometries (window 1 - 5,000, step 1 -
+    2 x window, 1 - 40 channels, contiguous / strided / 4-B offset rows, a
+    NaN and an inf in some) against the oracle: identical null footprint, and
+    relRMS gated per geometry at 10x its measured value (most are 0)."""
+    import torch
+    from lfdas.plan import rolling_mean_device
+    rng = np.random.default_rng(2000 + seed)
+    W = int(rng.integers(1, 5001))
+    S_ = int(rng.integers(1, 2 * W + 1)) if rng.random() < 0.5 else int(rng.choice([1, max(1, W // 4), W]))
+    n = int(rng.integers(W, 40 * W + 2)) if W > 100 else int(rng.integers(W, 4000 + W))
+    n_ch = int(rng.integers(1, 41))
+    while n_ch * n > 20_000_000 and n_ch > 1:
+        n_ch //= 2
+    x = (rng.standard_normal((n_ch, n)) + 1.5).astype(np.float32)
+    if rng.random() < 0.5:
+        x[int(rng.integers(0, n_ch)), int(rng.integers(0, n))] = np.nan
+        x[int(rng.integers(0, n_ch)), int(rng.integers(0, n))] = np.inf
+    layout = str(rng.choice(["tc", "cc", "tc_unaligned"]))
+    if layout == "tc":
+        xd = torch.from_numpy(x).cuda()
+    elif layout == "cc":
+        xd = torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()
+    else:
+        full = torch.from_numpy(np.concatenate([np.zeros((n_ch, 1), np.float32), x], 1)).cuda()
+        xd = full[:, 1:]
+    ref = oracle.rolling_mean(x, W, S_)
+    y = rolling_mean_device(xd, W, S_).cpu().numpy()
+    assert y.shape == ref.shape
+    np.testing.assert_array_equal(np.isnan(y), np.isnan(ref))
+    np.testing.assert_array_equal(np.isposinf(y), np.isposinf(ref))
+    m = np.isfinite(ref)
+    gates.check(f"rolling_random seed={seed} {(W, S_, n, n_ch, layout)}",
+                _relrms(y[m], ref[m]) if m.any() else 0.0, gates.ROLL)
+
+
 @pytest.mark.parametrize("W,S_,n", [
     (320, 16, 12_345),     # 80 outputs per unit: a batch of 64 leaves mid-unit, the rest at its end
     (2032, 1008, 50_000),  # Q = 63: the prefix ring only fits batches of 8 (9 outputs per unit)
