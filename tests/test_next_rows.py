@@ -268,3 +268,70 @@ def test_decimate_fir_device_nulls_and_ragged(q, aligned):
     y2 = fir_decimate_device(torch.from_numpy(xf).cuda(), h, q, delay).cpu().numpy()
     assert load().lfd_fir_decimate_last_kernel() == 1
     assert _rel(y2, fir_decimate_mfma_model(xf.astype(np.float64), h, q, delay)) < 1e-12
+
+
+def _layout(x, kind):
+    import torch
+    if kind == "row":
+        return torch.from_numpy(x).cuda()
+    if kind == "col":
+        return torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()
+    full = torch.from_numpy(np.concatenate([np.zeros((x.shape[0], 1), np.float32), x], 1)).cuda()
+    return full[:, 1:]  # rows 4 B past 16-B alignment
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(10))
+def test_fullrate_random_geometry(seed):
+    """Ten seeded random full-rate zero-phase filters (Patch.pass_filter(...)
+    .data: low / high / band-pass, 2 - 8 corners, rates 50 Hz - 2 kHz,
+    records from just past padlen to 120,000 samples, SciPy's or a random
+    padlen, three row layouts) against the oracle's sosfiltfilt, gated per
+    geometry at 10x its measured relRMS."""
+    from lfdas.plan import sosfiltfilt_device
+    rng = np.random.default_rng(3000 + seed)
+    fs = float(rng.choice([50.0, 100.0, 250.0, 500.0, 1000.0, 2000.0]))
+    kind = str(rng.choice(["low", "high", "band"]))
+    corners = int(rng.choice([2, 4])) if kind == "band" else int(rng.choice([2, 4, 6, 8]))
+    f1 = float(fs * rng.uniform(0.002, 0.2))
+    f2 = float(min(fs * 0.45, f1 * rng.uniform(1.5, 8.0)))
+    lo, hi = {"low": (None, f1), "high": (f1, None), "band": (f1, f2)}[kind]
+    sos = oracle.dascore_pass_filter_sos(fs, lo, hi, corners)
+    pad_ref = oracle.sosfiltfilt_ref_padlen(sos)
+    padlen = None if rng.random() < 0.6 else int(rng.integers(0, 3 * pad_ref + 1))
+    pl = pad_ref if padlen is None else padlen
+    n_t = int(rng.integers(pl + 2, pl + 200)) if rng.random() < 0.3 else int(rng.integers(2_000, 120_001))
+    n_ch = int(rng.integers(1, 17))
+    layout = str(rng.choice(["row", "col", "row_unaligned"]))
+    x = (rng.standard_normal((n_ch, n_t)) + 2.0).astype(np.float32)
+    y = sosfiltfilt_device(_layout(x, layout), sos, -1 if padlen is None else padlen).cpu().numpy()
+    ref = oracle.sosfiltfilt(sos, x, padlen=padlen)
+    assert y.shape == ref.shape and np.isfinite(y).all()
+    gates.check(f"fullrate_random seed={seed} {(fs, kind, corners, lo, hi, padlen, n_t, n_ch, layout)}",
+                _rel(y, ref), gates.PATHS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(10))
+def test_fir_decimate_random_geometry(seed):
+    """Ten seeded random FIR decimations (decimate(q, ftype='fir'): q 2 - 12,
+    records of 3 - 200,000 samples, 1 - 16 channels, three row layouts, a
+    NaN in some) against the oracle on the same float32 samples: identical
+    NaN footprint, relRMS gated per geometry at 10x its measured value."""
+    from lfdas.plan import fir_decimate_device
+    from lfdas.proc import fir_decimate_design
+    rng = np.random.default_rng(4000 + seed)
+    q = int(rng.integers(2, 13))
+    n_t = int(rng.integers(3, 400)) if rng.random() < 0.3 else int(rng.integers(1_000, 200_001))
+    n_ch = int(rng.integers(1, 17))
+    layout = str(rng.choice(["row", "col", "row_unaligned"]))
+    x = (rng.standard_normal((n_ch, n_t)) + 1.0).astype(np.float32)
+    if rng.random() < 0.4:
+        x[int(rng.integers(0, n_ch)), int(rng.integers(0, n_t))] = np.nan
+    taps, delay = fir_decimate_design(q)
+    y = fir_decimate_device(_layout(x, layout), taps, q, delay).cpu().numpy()
+    ref = oracle.decimate_fir(x.astype(np.float64), q)
+    assert y.shape == ref.shape
+    np.testing.assert_array_equal(np.isnan(y), np.isnan(ref))
+    m = np.isfinite(ref)
+    gates.check(f"fir_random seed={seed} {(q, n_t, n_ch, layout)}", _rel(y[m], ref[m]), gates.PATHS)
