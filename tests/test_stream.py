@@ -246,3 +246,49 @@ def test_3khz_edge_stream_reuses_lattice_plans():
     assert runs >= n_push - 2
     assert created + hits >= runs
     assert created <= runs // 3, (created, hits, runs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_continuous_stream_random_pushes(seed):
+    """Eight seeded random out-of-core streams (rates 100 Hz - 1 kHz, output
+    intervals 0.5 - 5 s, edge buffers 1 - 7, patch sizes 2B + 2 .. 2B + 40,
+    pushes of random lengths, an arena a few pushes deep so it compacts)
+    against the oracle's process_time_range over the whole range: identical
+    output times, relRMS gated per stream at 10x its measured value."""
+    rng = np.random.default_rng(5000 + seed)
+    while True:
+        fs = float(rng.choice([100.0, 200.0, 250.0, 500.0, 1000.0]))
+        dt_out = float(rng.choice([0.5, 1.0, 2.0, 5.0]))
+        if fs * dt_out >= 20:
+            break
+    B = int(rng.integers(1, 8))
+    P = int(rng.integers(2 * B + 2, 2 * B + 41))
+    n_ch = int(rng.integers(1, 40))
+    n_grid = int(rng.integers(2 * P, 6 * P + 1))
+    n = int(n_grid * dt_out * fs)
+    dt_ns = int(round(1e9 / fs))
+    x = (rng.standard_normal((n_ch, n)) + 10.0).astype(np.float32)
+    t2 = T0 + (n - 1) * dt_ns
+    ref = oracle.lfproc_process(x, T0, dt_ns, T0, t2, dt_out, P, B)
+    r = np.concatenate([d for _, d in ref], axis=1)
+    rt = np.concatenate([t for t, _ in ref])
+    mean_push = max(8, int(n / rng.integers(4, 30)))
+    s = ST.LowpassStream(n_ch, dt_ns, dt_out, P, B, mode="continuous", t_start=T0, t_end=t2,
+                         capacity=int(3 * mean_push + (2 * B + P + 2) * dt_out * fs))
+    ys, ts = [], []
+    k0 = 0
+    while k0 < n:
+        k1 = min(n, k0 + int(rng.integers(max(1, mean_push // 3), 2 * mean_push)))
+        o = s.push(np.ascontiguousarray(x[:, k0:k1]), T0 + k0 * dt_ns)
+        ys.append(s.fetch())
+        ts.append(o.times_ns)
+        k0 = k1
+    o = s.flush()
+    ys.append(s.fetch())
+    ts.append(o.times_ns)
+    s.close()
+    y = np.concatenate(ys, axis=1)
+    np.testing.assert_array_equal(np.concatenate(ts), rt)
+    gates.check(f"continuous_random seed={seed} {(fs, dt_out, P, B, n_ch, n, mean_push)}", _relrms(y, r),
+                gates.STREAM)
