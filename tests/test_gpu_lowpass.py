@@ -194,6 +194,39 @@ def test_lfproc_parity_lattice_grid(layout, off_ns, null, phases):
     assert _run.last_kernel == ("mfma_runs" if layout == "tc" else "mfma_runs_tm")
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_lfproc_parity_lattice_random(seed):
+    """Six seeded random drifting grids: rates whose integer-ns sample
+    interval does not divide the output interval (750 Hz - 6 kHz), 300 -
+    1,400 s, random start offset, edge buffer, patch size and layout, the
+    one-pass or the per-phase lattice plan — against the oracle, gated per
+    geometry at 10x its measured value."""
+    rng = np.random.default_rng(6000 + seed)
+    fs = float(rng.choice([750.0, 1200.0, 1500.0, 2400.0, 3000.0, 6000.0]))
+    dt_out = float(rng.choice([1.0, 2.0]))
+    B = int(rng.integers(2, 8))
+    P = int(rng.integers(2 * B + 5, 2 * B + 120))
+    dur = float(rng.integers(300, 1401))
+    n_ch = int(rng.integers(1, 9))
+    n = int(dur * fs)
+    dt_ns = int(round(1e9 / fs))
+    off_ns = int(rng.integers(0, dt_ns))
+    layout = "tc" if rng.random() < 0.7 else "cc"
+    phases = bool(rng.random() < 0.3)
+    t = np.arange(n) / fs
+    x = (rng.standard_normal((n_ch, n)) + np.sin(2 * np.pi * 0.02 * t) + 20.0).astype(np.float32)
+    with kernel_options(lattice_phases=1 if phases else 0):
+        y, ref, sched = _run(x, fs, dt_out, P, B, layout, off_ns=off_ns)
+    num = den = 0.0
+    for (tt, r), (a, b, oa, ob) in zip(ref, sched):
+        assert r.shape == (n_ch, ob - oa)
+        assert not np.isnan(y[:, oa:ob]).any()
+        num += float(np.sum((y[:, oa:ob] - r) ** 2))
+        den += float(np.sum(r ** 2))
+    gates.check(f"lattice_random seed={seed} {(fs, dt_out, P, B, n_ch, n, off_ns, layout, phases)} {_run.lattice}",
+                (num / den) ** 0.5, gates.MFMA)
+
+
 def _plan_cfg(fs, dt_out, P, B, n_ch, n):
     from lfdas.plan import LowpassPlan
     dt_ns = int(round(1e9 / fs))
