@@ -252,3 +252,57 @@ def test_sharded_driver_prints_reference_messages(tmp_path, capsys):
     lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("Processing patch")]
     assert lines == ["Processing patch  1", "Processing patch  2", "Processing patch  3",
                      "Processing patch 4 (Last portion of data)"]
+
+
+def _random_world_worker(rank, world, port, n_ch, seed, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import lfdas.dc as dc
+    import synth
+    from lfdas.shard import process_time_range_sharded, shard_spool
+    x = synth.noise_sine(n_ch, 6000, 250.0, seed=seed)
+    t = (np.datetime64(synth.T0_NS, "ns") + np.arange(6000) * np.timedelta64(4_000_000, "ns"))
+    sp = dc.spool([dc.Patch(data=x, coords={"distance": np.arange(float(n_ch)), "time": t},
+                            dims=("distance", "time"))])
+    sub, (c0, c1) = shard_spool(sp, world, rank)
+    outs = process_time_range_sharded(sp, T1, T2, PARAMS, run_shard=_oracle_shard, verbose=False)
+    out_q.put((rank, (c0, c1), sub is None, [np.asarray(o.data) for o in outs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_random_worlds_including_empty_shards():
+    """Seeded random (world, channel count) pairs, including more ranks than
+    channels (ranks with an empty shard): every rank gets the full-width
+    outputs of every chunk from the all-gather, equal to one process over
+    the whole spool."""
+    import lfdas.dc as dc
+    import synth
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join([here, os.path.dirname(here),
+                                                os.path.join(os.path.dirname(here), "low-freq-real-time_amd"),
+                                                os.environ.get("PYTHONPATH", "")])
+    ctx = mp.get_context("spawn")
+    for world, n_ch, seed in [(3, 2, 1), (4, 7, 2), (2, 13, 3)]:
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_random_world_worker, args=(r, world, port, n_ch, seed, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        got = [q.get(timeout=180) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        x = synth.noise_sine(n_ch, 6000, 250.0, seed=seed)
+        t = (np.datetime64(synth.T0_NS, "ns") + np.arange(6000) * np.timedelta64(4_000_000, "ns"))
+        sp = dc.spool([dc.Patch(data=x, coords={"distance": np.arange(float(n_ch)), "time": t},
+                                dims=("distance", "time"))])
+        ref = _oracle_shard(sp, T1, T2, PARAMS)
+        empties = sum(1 for _, _, e, _ in got if e)
+        assert empties == max(0, world - -(-n_ch // -(-n_ch // world)))
+        for rank, (c0, c1), empty, outs in got:
+            assert len(outs) == len(ref)
+            for d, r in zip(outs, ref):
+                assert d.shape == r.data.shape
+                np.testing.assert_allclose(d, r.data, rtol=0, atol=1e-12)
